@@ -1,0 +1,259 @@
+#!/usr/bin/env python
+"""Benchmark: BB solver iterations/sec on the 1M-route block-LSQ problem (C3) +
+proj_simplex HBM GB/s (C2), on MI355X.  One JSON line on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A step = one full projected-BB iteration (python/BB.py:17-41 semantics, fused
+K2 -> K3 -> K1 on the device) over the whole problem, inputs resident in HBM.
+N = 1: config C3 (1M routes, 50k blocks, 100k links, 16M nnz, fp64).
+N > 1 (torchrun, one rank per GPU): weak scaling -- every rank owns a C3-sized
+column shard (1M routes) of an N x 1M-route problem whose m = N x 100k rows
+are shared; per iteration one RCCL all-reduce of the residual r (8 m bytes)
+and one of the four BB sums.  value = N x (iterations/s of the whole job),
+i.e. 1M-route-equivalent BB iterations per second.
+
+Early exits are disabled for timing: exactly K iterations run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault('OPENBLAS_NUM_THREADS', '1')   # CPU baseline = 1 thread, like the reference
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = 'BB solver iterations/sec (1M-route block-LSQ) + proj_simplex HBM GB/s'
+HBM_PEAK = 8.0e12   # MI355X_MICROARCH.md chip table (spec)
+
+
+def kernel_bytes(m, n, nz, p, nnz_a, nnz_at):
+    """Algorithmic HBM bytes per launch."""
+    return {
+        'K1_spmv_A': 12 * nnz_a + 8 * (m + 1) + 8 * n + 16 * m,
+        'K2_spmvT_Nt_dots': 12 * nnz_at + 8 * (n + 1) + 8 * m + 4 * n + 32 * nz,
+        'K3_pava_clip_z2x': 24 * nz + 8 * n + 16 * p,
+    }
+
+
+def survey_iter_bytes(m, n, nz, nnz):
+    """B_iter = 24 nnz + 4 (m+n+2) + 8 (3m + n + 5 n_z)."""
+    return 24 * nnz + 4 * (m + n + 2) + 8 * (3 * m + n + 5 * nz)
+
+
+def cpu_baseline_bb(A, b, sizes, budget_s=12.0):
+    """The oracle's restatement of BB.solve over main.solve_in_z's closures
+    (SciPy csr_matvec + the C PAVA restatement), 1 thread, bounded sample."""
+    from oracle import oracle as orc
+    P = orc.solve_in_z_parts(A, b, sizes)
+    z = P['z0']
+    z_prev = z + 1
+    g_prev = P['nabla_f'](z_prev)
+    t0 = time.perf_counter()
+    it = 0
+    while True:
+        g = P['nabla_f'](z)
+        dg = g - g_prev
+        _ = sum(dg)                      # BB.py:22 (22 % of the reference's time)
+        dx = z - z_prev
+        t = dx.dot(dg) / dg.dot(dg)
+        z_prev, z = z, P['proj'](z - t * g)
+        g_prev = g
+        _fx = P['f'](z)
+        _ = orc.stopping(g, _fx, it + 1, t, delta_g=dg, options={'max_iter': 10 ** 9,
+                                                                   'opt_tol': 1e-30})
+        it += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or it >= 200:
+            return it / el, it, el
+
+
+def bench_proj(reps=50):
+    import torch
+    import _native
+    from _native import ptr, stream_handle, check
+    from synthetic import proj_input
+    L = _native.lib()
+    y_h, starts_h = proj_input()
+    n, p = y_h.shape[0], starts_h.shape[0]
+    mb = int(np.max(np.diff(np.append(starts_h, n))))
+    y0 = torch.from_numpy(y_h).cuda()
+    y = y0.clone()
+    st = torch.from_numpy(starts_h).cuda()
+    ws = torch.zeros(L.bsls_proj_workspace_size(n, p, mb), dtype=torch.uint8, device='cuda')
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for k in range(reps + 5):
+        y.copy_(y0)
+        if k >= 5:
+            evs[k - 5][0].record()
+        check(L.bsls_proj_multi_simplex(ptr(y), ptr(st), p, n, mb, ptr(ws), ws.numel(),
+                                        stream_handle()), 'proj')
+        if k >= 5:
+            evs[k - 5][1].record()
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in evs)
+    med = ms[len(ms) // 2]
+    byt = 16 * n + 4 * (p + 1)
+    # CPU baseline for the same call: the oracle (1 thread)
+    from oracle import oracle as orc
+    yc = y_h.copy()
+    t0 = time.perf_counter()
+    orc.proj_multi_simplex_c(yc, starts_h)
+    cpu_s = time.perf_counter() - t0
+    ok = bool(np.array_equal(yc.view(np.int64), y.cpu().numpy().view(np.int64)))
+    return {'n': n, 'blocks': p, 'median_us': med * 1e3, 'min_us': ms[0] * 1e3,
+            'GB_s': byt / (med * 1e-3) / 1e9, 'alg_bytes': byt,
+            'frac_hbm_peak': byt / (med * 1e-3) / HBM_PEAK,
+            'cpu_oracle_ms_1thread': cpu_s * 1e3, 'bit_exact_vs_oracle': ok}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--profile-iters', type=int, default=50)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    from synthetic import make_shard, add_noise, SEED
+    from device import BBEngine, DeviceCSR
+    n_g, p_g, m_per, per_col = 1_000_000, 50_000, 100_000, 16
+    m = m_per * world
+    sh = make_shard(n_g, p_g, m, per_col, seed=SEED, rank=rank)
+    Ax = torch.from_numpy(sh['Ax']).cuda()
+    if dist:
+        dist.all_reduce(Ax)
+    b = add_noise(Ax.cpu().numpy(), 0.02, seed=SEED)
+    opts = {'max_iter': 10 ** 12, 'opt_tol': 1e-30}
+    if dist:
+        from distributed import ShardedBB, torch_all_reduce
+        A_dev = DeviceCSR(sh['A'])
+        x0 = torch.zeros(n_g, dtype=torch.float64, device='cuda')
+        x0[torch.from_numpy(np.cumsum(sh['block_sizes']) - 1).cuda()] = 1.0
+        part = A_dev.matvec(x0)
+        dist.all_reduce(part)
+        target = part - torch.from_numpy(b).cuda()
+        eng = BBEngine(sh['A'], None, sh['block_sizes'], options=opts, early_exit=False,
+                       A_dev=A_dev, AT=sh['AT'], target=target)
+        eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+        drv = ShardedBB(eng, torch_all_reduce())
+        drv.prologue()
+        run = drv.iterate
+    else:
+        eng = BBEngine(sh['A'], b, sh['block_sizes'], options=opts, early_exit=False,
+                       AT=sh['AT'])
+        eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+        eng.prologue()
+        run = eng.iterate
+    nnz = sh['A'].nnz
+    run(1, args.warmup)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(1 + args.warmup, args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    it_s = args.steps / el
+    value = it_s * world
+    s = eng.scalars()
+    finite = bool(np.isfinite(s[4]))
+
+    out = None
+    if rank == 0:
+        kb = kernel_bytes(m, n_g, eng.nz, p_g, nnz, sh['AT'].nnz)
+        kern = {}
+        if world == 1 and args.profile_iters > 0:
+            # per-kernel HIP-event timing on the stream the kernels run on
+            names = [(3, 'K2_spmvT_Nt_dots'), (4, 'K3_pava_clip_z2x'), (7, 'K1_spmv_A')]
+            acc = {nm: [] for _, nm in names}
+            it0 = 1 + args.warmup + args.steps
+            for it in range(it0, it0 + args.profile_iters):
+                evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                evs[0].record()
+                for k, (stg, _) in enumerate(names):
+                    eng.stage(stg, it)
+                    evs[k + 1].record()
+                torch.cuda.synchronize()
+                for k, (_, nm) in enumerate(names):
+                    acc[nm].append(evs[k].elapsed_time(evs[k + 1]) * 1e3)
+            for nm, v in acc.items():
+                us = float(np.mean(v))
+                kern[nm] = {'avg_us': us, 'alg_bytes': kb[nm],
+                            'GB_s': kb[nm] / (us * 1e-6) / 1e9,
+                            'frac': kb[nm] / (us * 1e-6) / HBM_PEAK}
+        dom = max(kern, key=lambda k: kern[k]['avg_us']) if kern else None
+        traffic = None
+        tfile = os.path.join(ROOT, 'profiles', 'traffic_r01.json')
+        if dom and os.path.exists(tfile):
+            try:
+                traffic = json.load(open(tfile)).get(dom, {}).get('hbm_bytes_per_launch')
+            except Exception:
+                traffic = None
+        roof = None
+        if dom:
+            roof = {'bound': 'hbm', 'kernel': dom,
+                    'achieved': kern[dom]['GB_s'], 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
+                    'frac': kern[dom]['frac'], 'traffic': traffic}
+        ib = survey_iter_bytes(m, n_g * world, eng.nz * world, nnz * world)
+        proj = bench_proj() if world == 1 else None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cps, cit, cel = cpu_baseline_bb(sh['A'], b, sh['block_sizes'])
+            cpu = {'value': cps, 'unit': 'BB it/s', 'cores': 1, 'kind': 'port',
+                   'sample': '%d BB iterations (%.1f s) of the same C3 problem: oracle '
+                             'restatement of BB.py over SciPy csr_matvec + C PAVA, '
+                             'OPENBLAS_NUM_THREADS=1' % (cit, cel)}
+        out = {
+            'metric': METRIC, 'value': value,
+            'unit': 'BB iterations/s (1M-route problem; N x 1M routes at N GPUs)',
+            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
+            'config': {'workload': 'C3: BB (z-space, PAVA projection) on 1M routes / 50k '
+                                   'blocks / %d links / %d nnz per GPU' % (m, nnz),
+                       'routes_per_gpu': n_g, 'blocks_per_gpu': p_g, 'links': m,
+                       'nnz_per_gpu': nnz, 'parallelism': 'column-shard x%d' % world},
+            'roofline': roof,
+            'iteration_roofline': {'survey_bytes_per_iter': ib,
+                                   'achieved_GB_s': ib * it_s / 1e9,
+                                   'frac': ib * it_s / HBM_PEAK},
+            'kernels': kern, 'proj_simplex': proj, 'cpu_baseline': cpu,
+            'finite': finite,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

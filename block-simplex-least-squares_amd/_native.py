@@ -1,0 +1,144 @@
+"""Loader for the gfx950 C-ABI library lib/libbsls_hip.so (include/bsls_hip.h).
+
+There is deliberately no CPU fallback: every compute entry point of this
+package goes through this library on a HIP device, and `lib()` raises if the
+library is missing or no device is present.  (Loading the .so itself works
+without a GPU, which is what the CPU test-suite checks.)
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'lib', 'libbsls_hip.so')
+CSRC = os.path.join(HERE, 'csrc')
+HEADER = os.path.join(os.path.dirname(HERE), 'include', 'bsls_hip.h')
+
+BSLS_OK = 0
+BSLS_E_ARG = -1
+BSLS_E_WORKSPACE = -2
+
+# scal[] slots and stop reasons (include/bsls_hip.h)
+S_STOP, S_ITER, S_ZBUF, S_T, S_FX, S_SUMDG, S_DZDG, S_DGDG, S_GG, S_RR, S_WARN = range(11)
+S_COUNT = 16
+STOP_NOCHANGE, STOP_MAXITER, STOP_GRAD, STOP_DG = 1, 2, 3, 4
+STOP_TEXT = {STOP_NOCHANGE: 'Exiting... no change in gradient',
+             STOP_MAXITER: 'max_iter',
+             STOP_GRAD: 'Exiting... norm(grad) too small',
+             STOP_DG: 'Exiting... no change in gradient'}
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_dbl = ctypes.c_double
+_sz = ctypes.c_size_t
+_int = ctypes.c_int
+
+
+class BBProblem(ctypes.Structure):
+    """Mirror of struct bsls_bb_problem (include/bsls_hip.h)."""
+    _fields_ = [('m', _i64), ('n', _i64), ('nz', _i64), ('nblocks', _i64),
+                ('A_indptr', _vp), ('A_indices', _vp), ('A_data', _vp),
+                ('AT_indptr', _vp), ('AT_indices', _vp), ('AT_data', _vp),
+                ('target', _vp), ('xstarts', _vp), ('zstarts', _vp), ('xz', _vp),
+                ('z', _vp * 2), ('g', _vp * 2), ('x', _vp), ('r', _vp), ('scal', _vp),
+                ('work', _vp),
+                ('max_zblock', _i64), ('max_iter', _i64), ('opt_tol', _dbl),
+                ('early_exit', _i32), ('a_group', _i32), ('at_group', _i32)]
+
+
+_SIGS = {
+    'bsls_proj_workspace_size': (_sz, [_i64, _i64, _i64]),
+    'bsls_proj_multi_simplex': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
+    'bsls_proj_multi_ball': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
+    'bsls_isotonic_workspace_size': (_sz, [_i64]),
+    'bsls_isotonic_multi': (_int, [_int, _vp, _vp, _i64, _i64, _vp, _int, _i64, _vp, _sz, _vp,
+                                   _vp]),
+    'bsls_x2z': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    'bsls_z2x': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    'bsls_n_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _int, _vp]),
+    'bsls_nt_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    'bsls_quad_obj': (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    'bsls_line_search': (_int, [_vp, _dbl, _vp, _vp, _dbl, _vp, _vp, _vp, _i64, _vp, _vp]),
+    'bsls_spmv_workspace_size': (_sz, [_i64]),
+    'bsls_csr_spmv': (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _dbl, _vp, _vp, _int, _vp, _sz, _vp]),
+    'bsls_bb_workspace_size': (_sz, [_i64, _i64, _i64]),
+    'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
+    'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
+    'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
+    'bsls_md_update': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _vp, _vp, _sz, _vp]),
+    'bsls_md_workspace_size': (_sz, [_i64]),
+    'bsls_version': (ctypes.c_char_p, []),
+    'bsls_device_arch': (_int, [ctypes.c_char_p, _int]),
+}
+
+
+def build(force=False):
+    """Compile csrc/*.hip for gfx950 into lib/libbsls_hip.so (hipcc via make)."""
+    args = ['make', '-s', '-C', CSRC, '-j8']
+    if force:
+        subprocess.check_call(['make', '-s', '-C', CSRC, 'clean'])
+    subprocess.check_call(args)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def load():
+    """dlopen the library and bind every entry point (works without a GPU)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError('bsls: %s is missing -- run __graft_entry__.build() '
+                               '(or make -C %s)' % (LIB_PATH, CSRC))
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+_checked_device = False
+
+
+def lib():
+    """The library, after checking that a HIP device is usable (raises if not)."""
+    global _checked_device
+    L = load()
+    if not _checked_device:
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError('bsls: no HIP device visible; this package has no CPU path '
+                               '(the CPU oracle lives under oracle/ for tests only)')
+        _checked_device = True
+    return L
+
+
+def check(rc, what='bsls call'):
+    if rc != BSLS_OK:
+        if rc == BSLS_E_ARG:
+            raise ValueError('%s: invalid arguments (BSLS_E_ARG)' % what)
+        if rc == BSLS_E_WORKSPACE:
+            raise RuntimeError('%s: workspace too small' % what)
+        raise RuntimeError('%s failed with hipError %d' % (what, rc))
+
+
+def stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def declared_symbols():
+    """Every function name declared in include/bsls_hip.h."""
+    import re
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r'^\s*(?:size_t|int|const char \*)\s*(bsls_\w+)\s*\(',
+                                 text, re.M)))

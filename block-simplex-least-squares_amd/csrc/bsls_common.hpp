@@ -1,0 +1,135 @@
+// bsls_common.hpp -- shared device helpers for the gfx950 (MI355X, CDNA4) kernels.
+//
+// Conventions
+//   * wave = 64 lanes; every block size here is a multiple of 64;
+//   * all arithmetic that must match the reference bit-for-bit is compiled with
+//     -ffp-contract=off (Makefile) so a*b+c stays two roundings, like the
+//     reference's x86-64 g++ build;
+//   * reductions are deterministic: fixed lane/thread trees, fixed partial order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bsls_hip.h"
+
+#define BSLS_CHECK(expr)                                   \
+    do {                                                   \
+        hipError_t e_ = (expr);                            \
+        if (e_ != hipSuccess) return (int)e_;              \
+    } while (0)
+
+#define BSLS_LAUNCH_CHECK() BSLS_CHECK(hipGetLastError())
+
+namespace bsls {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (WAVE - 1)); }
+
+// end of block b (the last block ends at n), reference proj_simplex.h:43-46
+__device__ __forceinline__ int64_t block_end(const int64_t *starts, int64_t nb, int64_t b,
+                                             int64_t n) {
+    return (b + 1 < nb) ? starts[b + 1] : n;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        T u = __shfl_xor(v, o, WAVE);
+        v = (u > v) ? u : v;
+    }
+    return v;
+}
+
+// Sum over G consecutive lanes (G power of two <= 64); result valid in all G lanes.
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+
+// Deterministic block-wide sum of NV values per thread (fixed tree); the result
+// is valid in thread 0.  `red` must hold NV * (blockDim.x / 64) doubles.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double *red) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = group_sum<WAVE>(v[k]);
+    const int w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[k * nw + w] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            double s = red[k * nw];
+            for (int i = 1; i < nw; ++i) s += red[k * nw + i];
+            v[k] = s;
+        }
+    }
+    __syncthreads();
+}
+
+// "Last workgroup reduces": every workgroup publishes NV partials; the
+// workgroup whose ticket add comes last sums all partials in index order
+// (deterministic) and returns true with the totals in thread 0's `tot`.
+// Protocol per cdna_hip_programming.md Guideline 16: plain partial stores ->
+// vmcnt(0) -> agent release -> relaxed agent ticket add; the last arriver does
+// one agent acquire -> vmcnt(0) -> barrier -> plain loads.  The ticket resets
+// itself (kernel-boundary ordered for the next launch).
+template <int NV>
+__device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsigned *ticket,
+                               double (&tot)[NV], double *red) {
+    __shared__ int am_last;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) partials[(size_t)blockIdx.x * NV + k] = mine[k];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        am_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!am_last) return false;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    double acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] += partials[(size_t)i * NV + k];
+    }
+    block_sum<NV>(acc, red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) tot[k] = acc[k];
+        *ticket = 0u;
+    }
+    return true;
+}
+
+// numpy.minimum(v, 1.) then numpy.maximum(., 0.) (python/main.py:65):
+// NaN propagates, -0.0 is kept.
+__device__ __forceinline__ double clip01(double v) {
+    double a = (v > 1.0) ? 1.0 : v;
+    return (a < 0.0) ? 0.0 : a;
+}
+
+// std::max(v, 0.) as in proj_simplex.h:33.
+__device__ __forceinline__ double relu_ref(double v) { return (v < 0.) ? 0. : v; }
+
+inline int grid_for(int64_t work, int per_block) {
+    int64_t g = (work + per_block - 1) / per_block;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace bsls

@@ -1,0 +1,89 @@
+"""Column-sharded BB across GPUs of one node (one process per GPU).
+
+The reference has no parallelism at all; its only natural
+decomposition is by block: blocks are independent in the projection and
+blockify() already makes each block's columns contiguous
+(python/bsls_matrices.py:109-126).  So rank g owns a contiguous run of whole
+blocks = a column slice A_g (m x n_g), its transpose, and its slices of
+z, g, x.  Per BB iteration:
+
+    stage 3   g_g = N_g' A_g' r  and the four local BB sums
+    all-reduce(sum) of the 4 BB sums  (32 bytes)
+    stage 4   t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = x0_g + N_g z_g   (local)
+    stage 1   r_g = A_g x_g   (partial residual, length m)
+    all-reduce(sum) of r_g  (8 m bytes: the one real exchange of the algorithm)
+    stage 2   r += target, ||r||^2, f, stopping test (redundant on every rank)
+
+The collectives go through torch.distributed: backend "nccl" is RCCL over xGMI
+on MI355X; "gloo" runs the same orchestration in CPU tests with a fake stage
+backend.  Results depend on the rank count only through the summation order of
+the r all-reduce (within the 1e-6 iterate contract).
+"""
+import numpy as np
+
+
+def partition_blocks(block_sizes, col_weights, world):
+    """Split blocks into `world` contiguous runs balancing the per-block weight
+    (nnz of the block's columns).  Returns block boundaries [b_0=0, ..., b_W=p]."""
+    bs = np.asarray(block_sizes, dtype=np.int64)
+    w = np.asarray(col_weights, dtype=np.float64)
+    if w.shape[0] != bs.shape[0]:
+        raise ValueError('one weight per block expected')
+    p = bs.shape[0]
+    if world < 1 or world > p:
+        raise ValueError('need 1 <= world <= number of blocks')
+    cum = np.concatenate(([0.0], np.cumsum(w)))
+    total = cum[-1]
+    bounds = [0]
+    for g in range(1, world):
+        target = total * g / world
+        b = int(np.searchsorted(cum, target, side='left'))
+        b = min(max(b, bounds[-1] + 1), p - (world - g))
+        bounds.append(b)
+    bounds.append(p)
+    return np.array(bounds, dtype=np.int64)
+
+
+class ShardedBB:
+    """Drive one rank's stages with the all-reduces between them.
+
+    `engine` exposes stage(k, it), r (m-vector), scal (BSLS_S_COUNT vector) --
+    device.BBEngine on GPUs; a numpy/torch fake in the gloo tests.
+    `all_reduce(t)` sums a tensor in place across ranks."""
+
+    SUMS = slice(5, 9)   # scal[SUMDG..GG]
+
+    def __init__(self, engine, all_reduce):
+        self.e = engine
+        self.all_reduce = all_reduce
+
+    def prologue(self):
+        e = self.e
+        e.stage(0, 0)
+        e.stage(5, 0)            # z[1] = z0 + 1, x = x0 + N z[1]
+        e.stage(1, 0)
+        self.all_reduce(e.r)
+        e.stage(2, 0)            # r(z0 + 1)
+        e.stage(3, 0)            # g_prev = grad(z0 + 1) -> g[0]
+        e.stage(6, 0)            # x = x0 + N z0
+        e.stage(1, 0)
+        self.all_reduce(e.r)
+        e.stage(2, 0)            # r(z0), f(z0)
+
+    def iterate(self, first, count):
+        e = self.e
+        for i in range(first, first + count):
+            e.stage(3, i)
+            self.all_reduce(e.scal[self.SUMS])
+            e.stage(4, i)
+            e.stage(1, i)
+            self.all_reduce(e.r)
+            e.stage(2, i)
+
+
+def torch_all_reduce(group=None):
+    import torch.distributed as dist
+
+    def f(t):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return f

@@ -1,0 +1,153 @@
+#!/usr/bin/env python
+"""Entry point and z-space problem build (reference: python/main.py).
+
+    python main.py --file X.mat --method BB [--log INFO] [--eq CP] [--noise 0.02]
+
+solve_in_z(A, b, x0, N, block_sizes, method) keeps the reference's signature
+and return value (iters, times, states); the z-space closures f / nabla_f /
+proj of python/main.py:53-65 become the device engine (device.BBEngine): the
+6 SciPy SpMVs + PAVA of each reference BB iteration become three fused HIP
+kernels.  LS_postprocess returns the reference's output dict with the same keys
+(python/main.py:81-136), its matrix work done on the device.
+"""
+import argparse
+import logging
+import sys
+
+import numpy as np
+
+from bsls_utils import particular_x0, x2z
+from gradient_descent import GradientDescent
+
+ACCEPTED_LOG_LEVELS = ['CRITICAL', 'ERROR', 'WARNING', 'INFO', 'DEBUG', 'WARN']
+
+
+def parser():
+    p = argparse.ArgumentParser()
+    p.add_argument('--file', help='Data file (*.mat)', default='route_assignment_matrices_ntt.mat')
+    p.add_argument('--log', dest='log', nargs='?', const='INFO', default='WARN',
+                   help='Set log level (default: WARN)')
+    p.add_argument('--method', dest='method', type=str, default='BB', help='Least squares method')
+    p.add_argument('--init', dest='init', action='store_true', default=False,
+                   help='Initial solution from data')
+    p.add_argument('--eq', dest='eq', type=str, default='CP',
+                   help='Type of equality constraint (CP or OD)')
+    p.add_argument('--noise', dest='noise', type=float, default=None, help='Noise level')
+    return p
+
+
+def build_engine(A, b, x0, block_sizes, options=None):
+    from device import BBEngine
+    return BBEngine(A, b, block_sizes, options=options, x0=x0)
+
+
+def solve_in_z(A, b, x0, N, block_sizes, method, options=None, engine=None):
+    """python/main.py:41-79 on the device.  N is accepted for signature
+    compatibility and never used: the engine applies N / N' as per-block
+    differences without materialising it."""
+    if block_sizes is not None and len(block_sizes) == A.shape[1]:
+        logging.error('Trivial example: nblocks == nroutes, exiting solver')
+        sys.exit()
+    block_sizes = np.asarray(block_sizes)
+    # the reference's proj asserts strictly increasing z-block starts
+    # (c_extensions.pyx:78 through main.py:64): every block needs >= 2 routes
+    assert np.all(block_sizes >= 2)
+    z0 = x2z(x0, block_sizes)
+    eng = engine or build_engine(A, b, x0, block_sizes)
+    gd = GradientDescent(z0=z0, method=method, options=options, engine=eng)
+    iters, times, states = gd.run()
+    import torch
+    zl = torch.from_numpy(np.ascontiguousarray(states[-1], dtype=np.float64)).cuda()
+    x = eng.n_apply(zl, with_x0=True).cpu().numpy()   # particular_x0 + N z
+    assert np.all(x >= 0), "x shouldn't have negative entries after projection"
+    return iters, times, states
+
+
+def LS_postprocess(states, x0, A, b, x_true, scaling=None, block_sizes=None, output=None, N=None,
+                   is_x=False, engine=None):
+    """python/main.py:81-136: objective and route-flow error metrics per logged
+    state.  X_hat = x0 + N Z and A X_hat are formed on the device."""
+    import torch
+    if x_true is None:
+        return [], [], output
+    if scaling is None:
+        scaling = np.ones(x_true.shape)
+    if output is None:
+        output = {}
+    d = len(states)
+    from device import DeviceCSR, BlockLayout
+    Ad = engine.A if engine is not None else DeviceCSR(A)
+    bt = torch.from_numpy(np.asarray(b, dtype=np.float64)).cuda()
+    cols = []
+    if not is_x and (N is None or N.size > 0):
+        lay = engine.layout if engine is not None else BlockLayout(block_sizes)
+        from c_extensions.c_extensions import z2x_c  # noqa: F401  (same kernel family)
+        import _native
+        from _native import ptr, stream_handle, check
+        x0d = torch.from_numpy(np.asarray(x0, dtype=np.float64)).cuda()
+        for s in states:
+            zd = torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64)).cuda()
+            xd = torch.empty(lay.n, dtype=torch.float64, device='cuda')
+            check(_native.lib().bsls_n_apply(ptr(xd), ptr(zd), ptr(lay.xstarts), lay.p, lay.n,
+                                             0, stream_handle()), 'bsls_n_apply')
+            cols.append(xd + x0d)
+    else:
+        cols = [torch.from_numpy(np.asarray(s, dtype=np.float64)).cuda() for s in states]
+    X = torch.stack(cols, dim=1)                       # n x d
+    x_last = X[:, -1].cpu().numpy()
+    output['AA'] = A.shape
+    output['x_hat'] = tuple(X.shape)
+    output['blocks'] = block_sizes.shape if block_sizes is not None else None
+    x0d = torch.from_numpy(np.asarray(x0, dtype=np.float64)).cuda()
+    xtd = torch.from_numpy(np.asarray(x_true, dtype=np.float64)).cuda()
+    r0 = Ad.matvec(x0d, add=-bt)
+    rs = Ad.matvec(xtd, add=-bt)
+    starting_error = 0.5 * float(r0.norm()) ** 2
+    opt_error = 0.5 * float(rs.norm()) ** 2
+    err = np.array([0.5 * float(Ad.matvec(X[:, k].contiguous(), add=-bt).square().sum())
+                    for k in range(d)])
+    output['0.5norm(Ax-b)^2'], output['0.5norm(Ax_init-b)^2'] = err, starting_error
+    output['0.5norm(Ax*-b)^2'] = opt_error
+    sc = torch.from_numpy(np.asarray(scaling, dtype=np.float64)).cuda()
+    xdiff = xtd[None, :] - X.T                          # d x n
+    xds = sc[None, :] * xdiff
+    xts = sc[None, :] * xtd[None, :].expand_as(xdiff)
+    output['max|f * (x-x_true)|'] = xds.max(dim=1).values.cpu().numpy()
+    wrong = torch.nonzero(xdiff > 1e-3)[:, 0].cpu().numpy()
+    output['incorrect x entries'] = np.bincount(wrong)
+    output['percent flow allocated incorrectly'] = (xds.abs().sum(dim=1) /
+                                                    xts.sum(dim=1)).cpu().numpy()
+    output['max|f * (x_init-x_true)|'] = float(np.max(scaling * np.abs(x_true - x0)))
+    return x_last, err, output
+
+
+def main(args=None, plot=False):
+    if args is None:
+        args = parser().parse_args()
+    if args.log in ACCEPTED_LOG_LEVELS:
+        logging.basicConfig(level=getattr(logging, args.log))
+    config = {'full': True, 'L': True, 'OD': True, 'CP': True, 'LP': True,
+              'eq': args.eq, 'init': args.init}
+    from bsls_matrices import BSLSMatrices
+    bm = BSLSMatrices(fname=args.file, **config)
+    bm.degree_reduced_form()
+    AA, bb, N, block_sizes, x_split, nz, scaling, rsort_index, x0 = bm.get_LS()
+    output = bm.info
+    if args.noise:
+        delta = np.random.normal(scale=bb * args.noise)
+        bb = bb + delta
+    eng = build_engine(AA, bb, x0, block_sizes)
+    iters, times, states = solve_in_z(AA, bb, x0, N, block_sizes, args.method, engine=eng)
+    x_last, error, output = LS_postprocess(states, x0, AA, bb, x_split, scaling=scaling,
+                                           block_sizes=block_sizes, N=N, output=output,
+                                           engine=eng)
+    if plot:
+        import matplotlib.pyplot as plt
+        plt.figure(); plt.hist(x_last)
+        plt.figure(); plt.loglog(np.cumsum(times), error); plt.show()
+    return iters, times, states, output
+
+
+if __name__ == '__main__':
+    iters, times, states, output = main()
+    print(output)

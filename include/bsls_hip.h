@@ -1,0 +1,196 @@
+/*
+ * bsls_hip.h -- C ABI of the MI355X (gfx950) block-simplex least-squares hot path.
+ *
+ * Built from the .hip sources in block-simplex-least-squares_amd/csrc into
+ * block-simplex-least-squares_amd/lib/libbsls_hip.so.  Plain pointers and sizes only:
+ * every pointer argument named d_* is DEVICE memory (HBM); `stream` is a
+ * hipStream_t passed as void* (NULL = the null stream).  Nothing here takes host
+ * buffers: the Python drop-in (c_extensions) stages NumPy inputs itself.
+ *
+ * Return value: BSLS_OK (0) on success; a positive hipError_t code when a HIP
+ * call failed; a negative BSLS_E_* code for invalid arguments.  Launches are
+ * asynchronous on `stream`; kernel-side argument faults (e.g. PAVA weights < 1)
+ * are reported through the optional d_status word (0 = fine), which the caller
+ * reads after synchronising.
+ *
+ * Reference interface each entry replaces (paths relative to the reference repo):
+ *   python/c_extensions/c_extensions.pyx (the Cython module c_extensions) and the
+ *   header-only kernels it wraps; SciPy csr_matvec behind A.dot at python/main.py:53-54.
+ */
+#ifndef BSLS_HIP_H
+#define BSLS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSLS_OK 0
+#define BSLS_E_ARG (-1)        /* bad size / null pointer / layout */
+#define BSLS_E_WORKSPACE (-2)  /* workspace smaller than *_workspace_size() */
+
+/* Block layout shared by every projection entry: block b covers
+ * [d_starts[b], d_starts[b+1]) (the last block ends at n); d_starts strictly
+ * increasing, d_starts[0] >= 0, d_starts[nblocks-1] < n; elements before
+ * d_starts[0] are left untouched.  max_block = the largest block size (the
+ * host knows it; it picks the kernel paths and the workspace size). */
+
+/* ---- simplex / l1-ball projection -------------------------------------------
+ * Replaces proj_multi_simplex_c / proj_multi_ball_c (c_extensions.pyx:31-50)
+ * -> proj_multi_simplex / proj_multi_ball (proj_simplex.h:37-74).  In place on
+ * d_y (fp64).  Bit-identical to the reference for finite inputs. */
+size_t bsls_proj_workspace_size(int64_t n, int64_t nblocks, int64_t max_block);
+int bsls_proj_multi_simplex(double *d_y, const int64_t *d_starts, int64_t nblocks, int64_t n,
+                            int64_t max_block, void *d_work, size_t work_bytes, void *stream);
+int bsls_proj_multi_ball(double *d_y, const int64_t *d_starts, int64_t nblocks, int64_t n,
+                         int64_t max_block, void *d_work, size_t work_bytes, void *stream);
+
+/* ---- isotonic regression (PAVA) ---------------------------------------------
+ * Replaces isotonic_regression_multi_c{,_2,_3} (c_extensions.pyx:76-138) ->
+ * isotonic_regression_multi{,_2,_3} (isotonic_regression.h:85-102,157-164).
+ * d_weight: run-length array of n int32 (NULL = fresh ones, as weight=None);
+ * updated in place like the reference's int weight buffer.  expand = the
+ * reference's `update` flag.  Variant 1 is what python/main.py:64 calls. */
+size_t bsls_isotonic_workspace_size(int64_t n);
+int bsls_isotonic_multi(int variant, double *d_y, const int64_t *d_starts, int64_t nblocks,
+                        int64_t n, int32_t *d_weight, int expand, int64_t max_block,
+                        void *d_work, size_t work_bytes, int32_t *d_status, void *stream);
+
+/* ---- z <-> x change of variables --------------------------------------------
+ * Replaces x2z_c / z2x_c (c_extensions.pyx:195-248); d_starts[0] must be 0. */
+int bsls_x2z(const double *d_x, double *d_z, const int64_t *d_starts, int64_t nblocks,
+             int64_t n, void *stream);
+int bsls_z2x(double *d_x, const double *d_z, const int64_t *d_starts, int64_t nblocks,
+             int64_t n, void *stream);
+
+/* N z (with_x0 = 0) or x0 + N z (with_x0 = 1), and g = N' w, for the z-space
+ * change of variables (N of bsls_utils.block_sizes_to_N, python/bsls_utils.py:139-162,
+ * never materialised): (N z)_i = z_j - z_{j-1} inside a block, last entry -z_last;
+ * (N' w)_j = w_i - w_{i+1}.  d_starts are the x-space block starts. */
+int bsls_n_apply(double *d_x, const double *d_z, const int64_t *d_starts, int64_t nblocks,
+                 int64_t n, int with_x0, void *stream);
+int bsls_nt_apply(const double *d_w, double *d_g, const int64_t *d_starts, int64_t nblocks,
+                  int64_t n, void *stream);
+
+/* ---- dense QP helpers (not on the sparse hot path; kept for ABI parity) ------
+ * Replace quad_obj_c / line_search_quad_obj_c (c_extensions.pyx:148-192) ->
+ * quadratic_objective.h:15-61.  The scalar result is written to *d_f (device).
+ * line_search: *d_f_out receives f_new; d_x_new / d_g_new updated in place. */
+int bsls_quad_obj(const double *d_x, const double *d_Q, const double *d_c, double *d_g,
+                  int64_t n, double *d_f, void *stream);
+int bsls_line_search(const double *d_x, double f, const double *d_g, double *d_x_new,
+                     double f_new, double *d_g_new, const double *d_Q, const double *d_c,
+                     int64_t n, double *d_f_out, void *stream);
+
+/* ---- CSR SpMV ----------------------------------------------------------------
+ * Replaces scipy csr_matvec behind A.dot(x) (python/main.py:53-54,
+ * python/algorithm_utils.py:91-92, python/mirror_descent.py:32-34):
+ *   d_out[r] = sum_e data[e] * x[indices[e]]  (+ d_add[r] if d_add)  (* 1 if alpha == 1)
+ * int64 row pointers, int32 column indices, fp64 values.  `group` = lanes per
+ * row (power of two 1..64; pick ~ the mean row length).  If d_sq_out is
+ * non-NULL it receives sum_r d_out[r]^2 (deterministic tree order).
+ * The product is alpha * (A x) (alpha == 1.0: no scaling multiply). */
+size_t bsls_spmv_workspace_size(int64_t m);
+int bsls_csr_spmv(int64_t m, const int64_t *d_indptr, const int32_t *d_indices,
+                  const double *d_data, const double *d_x, const double *d_add, double alpha,
+                  double *d_out, double *d_sq_out, int group, void *d_work, size_t work_bytes,
+                  void *stream);
+
+/* ---- fused z-space Barzilai-Borwein engine ----------------------------------
+ * Replaces, per iteration, BB.solve's loop body (python/BB.py:17-41) over the
+ * closures of main.solve_in_z (python/main.py:53-65) and the stopping rule
+ * solvers.stopping (python/solvers.py:40-63):
+ *   K1  r = A x + target (= A N z + A x0 - b), ||r||^2, stop test (SpMV, A CSR)
+ *   K2  g = N' A' r, dg = g - g_prev, BB dot products      (SpMV', explicit A' CSR)
+ *   K3  z <- clip01(PAVA(z - t g)), x <- N z               (per-block projection)
+ * The caller owns every buffer (see struct); bsls_bb_prologue() performs
+ * BB.py:14-15 (g_prev = grad(z0 + 1)) and evaluates r(z0).  Iterations keep
+ * running until the device-side stop flag is set; after it is set, further
+ * enqueued iterations are no-ops.  scal[] layout: BSLS_S_* below. */
+enum {
+    BSLS_S_STOP = 0,       /* 0 running, else the stop reason BSLS_STOP_* */
+    BSLS_S_ITER = 1,       /* last completed iteration i */
+    BSLS_S_ZBUF = 2,       /* index (0/1) of the z buffer holding the current iterate */
+    BSLS_S_T = 3,          /* last BB step t */
+    BSLS_S_FX = 4,         /* f(z) = 0.5 ||r||^2 at the current iterate */
+    BSLS_S_SUMDG = 5,      /* sum(delta_g) */
+    BSLS_S_DZDG = 6,       /* delta_z . delta_g */
+    BSLS_S_DGDG = 7,       /* delta_g . delta_g */
+    BSLS_S_GG = 8,         /* g . g */
+    BSLS_S_RR = 9,         /* r . r */
+    BSLS_S_WARN = 10,      /* count of |t| outside [1e-10, 1e10] (BB.py:27-28) */
+    BSLS_S_COUNT = 16
+};
+enum {
+    BSLS_STOP_NOCHANGE = 1,   /* BB.py:22  sum(delta_g) == 0 */
+    BSLS_STOP_MAXITER = 2,    /* solvers.py:42-44 */
+    BSLS_STOP_GRAD = 3,       /* solvers.py:51-54 */
+    BSLS_STOP_DG = 4          /* solvers.py:59-62 */
+};
+typedef struct bsls_bb_problem {
+    int64_t m, n, nz, nblocks;      /* rows, x length, z length (n - nblocks), blocks */
+    const int64_t *A_indptr;        /* m+1 */
+    const int32_t *A_indices;       /* nnz */
+    const double *A_data;           /* nnz */
+    const int64_t *AT_indptr;       /* n+1 (CSR of A transposed) */
+    const int32_t *AT_indices;
+    const double *AT_data;
+    const double *target;           /* m: A x0 - b (python/main.py:48) */
+    const int64_t *xstarts;         /* nblocks, x-space block starts, xstarts[0] = 0 */
+    const int64_t *zstarts;         /* nblocks, z-space block starts (xstarts[b] - b) */
+    const int32_t *xz;              /* n: z index of x entry i, or -1 for a block's last entry */
+    double *z[2];                   /* ping-pong iterate buffers, nz each */
+    double *g[2];                   /* ping-pong gradient buffers, nz each */
+    double *x;                      /* n: N z of the current iterate (x0 is in target) */
+    double *r;                      /* m: residual */
+    double *scal;                   /* BSLS_S_COUNT doubles */
+    void *work;                     /* bsls_bb_workspace_size() bytes, zeroed once */
+    int64_t max_zblock;             /* largest z-block (x-block size - 1) */
+    int64_t max_iter;               /* options['max_iter'] */
+    double opt_tol;                 /* options['opt_tol'] */
+    int32_t early_exit;             /* 0 disables every early exit (fixed-count timing) */
+    int32_t a_group, at_group;      /* lanes per CSR row for A and A' (power of 2, <= 64) */
+} bsls_bb_problem;
+
+size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
+/* BB.py:14-15 and the first f(z0): resets scal/tickets, g[0] = grad(z0 + 1),
+ * r = r(z0), scal[FX] = f(z0).  z[0] must hold z0. */
+int bsls_bb_prologue(const bsls_bb_problem *p, void *stream);
+/* Enqueue iterations first_iter .. first_iter+count-1 (first_iter >= 1); after
+ * iteration i the iterate is z[i & 1] unless the run stopped (scal[ZBUF]). */
+int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count, void *stream);
+/* The building blocks, for multi-GPU column sharding where RCCL all-reduces sit
+ * between them (A_g = the rank's block-aligned column slice):
+ *   0  reset scal[] and the reduction tickets
+ *   1  r = A_g x_g            (partial residual; all-reduce r afterwards)
+ *   2  r += target, ||r||^2, f, stopping test of iteration `iter` (iter 0: none)
+ *   3  g = N'A'r -> g[iter & 1]; iter > 0 also dg and the four BB sums into
+ *      scal[SUMDG..GG] (all-reduce those four afterwards)
+ *   4  t from the sums, z[iter&1] = clip01(PAVA(z - t g)), x = N z
+ *   5  z[1] = z[0] + 1, x = N z[1]           (prologue)
+ *   6  x = N z[0]                             (prologue)
+ *   7  single GCD: r = A x + target, ||r||^2, f, stopping test (= 1 then 2 fused)
+ * One iteration i >= 1 = 3, [allreduce sums], 4, 1, [allreduce r], 2; on one GCD
+ * bsls_bb_iterate runs 3, 4, 7. */
+int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
+
+/* ---- mirror descent ---------------------------------------------------------
+ * Replaces mirror_descent.least_squares's step (python/mirror_descent.py:37-47):
+ * x <- x * exp(-t_k g) per coordinate, t_k = sqrt(2 ln k_b)/(sqrt(k) Lf), then
+ * every block divided by its sum; *d_dxinf receives ||x_new - x_old||_inf.
+ * d_g = A'(Ax - b) computed with bsls_csr_spmv.  In place on d_x. */
+int bsls_md_update(double *d_x, const double *d_g, const int64_t *d_starts, int64_t nblocks,
+                   int64_t n, double step_scale, double *d_dxinf, void *d_work,
+                   size_t work_bytes, void *stream);
+size_t bsls_md_workspace_size(int64_t nblocks);
+
+/* Library / device info (for the loader's self-check). */
+const char *bsls_version(void);
+int bsls_device_arch(char *buf, int buflen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSLS_HIP_H */

@@ -1,0 +1,159 @@
+"""Column-sharded BB orchestration (distributed.ShardedBB) on 2 gloo ranks (CPU).
+
+The GPU stages are replaced by a NumPy test double that implements each stage's
+contract from include/bsls_hip.h (bsls_bb_stage) with the oracle's PAVA, so
+what is tested is the sharding: block-aligned column split, the r all-reduce,
+the four-sum all-reduce and the stage order.  The sharded run must reproduce
+the unsharded run and the oracle's BB trajectory (python/BB.py semantics).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
+
+
+class FakeStages:
+    """NumPy model of bsls_bb_stage for one column shard."""
+
+    def __init__(self, A, AT, sizes, target, orc, max_iter):
+        self.A, self.AT, self.sizes, self.target = A, AT, np.asarray(sizes), target
+        self.orc, self.max_iter = orc, max_iter
+        self.n = int(self.sizes.sum())
+        self.nz = self.n - len(self.sizes)
+        self.xst = np.concatenate(([0], np.cumsum(self.sizes)[:-1]))
+        self.zst = self.xst - np.arange(len(self.sizes))
+        self.z = [np.zeros(self.nz), np.zeros(self.nz)]
+        self.g = [np.zeros(self.nz), np.zeros(self.nz)]
+        self.x = np.zeros(self.n)
+        self.r = torch.zeros(A.shape[0], dtype=torch.float64)
+        self.scal = torch.zeros(16, dtype=torch.float64)
+
+    def Nz(self, z):
+        out = np.empty(self.n)
+        for b, (xs, k) in enumerate(zip(self.xst, self.sizes)):
+            zb = z[self.zst[b]:self.zst[b] + k - 1]
+            prev = np.concatenate(([0.0], zb))
+            out[xs:xs + k] = np.concatenate((zb, [0.0])) - prev
+        return out
+
+    def Ntw(self, w):
+        g = np.empty(self.nz)
+        for b, (xs, k) in enumerate(zip(self.xst, self.sizes)):
+            g[self.zst[b]:self.zst[b] + k - 1] = w[xs:xs + k - 1] - w[xs + 1:xs + k]
+        return g
+
+    def stage(self, k, it):
+        s = self.scal
+        zc, zn = (it - 1) & 1, it & 1
+        if k == 0:
+            s.zero_()
+        elif k == 1:
+            self.r[:] = torch.from_numpy(self.A.dot(self.x))
+        elif k == 2:
+            self.r += torch.from_numpy(self.target)
+            rr = float(self.r.dot(self.r))
+            s[4], s[9] = 0.5 * np.sqrt(rr) ** 2, rr
+            if it > 0:
+                s[1], s[2] = it, it & 1
+                if it >= self.max_iter:
+                    s[0] = 2
+        elif k == 3:
+            g = self.Ntw(self.AT.dot(self.r.numpy()))
+            if it == 0:
+                self.g[0][:] = g
+                return
+            self.g[zn][:] = g
+            dg = g - self.g[zc]
+            dz = self.z[zc] - self.z[zn]
+            s[5], s[6], s[7], s[8] = dg.sum(), dz.dot(dg), dg.dot(dg), g.dot(g)
+        elif k == 4:
+            t = float(s[6]) / float(s[7])
+            y = self.z[zc] - t * self.g[zn]
+            self.orc.isotonic_regression_multi_c(y, self.zst)
+            self.z[zn][:] = np.maximum(np.minimum(y, 1.0), 0.0)
+            self.x = self.Nz(self.z[zn])
+        elif k == 5:
+            self.z[1][:] = self.z[0] + 1
+            self.x = self.Nz(self.z[1])
+        elif k == 6:
+            self.x = self.Nz(self.z[0])
+
+
+def _problem():
+    sys.path.insert(0, PKG)
+    from synthetic import make_shard, add_noise
+    sh = make_shard(6_000, 300, 800, per_col=8, seed=21)
+    b = add_noise(sh['Ax'], 0.02, seed=21)
+    return sh, b
+
+
+def _run(rank, world, iters, out_q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, PKG)
+    from oracle import oracle as orc
+    from distributed import ShardedBB, partition_blocks
+    if world > 1:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        red = lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    else:
+        red = lambda t: None
+    sh, b = _problem()
+    sizes = sh['block_sizes']
+    bounds = partition_blocks(sizes, sizes * 8.0, world)
+    xst = np.concatenate(([0], np.cumsum(sizes)))
+    c0, c1 = xst[bounds[rank]], xst[bounds[rank + 1]]
+    A_g = sh['A'][:, c0:c1].tocsr()
+    sz_g = sizes[bounds[rank]:bounds[rank + 1]]
+    x0 = np.zeros(c1 - c0)
+    x0[np.cumsum(sz_g) - 1] = 1.0
+    part = torch.from_numpy(A_g.dot(x0))
+    red(part)
+    target = part.numpy() - b
+    eng = FakeStages(A_g, A_g.T.tocsr(), sz_g, target, orc, iters)
+    drv = ShardedBB(eng, red)
+    drv.prologue()
+    traj = {}
+    for i in range(1, iters + 1):
+        drv.iterate(i, 1)
+        traj[i] = eng.z[i & 1].copy()
+    out_q.put((rank, {k: v for k, v in traj.items() if k in (1, 5, iters)}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _spawn(world, iters):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000))
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_run, args=(r, world, iters, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return {i: np.concatenate([res[r][i] for r in range(world)]) for i in res[0]}
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_sharded_bb_matches_single_and_oracle(orc):
+    iters = 20
+    one = _spawn(1, iters)
+    two = _spawn(2, iters)
+    for i in one:
+        d = np.max(np.abs(one[i] - two[i])) / max(1.0, np.max(np.abs(one[i])))
+        assert d < 1e-10, (i, d)
+    sh, b = _problem()
+    ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], iters, record_every=1)
+    for i in one:
+        d = np.max(np.abs(two[i] - ref[i])) / max(1.0, np.max(np.abs(ref[i])))
+        assert d < 1e-8, (i, d)

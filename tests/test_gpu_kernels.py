@@ -1,0 +1,209 @@
+"""Parity of the HIP kernels (through the C ABI) with the oracle.  Needs an MI355X.
+
+Bar: bit-exact for projections / PAVA / x<->z / dense QP (the reference's own
+arithmetic order is reproduced); SpMV within 1e-13 relative (summation order
+differs from SciPy's sequential row loop).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sps
+
+from conftest import SEED
+
+pytestmark = pytest.mark.gpu
+
+
+def exact(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+@pytest.fixture(scope='module')
+def cx(cuda):
+    from c_extensions import c_extensions
+    return c_extensions
+
+
+# ------------------------------------------------------------------ projections
+
+def test_proj_golden_numpy(cx, golden):
+    G = golden('proj_simplex.npz')
+    for ci in range(int(G['ncases'])):
+        y, b = G['c%d_y' % ci], G['c%d_blocks' % ci]
+        ys = y.copy(); cx.proj_multi_simplex_c(ys, b)
+        assert exact(ys, G['c%d_simplex' % ci]), ('simplex', ci)
+        yb = y.copy(); cx.proj_multi_ball_c(yb, b)
+        assert exact(yb, G['c%d_ball' % ci]), ('ball', ci)
+    y = G['single_y'].copy(); cx.proj_simplex_c(y, 10, 40)
+    assert exact(y, G['single_out'])
+
+
+def test_proj_kats(cx):
+    z = np.array([5.352, 3.23, 32.78, -1.234, 1.7, 104., 53.])
+    for truth, s, e in [([5.352, 3.23, 1., 0., 1.7, 104., 53.], 2, 4),
+                        ([0., 0., 0., 0., 0, 1., 0.], 0, 7), (list(z), 4, 4)]:
+        y = z.copy(); cx.proj_simplex_c(y, s, e)
+        assert list(y) == truth
+    for b, truth in [([0, 2, 4], [1., 0., 1., 0., 0., 1., 0.]),
+                     ([0], [0., 0., 0., 0., 0., 1., 0.]), ([0, 3], [0., 0., 1., 0., 0., 1., 0.])]:
+        y = z.copy(); cx.proj_multi_simplex_c(y, np.array(b))
+        assert list(y) == truth
+    y = np.array([0.234, 0.5, 1.3, -1.234, 1.7, -1.0, 53.])
+    cx.proj_multi_ball_c(y, np.array([0, 2, 4]))
+    assert list(y) == [0.234, 0.5, 1., 0., 0., 0., 1.]
+
+
+@pytest.mark.parametrize('kind', ['unif', 'gauss'])
+def test_proj_c2_full_size_bit_exact(cx, orc, kind):
+    """Config C2 (3.2M fp64, 100k blocks) on device tensors vs the oracle."""
+    import torch
+    from synthetic import proj_input
+    y, starts = proj_input(kind=kind)
+    ref = y.copy()
+    orc.proj_multi_simplex_c(ref, starts)
+    yd = torch.from_numpy(y).cuda()
+    cx.proj_multi_simplex_c(yd, torch.from_numpy(starts).cuda())
+    assert exact(yd.cpu().numpy(), ref)
+
+
+def test_proj_size_classes(cx, orc):
+    """Blocks straddling every path: lane (<=64), LDS (<=8192), global (>8192)."""
+    rs = np.random.RandomState(SEED)
+    sizes = np.array([1, 2, 3, 7, 8, 9, 16, 17, 31, 33, 63, 64, 65, 100, 1000, 4096, 8192, 8193,
+                      20000, 5, 64, 1])
+    for trial in range(3):
+        perm = rs.permutation(sizes)
+        starts = np.concatenate(([3], 3 + np.cumsum(perm)[:-1])).astype(np.int64)
+        n = 3 + int(perm.sum())
+        for scale in (1.0, 0.001, 100.0):
+            y = rs.randn(n) * scale
+            for name in ('proj_multi_simplex_c', 'proj_multi_ball_c'):
+                a = y.copy(); getattr(cx, name)(a, starts)
+                r = y.copy(); getattr(orc, name)(r, starts)
+                assert exact(a, r), (trial, scale, name)
+
+
+def test_proj_ties_and_zeros(cx, orc):
+    rs = np.random.RandomState(SEED + 3)
+    n = 5000
+    starts = np.sort(rs.choice(np.arange(1, n), 150, replace=False))
+    starts = np.concatenate(([0], starts)).astype(np.int64)
+    for y in (np.zeros(n), np.full(n, 0.25), np.round(rs.rand(n) * 3) / 3, -np.abs(rs.randn(n)),
+              np.where(rs.rand(n) < 0.5, -0.0, 0.0)):
+        a = y.copy(); cx.proj_multi_simplex_c(a, starts)
+        r = y.copy(); orc.proj_multi_simplex_c(r, starts)
+        assert exact(a, r)
+
+
+# ------------------------------------------------------------------ PAVA
+
+def test_isotonic_golden(cx, golden):
+    G = golden('isotonic.npz')
+    for ci in range(int(G['ncases'])):
+        y, b = G['c%d_y' % ci], G['c%d_blocks' % ci]
+        for tag, fn in (('v1', cx.isotonic_regression_multi_c),
+                        ('v3', cx.isotonic_regression_multi_c_3)):
+            for upd in (1, 0):
+                yy = y.copy()
+                w = np.ones(len(y), dtype=np.int32)
+                fn(yy, b, w, upd)
+                assert exact(yy, G['c%d_%s_u%d' % (ci, tag, upd)]), (ci, tag, upd)
+                assert np.array_equal(w, G['c%d_%s_u%d_w' % (ci, tag, upd)]), (ci, tag, upd)
+        yy = y.copy(); cx.isotonic_regression_multi_c_2(yy, b)
+        assert exact(yy, G['c%d_v2' % ci]), ci
+    y = np.array([4., 5., 1., 6., 8., 7.])
+    cx.isotonic_regression_c(y, 0, 6)
+    assert exact(y, G['kat_single'])
+
+
+def test_isotonic_c3_full_size(cx, orc):
+    """z-space PAVA at config C3 (950k entries, 50k blocks) vs the oracle."""
+    import torch
+    rs = np.random.RandomState(SEED)
+    sizes = rs.multinomial(1_000_000 - 50_000, np.ones(50_000) / 50_000) + 1
+    zst = np.concatenate(([0], np.cumsum(sizes - 1)[:-1])).astype(np.int64)
+    nz = int((sizes - 1).sum())
+    y = rs.randn(nz)
+    ref = y.copy(); orc.isotonic_regression_multi_c(ref, zst)
+    yd = torch.from_numpy(y).cuda()
+    cx.isotonic_regression_multi_c(yd, torch.from_numpy(zst).cuda())
+    assert exact(yd.cpu().numpy(), ref)
+
+
+def test_isotonic_weight_semantics(cx):
+    # an int32 contiguous weight array is updated in place; int64 is copied
+    y = np.array([4., 5., 1., 6., 8., 7.])
+    w32 = np.ones(6, dtype=np.int32)
+    cx.isotonic_regression_multi_c(y, np.array([0]), w32, 0)
+    assert list(w32[[0, 3, 4]]) == [3, 1, 2]
+    w64 = np.ones(6, dtype=np.int64)
+    cx.isotonic_regression_multi_c(np.array([4., 5., 1., 6., 8., 7.]), np.array([0]), w64, 0)
+    assert list(w64) == [1] * 6
+
+
+# ------------------------------------------------------------------ x<->z, QP
+
+def test_xz_quad_golden(cx, golden):
+    G = golden('xz_quad.npz')
+    for ci in range(int(G['nxz'])):
+        x, b, zt = G['c%d_x' % ci], G['c%d_blocks' % ci], G['c%d_z' % ci]
+        z = np.zeros_like(zt)
+        cx.x2z_c(x, z, b)
+        assert exact(z, zt)
+        xb = np.zeros_like(x)
+        cx.z2x_c(xb, z, b)
+        assert exact(xb, G['c%d_xback' % ci])
+    for qi in range(int(G['nquad'])):
+        x, Q, c = G['q%d_x' % qi], G['q%d_Q' % qi], G['q%d_c' % qi]
+        g = np.zeros_like(x)
+        f = cx.quad_obj_c(x, Q.flatten(), c, g)
+        assert exact(g, G['q%d_g' % qi]) and f == float(G['q%d_f' % qi])
+
+
+def test_line_search_vs_oracle(cx, orc):
+    rs = np.random.RandomState(SEED)
+    Q = (2 * np.array([[2, .5], [.5, 1]])).flatten()
+    c = np.array([1.0, 1.0])
+    for x, f, g in [((.5, .5), 2., (3.5, 2.5)), ((.25, .75), 1.875, (2.75, 2.75)),
+                    ((.26, .74), 1.8752, (2.78, 2.74))]:
+        outs = []
+        for mod in (cx, orc):
+            xn, gn = np.array([0., 1.]), np.array([2., 3.])
+            fn = mod.line_search_quad_obj_c(np.array(x), f, np.array(g), xn, 2., gn, Q, c)
+            outs.append((fn, xn, gn))
+        assert outs[0][0] == outs[1][0] and exact(outs[0][1], outs[1][1]) and \
+            exact(outs[0][2], outs[1][2])
+    for n in (3, 17):
+        M = rs.randn(n, n); Qn = (M @ M.T).flatten(); cn = rs.randn(n)
+        x = rs.rand(n); g = np.zeros(n); f = orc.quad_obj_c(x, Qn, cn, g)
+        xn0 = x + rs.randn(n); gn0 = np.zeros(n); fn0 = orc.quad_obj_c(xn0, Qn, cn, gn0)
+        outs = []
+        for mod in (cx, orc):
+            xn, gn = xn0.copy(), gn0.copy()
+            fo = mod.line_search_quad_obj_c(x, f, g, xn, fn0, gn, Qn, cn)
+            outs.append((fo, xn, gn))
+        assert outs[0][0] == outs[1][0] and exact(outs[0][1], outs[1][1])
+        assert exact(outs[0][2], outs[1][2])
+
+
+# ------------------------------------------------------------------ SpMV
+
+@pytest.mark.parametrize('shape,per_row', [((1000, 3000), 40), ((5000, 800), 3), ((300, 300), 160)])
+def test_spmv_vs_scipy(cuda, shape, per_row):
+    import torch
+    from device import DeviceCSR
+    rs = np.random.RandomState(SEED)
+    m, n = shape
+    A = sps.random(m, n, density=min(1.0, per_row / n), random_state=rs, format='csr')
+    A.data = rs.randn(A.nnz)
+    x = rs.randn(n)
+    add = rs.randn(m)
+    D = DeviceCSR(A)
+    out, sq = D.matvec(torch.from_numpy(x).cuda(), add=torch.from_numpy(add).cuda(), want_sq=True)
+    ref = A.dot(x) + add
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-13, atol=1e-13)
+    assert abs(float(sq.item()) - ref.dot(ref)) <= 1e-12 * ref.dot(ref)
+    for G in (1, 2, 4, 8, 16, 32, 64):
+        D.group = G
+        o = D.matvec(torch.from_numpy(x).cuda())
+        np.testing.assert_allclose(o.cpu().numpy(), A.dot(x), rtol=1e-13, atol=1e-13)

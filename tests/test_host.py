@@ -1,0 +1,152 @@
+"""Host-side logic (CPU only): drop-in argument checking, data preparation and
+generators, pinned against the reference's fixtures."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sps
+
+from conftest import SEED
+
+
+# ------------------------------------------------ c_extensions argument checks
+# (they run before anything is launched, so they work without a GPU)
+
+@pytest.fixture(scope='module')
+def cx():
+    from c_extensions import c_extensions
+    return c_extensions
+
+
+def test_bad_indices_raise_assertion(cx):
+    # tests/fast/test_proj_simplex.py:36-42,54-59
+    y = np.random.rand(7)
+    for s, e in [(2, 8), (-1, 7), (-1, 4)]:
+        with pytest.raises(AssertionError):
+            cx.proj_simplex_c(y, s, e)
+        with pytest.raises(AssertionError):
+            cx.isotonic_regression_c(y, s, e)
+    for b in (np.array([-1, 2, 4]), np.array([1, 3, 7]), np.array([0, 4, 2])):
+        for fn in (cx.proj_multi_simplex_c, cx.proj_multi_ball_c, cx.isotonic_regression_multi_c,
+                   cx.isotonic_regression_multi_c_2, cx.isotonic_regression_multi_c_3):
+            with pytest.raises(AssertionError):
+                fn(y, b)
+    with pytest.raises(AssertionError):
+        cx.x2z_c(np.random.rand(5), np.zeros(3), np.array([1, 3]))   # blocks[0] must be 0
+
+
+def test_empty_range_is_a_no_op(cx):
+    y = np.random.rand(7)
+    y0 = y.copy()
+    assert cx.proj_simplex_c(y, 4, 4) is None
+    assert np.array_equal(y, y0)
+
+
+def test_buffer_typing(cx):
+    with pytest.raises(ValueError):
+        cx.proj_multi_simplex_c(np.arange(7), np.array([0, 2]))          # int y
+    with pytest.raises(ValueError):
+        cx.proj_multi_simplex_c(np.random.rand(7), np.array([0, 2], dtype=np.int32))
+    with pytest.raises(ValueError):
+        cx.proj_multi_simplex_c(np.random.rand(2, 7), np.array([0, 2]))
+    with pytest.raises(TypeError):
+        cx.proj_multi_simplex_c([0.1, 0.2], np.array([0]))
+
+
+def test_no_cpu_fallback(cx):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('a GPU is present')
+    with pytest.raises(RuntimeError, match='no HIP device'):
+        cx.proj_multi_simplex_c(np.random.rand(7), np.array([0, 2, 4]))
+
+
+# ------------------------------------------------ bsls_utils
+
+def test_particular_x0_kat():
+    from bsls_utils import particular_x0
+    assert list(particular_x0(np.array([1, 2, 3, 4]))) == [1, 0, 1, 0, 0, 1, 0, 0, 0, 1]
+
+
+def test_generate_data_matches_reference(golden):
+    import bsls_utils
+    G = golden('solvers.npz')
+    np.random.seed(SEED)
+    d = bsls_utils.generate_data()
+    for k in ('A', 'b', 'x_true', 'f', 'block_sizes'):
+        assert np.array_equal(np.asarray(d[k]), G['gen_%s' % k]), k
+    np.random.seed(SEED)
+    d = bsls_utils.generate_data(n=300, m1=40, m2=12, A_sparse=0.3, alpha=0.5)
+    for k in ('A', 'b', 'x_true', 'f', 'block_sizes'):
+        assert np.array_equal(np.asarray(d[k]), G['gen2_%s' % k]), k
+    assert abs(sum(d['f']) - sum(d['x_true'])) < 1e-10   # tests/fast/test_util.py:34-40
+
+
+def test_N_and_x2z_match_oracle(orc):
+    from bsls_utils import block_sizes_to_N, x2z
+    rs = np.random.RandomState(SEED)
+    bs = rs.randint(1, 9, size=50)
+    N1, N2 = block_sizes_to_N(bs), orc.block_sizes_to_N(bs)
+    assert (N1 != N2).nnz == 0
+    x = rs.rand(int(bs.sum()))
+    assert np.array_equal(x2z(x, bs), orc.x2z(x, bs))
+
+
+def test_bsls_matrices_matches_reference(golden, tmp_path):
+    """BSLSMatrices on the tests/fast/test_main.py .mat files reproduces the
+    matrices the reference's pipeline handed to solve_in_z."""
+    import bsls_utils
+    from bsls_matrices import BSLSMatrices
+    G = golden('solvers.npz')
+    for vi, kw in enumerate([{}, {'alpha': 0.5}, {'A_sparse': 0.05}]):
+        np.random.seed(SEED)
+        fname = os.path.join(str(tmp_path), 'test_main.mat')
+        bsls_utils.generate_data(fname=fname, **kw)
+        bm = BSLSMatrices(fname=fname, full=True, L=True, OD=True, CP=True, LP=True, eq='CP')
+        bm.degree_reduced_form()
+        AA, bb, N, bsz, x_split, nz, scaling, rsort, x0 = bm.get_LS()
+        AA = sps.csr_matrix(AA)
+        AA.sort_indices()
+        ref = sps.csr_matrix((G['main%d_A_data' % vi], G['main%d_A_indices' % vi],
+                              G['main%d_A_indptr' % vi]), shape=tuple(G['main%d_A_shape' % vi]))
+        ref.sort_indices()
+        assert AA.shape == ref.shape and (AA != ref).nnz == 0, vi
+        assert np.array_equal(bb, G['main%d_b' % vi])
+        assert np.array_equal(bsz, G['main%d_block_sizes' % vi])
+        assert np.array_equal(x_split, G['main%d_x_split' % vi])
+        assert np.array_equal(scaling, G['main%d_scaling' % vi])
+
+
+# ------------------------------------------------ synthetic generator + partition
+
+def test_synthetic_shard_properties():
+    from synthetic import make_shard
+    sh = make_shard(20_000, 1_000, 2_000, per_col=16, seed=1)
+    A, AT = sh['A'], sh['AT']
+    assert A.shape == (2_000, 20_000) and A.nnz == 16 * 20_000
+    assert (A.T.tocsr() != AT).nnz == 0
+    assert sh['block_sizes'].sum() == 20_000 and sh['block_sizes'].min() >= 1
+    # scaled incidence: one value per column; splits on the simplex
+    C = A.tocsc()
+    for j in range(0, 20_000, 997):
+        v = C.data[C.indptr[j]:C.indptr[j + 1]]
+        assert np.all(v == v[0]) and len(np.unique(C.indices[C.indptr[j]:C.indptr[j + 1]])) == 16
+    ends = np.cumsum(sh['block_sizes'])
+    sums = np.add.reduceat(sh['x_true'], ends - sh['block_sizes'])
+    assert np.allclose(sums, 1.0)
+    assert np.allclose(A.dot(sh['x_true']), sh['Ax'])
+    sh2 = make_shard(20_000, 1_000, 2_000, per_col=16, seed=1)
+    assert (sh2['A'] != A).nnz == 0                     # seeded
+
+
+def test_partition_blocks_balanced():
+    from distributed import partition_blocks
+    rs = np.random.RandomState(SEED)
+    bs = rs.multinomial(10_000 - 500, np.ones(500) / 500) + 1
+    for world in (1, 2, 3, 8):
+        bounds = partition_blocks(bs, bs * 16.0, world)
+        assert bounds[0] == 0 and bounds[-1] == 500 and np.all(np.diff(bounds) > 0)
+        loads = [bs[bounds[g]:bounds[g + 1]].sum() for g in range(world)]
+        assert max(loads) - min(loads) <= 2 * bs.max()
+    with pytest.raises(ValueError):
+        partition_blocks(bs, bs, 501)
