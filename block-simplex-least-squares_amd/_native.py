@@ -39,7 +39,9 @@ class BBProblem(ctypes.Structure):
     """Mirror of struct bsls_bb_problem (include/bsls_hip.h)."""
     _fields_ = [('m', _i64), ('n', _i64), ('nz', _i64), ('nblocks', _i64),
                 ('A_indptr', _vp), ('A_indices', _vp), ('A_data', _vp),
+                ('A_tiles', _vp), ('A_ntiles', _i64),
                 ('AT_indptr', _vp), ('AT_indices', _vp), ('AT_data', _vp),
+                ('AT_tiles', _vp), ('AT_ntiles', _i64),
                 ('target', _vp), ('xstarts', _vp), ('zstarts', _vp), ('xz', _vp),
                 ('z', _vp * 2), ('g', _vp * 2), ('x', _vp), ('r', _vp), ('scal', _vp),
                 ('work', _vp),
@@ -60,9 +62,11 @@ _SIGS = {
     'bsls_nt_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     'bsls_quad_obj': (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     'bsls_line_search': (_int, [_vp, _dbl, _vp, _vp, _dbl, _vp, _vp, _vp, _i64, _vp, _vp]),
+    'bsls_csr_plan_tiles': (_i64, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64]),
     'bsls_spmv_workspace_size': (_sz, [_i64]),
-    'bsls_csr_spmv': (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _dbl, _vp, _vp, _int, _vp, _sz, _vp]),
-    'bsls_bb_workspace_size': (_sz, [_i64, _i64, _i64]),
+    'bsls_csr_spmv': (_int, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _dbl, _vp, _vp, _int, _vp,
+                             _sz, _vp]),
+    'bsls_bb_workspace_size': (_sz, [_i64, _i64, _i64, _i64]),
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
@@ -134,6 +138,34 @@ def stream_handle(stream=None):
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def plan_tiles(indptr, nzt=2048, rmax=1024, ends=None):
+    """Row tiles for the CSR-stream kernels (bsls_csr_plan_tiles, host only)."""
+    import numpy as np
+    ip = np.ascontiguousarray(indptr, dtype=np.int64)
+    m = ip.shape[0] - 1
+    L = load()
+    e = None if ends is None else np.ascontiguousarray(ends, dtype=np.int64)
+    ep = ctypes.c_void_p(e.ctypes.data) if e is not None else ctypes.c_void_p(0)
+    ne = 0 if e is None else e.shape[0]
+    cnt = L.bsls_csr_plan_tiles(ctypes.c_void_p(ip.ctypes.data), m, nzt, rmax, ep, ne, None, 0)
+    if cnt < 0:
+        raise ValueError('tile planning failed (%d): a block spans more than %d rows'
+                         % (cnt, rmax))
+    out = np.zeros(cnt + 1, dtype=np.int64)
+    L.bsls_csr_plan_tiles(ctypes.c_void_p(ip.ctypes.data), m, nzt, rmax, ep, ne,
+                          ctypes.c_void_p(out.ctypes.data), cnt + 1)
+    return out
+
+
+def group_for_rows(mean_rows):
+    """Lanes per row in the tile reduce: the largest power of two with
+    G * mean_rows <= 256 (every thread of the tile busy)."""
+    g = 64
+    while g > 1 and g * mean_rows > 256:
+        g //= 2
+    return g
 
 
 def declared_symbols():

@@ -76,9 +76,13 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double *red) {
 // "Last workgroup reduces": every workgroup publishes NV partials; the
 // workgroup whose ticket add comes last sums all partials in index order
 // (deterministic) and returns true with the totals in thread 0's `tot`.
-// Protocol per cdna_hip_programming.md Guideline 16: plain partial stores ->
-// vmcnt(0) -> agent release -> relaxed agent ticket add; the last arriver does
-// one agent acquire -> vmcnt(0) -> barrier -> plain loads.  The ticket resets
+// Hand-off without fences (MI355X_MICROARCH.md "Valid forms", table row 1):
+// one lane stores the partials with agent-scope relaxed atomic stores (sc1,
+// write-through to the coherent level), drains them (vmcnt(0)), then adds to
+// the ticket (agent-scope atomic); the last arriver -- told by the value its
+// add returned -- reads every partial with sc1 loads, after a workgroup
+// barrier.  An agent release fence per workgroup (buffer_wbl2) measured
+// ~1 ms extra on a 25k-workgroup SpMV, so none is used.  The ticket resets
 // itself (kernel-boundary ordered for the next launch).
 template <int NV>
 __device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsigned *ticket,
@@ -86,9 +90,9 @@ __device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsig
     __shared__ int am_last;
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int k = 0; k < NV; ++k) partials[(size_t)blockIdx.x * NV + k] = mine[k];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        for (int k = 0; k < NV; ++k)
+            __hip_atomic_store(&partials[(size_t)blockIdx.x * NV + k], mine[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
@@ -96,17 +100,15 @@ __device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsig
     }
     __syncthreads();
     if (!am_last) return false;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep loads below the ticket
     double acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] = 0.0;
     for (unsigned i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
 #pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] += partials[(size_t)i * NV + k];
+        for (int k = 0; k < NV; ++k)
+            acc[k] += __hip_atomic_load(&partials[(size_t)i * NV + k], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
     }
     block_sum<NV>(acc, red);
     if (threadIdx.x == 0) {

@@ -197,10 +197,8 @@ __global__ __launch_bounds__(256) void md_kernel(double *__restrict__ x,
         mine[0] = m;
     }
     __shared__ int am_last;
-    if (threadIdx.x == 0) {
-        part[blockIdx.x] = mine[0];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (threadIdx.x == 0) {   // sc1 hand-off, as bsls_common.hpp last_block_sum
+        __hip_atomic_store(&part[blockIdx.x], mine[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         am_last = (prev == gridDim.x - 1);
@@ -208,10 +206,11 @@ __global__ __launch_bounds__(256) void md_kernel(double *__restrict__ x,
     __syncthreads();
     if (!am_last) return;
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         double m = 0.0;
-        for (unsigned i = 0; i < gridDim.x; ++i) m = part[i] > m ? part[i] : m;
+        for (unsigned i = 0; i < gridDim.x; ++i) {
+            const double v = __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            m = v > m ? v : m;
+        }
         *dxinf = m;
         *ticket = 0u;
     }

@@ -44,10 +44,18 @@ __device__ __forceinline__ void bitonic_desc(double (&v)[N]) {
             for (int i = 0; i < N; ++i) {
                 const int l = i ^ j;
                 if (l > i) {
-                    const double a = v[i], b = v[l];
-                    const double hi = fmax(a, b), lo = fmin(a, b);
-                    if ((i & k) == 0) { v[i] = hi; v[l] = lo; }
-                    else { v[i] = lo; v[l] = hi; }
+                    // in-place compare-exchange with one temporary: written as
+                    // asm so the scheduler cannot stretch a stage's live ranges
+                    // (plain fmax/fmin needed 255 VGPRs at N = 64, this 141)
+                    double t;
+                    if ((i & k) == 0)
+                        asm volatile(
+                            "v_max_f64 %0, %1, %2\n\tv_min_f64 %2, %1, %2\n\tv_mov_b64 %1, %0"
+                            : "=&v"(t), "+v"(v[i]), "+v"(v[l]));
+                    else
+                        asm volatile(
+                            "v_min_f64 %0, %1, %2\n\tv_max_f64 %2, %1, %2\n\tv_mov_b64 %1, %0"
+                            : "=&v"(t), "+v"(v[i]), "+v"(v[l]));
                 }
             }
         }
@@ -93,6 +101,7 @@ __device__ __forceinline__ void lane_block(double *__restrict__ y, int64_t s, in
     }
     bitonic_desc<N>(v);
     const double lam = lambda_sorted<N>(v, k);
+    asm volatile("" ::: "memory");   // re-read y after the sort, do not hoist
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         if (j < k) {

@@ -1,30 +1,34 @@
 // spmv.hip -- CSR sparse matrix-vector product (replaces SciPy csr_matvec behind
-// A.dot(x), python/main.py:53-54; python/mirror_descent.py:32-34).
+// A.dot(x), python/main.py:53-54; python/mirror_descent.py:32-34) and the host
+// tile planner shared with the fused BB kernels.
 //
-// G lanes per row (G = power of two <= 64, ~ the mean row length): the row's
-// values and column indices stream coalesced across the group, x is gathered,
-// the group sums by xor-shuffles (fixed tree).  HBM-bound: 12 B per nonzero +
-// 8 B per row of output; the x gather is served mostly by L2 / Infinity Cache.
+// HBM-bound: 12 B per nonzero (fp64 value + int32 index) + 8 B per row of
+// output + the x gather.  One workgroup per host-planned tile (spmv.hpp).
+#include <algorithm>
+#include <vector>
+
 #include "spmv.hpp"
 
 namespace bsls {
 
 template <int G>
-__global__ __launch_bounds__(256) void csr_spmv_kernel(
-    int64_t m, const int64_t *__restrict__ indptr, const int32_t *__restrict__ indices,
-    const double *__restrict__ data, const double *__restrict__ x,
-    const double *__restrict__ add, double alpha, double *__restrict__ out,
-    double *__restrict__ part, unsigned *__restrict__ ticket, double *__restrict__ sq_out) {
-    constexpr int RPB = 256 / G;
+__global__ __launch_bounds__(TB) void csr_spmv_tiles(
+    const int64_t *__restrict__ tiles, const int64_t *__restrict__ indptr,
+    const int32_t *__restrict__ indices, const double *__restrict__ data,
+    const double *__restrict__ x, const double *__restrict__ add, double alpha,
+    double *__restrict__ out, double *__restrict__ part, unsigned *__restrict__ ticket,
+    double *__restrict__ sq_out) {
+    __shared__ double prod[NZT];
+    __shared__ double wl[RMAX];
     __shared__ double red[4];
-    const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / G;
-    const double v = csr_row_dot<G>(row, m, indptr, indices, data, x);
+    const int64_t r0 = tiles[blockIdx.x], r1 = tiles[blockIdx.x + 1];
+    tile_rows<G>(indptr, indices, data, x, r0, r1, prod, wl);
     double sq[1] = {0.0};
-    if (row < m && (threadIdx.x % G) == 0) {
-        double o = (alpha == 1.0) ? v : alpha * v;
-        if (add) o += add[row];
-        out[row] = o;
-        sq[0] = o * o;
+    for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
+        double o = (alpha == 1.0) ? wl[t] : alpha * wl[t];
+        if (add) o += add[r0 + t];
+        out[r0 + t] = o;
+        sq[0] += o * o;
     }
     if (!sq_out) return;
     block_sum<1>(sq, red);
@@ -32,41 +36,83 @@ __global__ __launch_bounds__(256) void csr_spmv_kernel(
     if (last_block_sum<1>(sq, part, ticket, tot, red) && threadIdx.x == 0) *sq_out = tot[0];
 }
 
-template <int G>
-static void launch_spmv(int64_t m, const int64_t *ip, const int32_t *ix, const double *d,
-                        const double *x, const double *add, double alpha, double *out,
-                        double *part, unsigned *ticket, double *sq, hipStream_t st) {
-    constexpr int RPB = 256 / G;
-    csr_spmv_kernel<G><<<grid_for(m, RPB), 256, 0, st>>>(m, ip, ix, d, x, add, alpha, out, part,
-                                                         ticket, sq);
+// Greedy tiles of whole rows: <= nzt nonzeros (unless one row alone is longer)
+// and <= rmax rows; when `ends` is given a tile may only end at one of those
+// row indices (used to keep z-blocks inside one tile for the fused N').
+static int64_t plan_tiles(const int64_t *indptr, int64_t m, int64_t nzt, int64_t rmax,
+                          const int64_t *ends, int64_t nends, int64_t *out, int64_t cap) {
+    std::vector<int64_t> allowed;
+    if (ends) {
+        allowed.assign(ends, ends + nends);
+        std::sort(allowed.begin(), allowed.end());
+        if (allowed.empty() || allowed.back() != m) allowed.push_back(m);
+    }
+    int64_t cnt = 0;
+    if (cap > 0) out[0] = 0;
+    int64_t r0 = 0;
+    while (r0 < m) {
+        // largest r with indptr[r] - indptr[r0] <= nzt
+        const int64_t lim = indptr[r0] + nzt;
+        int64_t r = std::upper_bound(indptr + r0, indptr + m + 1, lim) - indptr - 1;
+        if (r > r0 + rmax) r = r0 + rmax;
+        if (r > m) r = m;
+        int64_t r1;
+        if (ends) {
+            auto it = std::upper_bound(allowed.begin(), allowed.end(), r);
+            // last allowed end <= r that is > r0, else the first allowed end > r0
+            if (it != allowed.begin() && *(it - 1) > r0) r1 = *(it - 1);
+            else r1 = *std::upper_bound(allowed.begin(), allowed.end(), r0);
+        } else {
+            r1 = (r > r0) ? r : r0 + 1;
+        }
+        if (r1 - r0 > rmax) return -2;   // a block longer than rmax rows (fused N' limit)
+        ++cnt;
+        if (cnt < cap) out[cnt] = r1;
+        r0 = r1;
+    }
+    return cnt;
 }
 
 }  // namespace bsls
 
 using namespace bsls;
 
-extern "C" size_t bsls_spmv_workspace_size(int64_t m) {
-    return 16 + (size_t)(((m + 3) / 4 + 1) * 8);
+extern "C" int64_t bsls_csr_plan_tiles(const int64_t *indptr, int64_t m, int64_t nzt,
+                                       int64_t rmax, const int64_t *ends, int64_t nends,
+                                       int64_t *tiles_out, int64_t cap) {
+    if (!indptr || m <= 0) return -1;
+    if (nzt <= 0) nzt = NZT;
+    if (rmax <= 0 || rmax > RMAX) rmax = RMAX;
+    return plan_tiles(indptr, m, nzt, rmax, ends, nends, tiles_out, cap);
+}
+
+extern "C" size_t bsls_spmv_workspace_size(int64_t ntiles) {
+    return 16 + (size_t)((ntiles + 1) * 8);
 }
 
 extern "C" int bsls_csr_spmv(int64_t m, const int64_t *d_indptr, const int32_t *d_indices,
-                             const double *d_data, const double *d_x, const double *d_add,
-                             double alpha, double *d_out, double *d_sq_out, int group,
-                             void *d_work, size_t work_bytes, void *stream) {
-    if (m <= 0 || !d_indptr || !d_x || !d_out) return BSLS_E_ARG;
-    if (d_sq_out && (!d_work || work_bytes < bsls_spmv_workspace_size(m))) return BSLS_E_WORKSPACE;
+                             const double *d_data, const int64_t *d_tiles, int64_t ntiles,
+                             const double *d_x, const double *d_add, double alpha,
+                             double *d_out, double *d_sq_out, int group, void *d_work,
+                             size_t work_bytes, void *stream) {
+    if (m <= 0 || !d_indptr || !d_tiles || ntiles <= 0 || !d_x || !d_out) return BSLS_E_ARG;
+    if (d_sq_out && (!d_work || work_bytes < bsls_spmv_workspace_size(ntiles)))
+        return BSLS_E_WORKSPACE;
     unsigned *ticket = d_work ? (unsigned *)d_work : nullptr;
     double *part = d_work ? (double *)((char *)d_work + 16) : nullptr;
     hipStream_t st = (hipStream_t)stream;
+    const int grid = (int)ntiles;
     switch (group) {
-        case 1: launch_spmv<1>(m, d_indptr, d_indices, d_data, d_x, d_add, alpha, d_out, part, ticket, d_sq_out, st); break;
-        case 2: launch_spmv<2>(m, d_indptr, d_indices, d_data, d_x, d_add, alpha, d_out, part, ticket, d_sq_out, st); break;
-        case 4: launch_spmv<4>(m, d_indptr, d_indices, d_data, d_x, d_add, alpha, d_out, part, ticket, d_sq_out, st); break;
-        case 8: launch_spmv<8>(m, d_indptr, d_indices, d_data, d_x, d_add, alpha, d_out, part, ticket, d_sq_out, st); break;
-        case 16: launch_spmv<16>(m, d_indptr, d_indices, d_data, d_x, d_add, alpha, d_out, part, ticket, d_sq_out, st); break;
-        case 32: launch_spmv<32>(m, d_indptr, d_indices, d_data, d_x, d_add, alpha, d_out, part, ticket, d_sq_out, st); break;
-        case 64: launch_spmv<64>(m, d_indptr, d_indices, d_data, d_x, d_add, alpha, d_out, part, ticket, d_sq_out, st); break;
-        default: return BSLS_E_ARG;
+#define SPMV_CASE(G)                                                                       \
+    case G:                                                                                \
+        csr_spmv_tiles<G><<<grid, TB, 0, st>>>(d_tiles, d_indptr, d_indices, d_data, d_x,   \
+                                               d_add, alpha, d_out, part, ticket, d_sq_out); \
+        break;
+        SPMV_CASE(1) SPMV_CASE(2) SPMV_CASE(4) SPMV_CASE(8) SPMV_CASE(16) SPMV_CASE(32)
+        SPMV_CASE(64)
+#undef SPMV_CASE
+        default:
+            return BSLS_E_ARG;
     }
     BSLS_LAUNCH_CHECK();
     return BSLS_OK;

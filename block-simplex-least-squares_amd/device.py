@@ -27,18 +27,12 @@ def _torch():
     return torch
 
 
-def pick_group(mean_row):
-    """Lanes per CSR row: the power of two nearest the mean row length, 4..64."""
-    g = 4
-    while g < 64 and g * 1.5 < mean_row:
-        g *= 2
-    return g
-
-
 class DeviceCSR:
-    """A CSR matrix resident in HBM (int64 indptr, int32 indices, fp64 data)."""
+    """A CSR matrix resident in HBM (int64 indptr, int32 indices, fp64 data) plus
+    its CSR-stream row tiles (<= 2048 nonzeros, <= 1024 rows each; with
+    `tile_ends` tiles end only at those rows)."""
 
-    def __init__(self, A, group=None):
+    def __init__(self, A, tile_ends=None, group=None):
         torch = _torch()
         A = sps.csr_matrix(A)
         A.sort_indices()
@@ -47,10 +41,14 @@ class DeviceCSR:
         self.nnz = int(A.nnz)
         if self.n >= 2 ** 31:
             raise ValueError('column count exceeds int32 indices; shard the columns')
-        self.indptr = torch.from_numpy(A.indptr.astype(np.int64)).cuda()
+        ip = A.indptr.astype(np.int64)
+        self.indptr = torch.from_numpy(ip).cuda()
         self.indices = torch.from_numpy(A.indices.astype(np.int32)).cuda()
         self.data = torch.from_numpy(A.data.astype(np.float64)).cuda()
-        self.group = group or pick_group(self.nnz / max(self.m, 1))
+        tiles = _native.plan_tiles(ip, ends=tile_ends)
+        self.ntiles = int(tiles.shape[0] - 1)
+        self.tiles = torch.from_numpy(tiles).cuda()
+        self.group = group or _native.group_for_rows(self.m / max(self.ntiles, 1))
         self._work = None
 
     def matvec(self, x, out=None, add=None, alpha=1.0, want_sq=False):
@@ -62,12 +60,12 @@ class DeviceCSR:
             out = torch.empty(self.m, dtype=torch.float64, device='cuda')
         sq = torch.zeros(1, dtype=torch.float64, device='cuda') if want_sq else None
         if self._work is None:
-            self._work = torch.zeros(L.bsls_spmv_workspace_size(self.m), dtype=torch.uint8,
+            self._work = torch.zeros(L.bsls_spmv_workspace_size(self.ntiles), dtype=torch.uint8,
                                      device='cuda')
         check(L.bsls_csr_spmv(self.m, ptr(self.indptr), ptr(self.indices), ptr(self.data),
-                              ptr(x), ptr(add), float(alpha), ptr(out), ptr(sq), self.group,
-                              ptr(self._work), self._work.numel(), stream_handle()),
-              'bsls_csr_spmv')
+                              ptr(self.tiles), self.ntiles, ptr(x), ptr(add), float(alpha),
+                              ptr(out), ptr(sq), self.group, ptr(self._work), self._work.numel(),
+                              stream_handle()), 'bsls_csr_spmv')
         return (out, sq) if want_sq else out
 
 
@@ -113,7 +111,9 @@ class BBEngine:
         if A.shape[1] != lay.n:
             raise ValueError('A has %d columns but the blocks cover %d' % (A.shape[1], lay.n))
         self.A = A_dev or DeviceCSR(A)
-        self.AT = AT_dev or DeviceCSR(AT if AT is not None else A.T.tocsr())
+        # A' tiles end at x-block ends: the fused N' difference stays in LDS
+        self.AT = AT_dev or DeviceCSR(AT if AT is not None else A.T.tocsr(),
+                                      tile_ends=np.cumsum(lay.sizes))
         self.m, self.n, self.nz = A.shape[0], lay.n, lay.nz
         opts = options or {}
         self.options = dict(opts)
@@ -138,15 +138,18 @@ class BBEngine:
         self.x = torch.empty(lay.n, **dev)
         self.r = torch.empty(self.m, **dev)
         self.scal = torch.zeros(_native.S_COUNT, **dev)
-        self.work = torch.zeros(L.bsls_bb_workspace_size(self.m, self.n, self.nz),
+        self.work = torch.zeros(L.bsls_bb_workspace_size(self.m, self.n, self.nz,
+                                                         max(self.A.ntiles, self.AT.ntiles)),
                                 dtype=torch.uint8, device='cuda')
         P = BBProblem()
         P.m, P.n, P.nz, P.nblocks = self.m, lay.n, lay.nz, lay.p
         P.A_indptr, P.A_indices, P.A_data = (self.A.indptr.data_ptr(),
                                              self.A.indices.data_ptr(), self.A.data.data_ptr())
+        P.A_tiles, P.A_ntiles = self.A.tiles.data_ptr(), self.A.ntiles
         P.AT_indptr, P.AT_indices, P.AT_data = (self.AT.indptr.data_ptr(),
                                                 self.AT.indices.data_ptr(),
                                                 self.AT.data.data_ptr())
+        P.AT_tiles, P.AT_ntiles = self.AT.tiles.data_ptr(), self.AT.ntiles
         P.target = self.target.data_ptr()
         P.xstarts, P.zstarts, P.xz = (lay.xstarts.data_ptr(), lay.zstarts.data_ptr(),
                                       lay.xz.data_ptr())
@@ -158,8 +161,8 @@ class BBEngine:
         P.max_iter = int(opts.get('max_iter', 300000))
         P.opt_tol = float(opts.get('opt_tol', 1e-6))
         P.early_exit = 1 if early_exit else 0
-        P.a_group = min(max(self.A.group, 4), 64)
-        P.at_group = min(max(self.AT.group, 2), 32)
+        P.a_group = self.A.group
+        P.at_group = self.AT.group
         self.P = P
         self.z0 = None
 

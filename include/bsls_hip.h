@@ -88,15 +88,23 @@ int bsls_line_search(const double *d_x, double f, const double *d_g, double *d_x
  * Replaces scipy csr_matvec behind A.dot(x) (python/main.py:53-54,
  * python/algorithm_utils.py:91-92, python/mirror_descent.py:32-34):
  *   d_out[r] = sum_e data[e] * x[indices[e]]  (+ d_add[r] if d_add)  (* 1 if alpha == 1)
- * int64 row pointers, int32 column indices, fp64 values.  `group` = lanes per
- * row (power of two 1..64; pick ~ the mean row length).  If d_sq_out is
+ * int64 row pointers, int32 column indices, fp64 values, one workgroup per
+ * host-planned tile (bsls_csr_plan_tiles); `group` = lanes per row in the
+ * reduce (power of two 1..64, ~ 256 / rows per tile).  If d_sq_out is
  * non-NULL it receives sum_r d_out[r]^2 (deterministic tree order).
  * The product is alpha * (A x) (alpha == 1.0: no scaling multiply). */
-size_t bsls_spmv_workspace_size(int64_t m);
+/* Host-side planner (no GPU): split rows [0, m) into tiles of whole rows with
+ * <= nzt nonzeros (a single longer row gets its own tile) and <= rmax rows;
+ * with `ends` (sorted or not) tiles end only at those row indices.  Writes
+ * up to cap+1 row starts into tiles_out (host memory) and returns the tile
+ * count (call once with cap = 0 to size), -2 if a forced tile exceeds rmax. */
+int64_t bsls_csr_plan_tiles(const int64_t *indptr, int64_t m, int64_t nzt, int64_t rmax,
+                            const int64_t *ends, int64_t nends, int64_t *tiles_out, int64_t cap);
+size_t bsls_spmv_workspace_size(int64_t ntiles);
 int bsls_csr_spmv(int64_t m, const int64_t *d_indptr, const int32_t *d_indices,
-                  const double *d_data, const double *d_x, const double *d_add, double alpha,
-                  double *d_out, double *d_sq_out, int group, void *d_work, size_t work_bytes,
-                  void *stream);
+                  const double *d_data, const int64_t *d_tiles, int64_t ntiles,
+                  const double *d_x, const double *d_add, double alpha, double *d_out,
+                  double *d_sq_out, int group, void *d_work, size_t work_bytes, void *stream);
 
 /* ---- fused z-space Barzilai-Borwein engine ----------------------------------
  * Replaces, per iteration, BB.solve's loop body (python/BB.py:17-41) over the
@@ -134,9 +142,13 @@ typedef struct bsls_bb_problem {
     const int64_t *A_indptr;        /* m+1 */
     const int32_t *A_indices;       /* nnz */
     const double *A_data;           /* nnz */
+    const int64_t *A_tiles;         /* A_ntiles+1 row starts (bsls_csr_plan_tiles) */
+    int64_t A_ntiles;
     const int64_t *AT_indptr;       /* n+1 (CSR of A transposed) */
     const int32_t *AT_indices;
     const double *AT_data;
+    const int64_t *AT_tiles;        /* tiles of A' that END AT x-BLOCK ENDS (fused N') */
+    int64_t AT_ntiles;
     const double *target;           /* m: A x0 - b (python/main.py:48) */
     const int64_t *xstarts;         /* nblocks, x-space block starts, xstarts[0] = 0 */
     const int64_t *zstarts;         /* nblocks, z-space block starts (xstarts[b] - b) */
@@ -146,15 +158,15 @@ typedef struct bsls_bb_problem {
     double *x;                      /* n: N z of the current iterate (x0 is in target) */
     double *r;                      /* m: residual */
     double *scal;                   /* BSLS_S_COUNT doubles */
-    void *work;                     /* bsls_bb_workspace_size() bytes, zeroed once */
+    void *work;                     /* bsls_bb_workspace_size() bytes */
     int64_t max_zblock;             /* largest z-block (x-block size - 1) */
     int64_t max_iter;               /* options['max_iter'] */
     double opt_tol;                 /* options['opt_tol'] */
     int32_t early_exit;             /* 0 disables every early exit (fixed-count timing) */
-    int32_t a_group, at_group;      /* lanes per CSR row for A and A' (power of 2, <= 64) */
+    int32_t a_group, at_group;      /* lanes per row in the tile reduce (power of 2, <= 64) */
 } bsls_bb_problem;
 
-size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
+size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz, int64_t max_tiles);
 /* BB.py:14-15 and the first f(z0): resets scal/tickets, g[0] = grad(z0 + 1),
  * r = r(z0), scal[FX] = f(z0).  z[0] must hold z0. */
 int bsls_bb_prologue(const bsls_bb_problem *p, void *stream);

@@ -47,14 +47,33 @@ def test_host_only_entry_points(native):
     assert L.bsls_proj_workspace_size(3_200_000, 100_000, 60) > 0
     assert L.bsls_proj_workspace_size(100, 2, 50) < L.bsls_proj_workspace_size(100_000, 2, 50_000)
     assert L.bsls_isotonic_workspace_size(1000) >= 4000
-    assert L.bsls_bb_workspace_size(100_000, 1_000_000, 950_000) > 4 * 950_000
-    assert L.bsls_spmv_workspace_size(100_000) > 8 * 25_000
+    assert L.bsls_bb_workspace_size(100_000, 1_000_000, 950_000, 8000) > 4 * 950_000
+    assert L.bsls_spmv_workspace_size(8000) > 8 * 8000
     assert L.bsls_md_workspace_size(50_000) > 0
 
 
 def test_bb_struct_layout_matches_header(native):
-    # struct bsls_bb_problem: 4 int64, 10 + 2 + 2 + 4 pointers, 2 int64, 1 double, 3 int32
-    assert ctypes.sizeof(native.BBProblem) == 8 * 4 + 8 * 18 + 8 * 2 + 8 + 4 * 3 + 4
+    # struct bsls_bb_problem: 4 int64; A (3 ptr + tiles ptr + int64); A' (same);
+    # 4 ptr; z[2], g[2], x, r, scal, work; 2 int64; 1 double; 3 int32 (+ pad)
+    assert ctypes.sizeof(native.BBProblem) == 32 + 40 + 40 + 32 + 64 + 16 + 8 + 12 + 4
+
+
+def test_tile_planner(native):
+    import numpy as np
+    rs = np.random.RandomState(1)
+    lens = rs.poisson(16, size=5000)
+    lens[100] = 10_000                                   # one long row
+    ip = np.concatenate(([0], np.cumsum(lens))).astype(np.int64)
+    t = native.plan_tiles(ip)
+    assert t[0] == 0 and t[-1] == 5000 and np.all(np.diff(t) > 0)
+    nnz = ip[t[1:]] - ip[t[:-1]]
+    rows = np.diff(t)
+    assert np.all((nnz <= 2048) | (rows == 1)) and np.all(rows <= 1024)
+    ends = np.cumsum(rs.randint(1, 40, size=400))
+    ends = ends[ends < 5000]
+    t2 = native.plan_tiles(ip, ends=ends)
+    assert set(t2[1:-1]) <= set(ends.tolist())
+    assert native.group_for_rows(12.8) == 16 and native.group_for_rows(128) == 2
 
 
 def test_invalid_arguments_rejected_without_launch(native):
