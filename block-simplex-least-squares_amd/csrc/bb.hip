@@ -41,9 +41,9 @@ static BBWork bb_layout(void *base, int64_t m, int64_t nz, int64_t max_tiles) {
     char *p = (char *)base;
     size_t off = 0;
     w.tk1 = (unsigned *)(p + off);
-    w.tk2 = (unsigned *)(p + off + 16);
-    w.tkf = (unsigned *)(p + off + 32);
-    off += 64;
+    w.tk2 = (unsigned *)(p + off + TICKET_BYTES);
+    w.tkf = (unsigned *)(p + off + 2 * TICKET_BYTES);
+    off += al16(3 * TICKET_BYTES);
     w.p1 = (double *)(p + off);
     off += al16((size_t)(max_tiles + 1) * 8);
     w.p2 = (double *)(p + off);
@@ -98,14 +98,16 @@ __global__ __launch_bounds__(TB) void bb_k1(bsls_bb_problem P, int64_t iter, dou
     __shared__ double wl[RMAX];
     __shared__ double red[4];
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
-    const int64_t r0 = P.A_tiles[blockIdx.x], r1 = P.A_tiles[blockIdx.x + 1];
-    tile_rows<G>(P.A_indptr, P.A_indices, P.A_data, P.x, r0, r1, prod, wl);
     double sq[1] = {0.0};
-    for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
-        double o = wl[t];
-        if (ADD) o += P.target[r0 + t];
-        P.r[r0 + t] = o;
-        sq[0] += o * o;
+    for (int64_t tile = blockIdx.x; tile < P.A_ntiles; tile += gridDim.x) {
+        const int64_t r0 = P.A_tiles[tile], r1 = P.A_tiles[tile + 1];
+        tile_rows<G>(P.A_indptr, P.A_indices, P.A_data, P.x, r0, r1, prod, wl);
+        for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
+            double o = wl[t];
+            if (ADD) o += P.target[r0 + t];
+            P.r[r0 + t] = o;
+            sq[0] += o * o;
+        }
     }
     if (!REDUCE) return;
     block_sum<1>(sq, red);
@@ -145,21 +147,23 @@ __global__ __launch_bounds__(TB) void bb_k2(bsls_bb_problem P, const double *__r
     __shared__ double wl[RMAX];
     __shared__ double red[16];
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
-    const int64_t r0 = P.AT_tiles[blockIdx.x], r1 = P.AT_tiles[blockIdx.x + 1];
-    tile_rows<G>(P.AT_indptr, P.AT_indices, P.AT_data, P.r, r0, r1, prod, wl);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
-        const int32_t j = P.xz[r0 + t];
-        if (j >= 0) {
-            const double g = wl[t] - wl[t + 1];
-            gout[j] = g;
-            if (ITER) {
-                const double dg = g - gp[j];
-                const double dz = zc[j] - zp[j];
-                acc[0] += dg;
-                acc[1] += dz * dg;
-                acc[2] += dg * dg;
-                acc[3] += g * g;
+    for (int64_t tile = blockIdx.x; tile < P.AT_ntiles; tile += gridDim.x) {
+        const int64_t r0 = P.AT_tiles[tile], r1 = P.AT_tiles[tile + 1];
+        tile_rows<G>(P.AT_indptr, P.AT_indices, P.AT_data, P.r, r0, r1, prod, wl);
+        for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
+            const int32_t j = P.xz[r0 + t];
+            if (j >= 0) {
+                const double g = wl[t] - wl[t + 1];
+                gout[j] = g;
+                if (ITER) {
+                    const double dg = g - gp[j];
+                    const double dz = zc[j] - zp[j];
+                    acc[0] += dg;
+                    acc[1] += dz * dg;
+                    acc[2] += dg * dg;
+                    acc[3] += g * g;
+                }
             }
         }
     }
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(256) void bb_z2x(bsls_bb_problem P, const double *_
 
 template <bool ADD, bool REDUCE, bool ITER>
 static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, hipStream_t st) {
-    const int grid = (int)P.A_ntiles;
+    const int grid = (int)(P.A_ntiles < MAX_TILE_WG ? P.A_ntiles : MAX_TILE_WG);
     switch (P.a_group) {
 #define K1CASE(G)                                                               \
     case G:                                                                     \
@@ -309,7 +313,7 @@ static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, h
 template <bool ITER>
 static void launch_k2(const bsls_bb_problem &P, const double *zc, const double *zp,
                       const double *gp, double *gout, const BBWork &w, hipStream_t st) {
-    const int grid = (int)P.AT_ntiles;
+    const int grid = (int)(P.AT_ntiles < MAX_TILE_WG ? P.AT_ntiles : MAX_TILE_WG);
     switch (P.at_group) {
 #define K2CASE(G)                                                               \
     case G:                                                                     \
@@ -357,7 +361,7 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
     switch (stage) {
         case 0:  // reset scalars and tickets
             BSLS_CHECK(hipMemsetAsync(P.scal, 0, BSLS_S_COUNT * sizeof(double), st));
-            BSLS_CHECK(hipMemsetAsync(P.work, 0, 64, st));
+            BSLS_CHECK(hipMemsetAsync(P.work, 0, al16(3 * TICKET_BYTES), st));
             return BSLS_OK;
         case 1:  // r_partial = A_g x_g
             if (iter > 0) launch_k1<false, false, true>(P, iter, w, st);

@@ -76,16 +76,24 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double *red) {
 // "Last workgroup reduces": every workgroup publishes NV partials; the
 // workgroup whose ticket add comes last sums all partials in index order
 // (deterministic) and returns true with the totals in thread 0's `tot`.
+//
 // Hand-off without fences (MI355X_MICROARCH.md "Valid forms", table row 1):
-// one lane stores the partials with agent-scope relaxed atomic stores (sc1,
-// write-through to the coherent level), drains them (vmcnt(0)), then adds to
-// the ticket (agent-scope atomic); the last arriver -- told by the value its
-// add returned -- reads every partial with sc1 loads, after a workgroup
-// barrier.  An agent release fence per workgroup (buffer_wbl2) measured
-// ~1 ms extra on a 25k-workgroup SpMV, so none is used.  The ticket resets
-// itself (kernel-boundary ordered for the next launch).
+// one lane stores the partials with agent-scope relaxed atomic stores (sc1),
+// drains them (vmcnt(0)), then adds to a ticket (agent-scope atomic); the last
+// arriver -- told by the value its add returned -- reads every partial with
+// sc1 loads after a workgroup barrier.  (An agent release fence per workgroup,
+// buffer_wbl2, measured ~1 ms extra on a 25k-workgroup SpMV.)
+//
+// Tickets are sharded 8 ways by blockIdx % 8 (the XCD group label; speed only,
+// correctness never depends on placement) plus one top-level ticket, each on
+// its own 64-B line: one device-scope word saturates near 88 adds/us (price
+// list "dequeue"), which 7.8k arrivals turned into ~90 us.  `tickets` points
+// at TICKET_BYTES of zeroed memory; the last arriver re-zeroes it.
+constexpr int TICKET_STRIDE = 16;               // unsigned words = 64 B
+constexpr int TICKET_BYTES = 9 * TICKET_STRIDE * 4;
+
 template <int NV>
-__device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsigned *ticket,
+__device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsigned *tickets,
                                double (&tot)[NV], double *red) {
     __shared__ int am_last;
     if (threadIdx.x == 0) {
@@ -94,9 +102,18 @@ __device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsig
             __hip_atomic_store(&partials[(size_t)blockIdx.x * NV + k], mine[k], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-        am_last = (prev == gridDim.x - 1);
+        const unsigned shard = blockIdx.x & 7u;
+        const unsigned members = (gridDim.x - shard + 7u) / 8u;
+        const unsigned shards = gridDim.x < 8u ? gridDim.x : 8u;
+        unsigned prev = __hip_atomic_fetch_add(&tickets[shard * TICKET_STRIDE], 1u,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = 0;
+        if (prev == members - 1) {
+            prev = __hip_atomic_fetch_add(&tickets[8 * TICKET_STRIDE], 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+            last = (prev == shards - 1);
+        }
+        am_last = last;
     }
     __syncthreads();
     if (!am_last) return false;
@@ -114,7 +131,7 @@ __device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsig
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) tot[k] = acc[k];
-        *ticket = 0u;
+        for (int k = 0; k < 9; ++k) tickets[k * TICKET_STRIDE] = 0u;
     }
     return true;
 }

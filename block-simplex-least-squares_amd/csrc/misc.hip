@@ -274,7 +274,7 @@ extern "C" int bsls_line_search(const double *d_x, double f, const double *d_g, 
 
 extern "C" size_t bsls_md_workspace_size(int64_t nblocks) {
     const int64_t grid = (nblocks + 255) / 256;
-    return (size_t)(16 + ((grid * 8 + 15) & ~(int64_t)15));
+    return (size_t)(TICKET_BYTES + ((grid * 8 + 15) & ~(int64_t)15));
 }
 
 extern "C" int bsls_md_update(double *d_x, const double *d_g, const int64_t *d_starts,
@@ -283,7 +283,7 @@ extern "C" int bsls_md_update(double *d_x, const double *d_g, const int64_t *d_s
     if (nblocks <= 0 || n <= 0 || !d_x || !d_g || !d_starts || !d_dxinf) return BSLS_E_ARG;
     if (!d_work || work_bytes < bsls_md_workspace_size(nblocks)) return BSLS_E_WORKSPACE;
     unsigned *ticket = (unsigned *)d_work;
-    double *part = (double *)((char *)d_work + 16);
+    double *part = (double *)((char *)d_work + TICKET_BYTES);
     md_kernel<<<grid_for(nblocks, 256), 256, 0, (hipStream_t)stream>>>(
         d_x, d_g, d_starts, nblocks, n, step_scale, d_dxinf, part, ticket);
     BSLS_LAUNCH_CHECK();

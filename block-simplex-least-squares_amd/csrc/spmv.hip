@@ -13,7 +13,7 @@ namespace bsls {
 
 template <int G>
 __global__ __launch_bounds__(TB) void csr_spmv_tiles(
-    const int64_t *__restrict__ tiles, const int64_t *__restrict__ indptr,
+    const int64_t *__restrict__ tiles, int64_t ntiles, const int64_t *__restrict__ indptr,
     const int32_t *__restrict__ indices, const double *__restrict__ data,
     const double *__restrict__ x, const double *__restrict__ add, double alpha,
     double *__restrict__ out, double *__restrict__ part, unsigned *__restrict__ ticket,
@@ -21,14 +21,16 @@ __global__ __launch_bounds__(TB) void csr_spmv_tiles(
     __shared__ double prod[NZT];
     __shared__ double wl[RMAX];
     __shared__ double red[4];
-    const int64_t r0 = tiles[blockIdx.x], r1 = tiles[blockIdx.x + 1];
-    tile_rows<G>(indptr, indices, data, x, r0, r1, prod, wl);
     double sq[1] = {0.0};
-    for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
-        double o = (alpha == 1.0) ? wl[t] : alpha * wl[t];
-        if (add) o += add[r0 + t];
-        out[r0 + t] = o;
-        sq[0] += o * o;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tiles[tile], r1 = tiles[tile + 1];
+        tile_rows<G>(indptr, indices, data, x, r0, r1, prod, wl);
+        for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
+            double o = (alpha == 1.0) ? wl[t] : alpha * wl[t];
+            if (add) o += add[r0 + t];
+            out[r0 + t] = o;
+            sq[0] += o * o;
+        }
     }
     if (!sq_out) return;
     block_sum<1>(sq, red);
@@ -87,7 +89,7 @@ extern "C" int64_t bsls_csr_plan_tiles(const int64_t *indptr, int64_t m, int64_t
 }
 
 extern "C" size_t bsls_spmv_workspace_size(int64_t ntiles) {
-    return 16 + (size_t)((ntiles + 1) * 8);
+    return TICKET_BYTES + (size_t)((ntiles + 1) * 8);
 }
 
 extern "C" int bsls_csr_spmv(int64_t m, const int64_t *d_indptr, const int32_t *d_indices,
@@ -99,13 +101,13 @@ extern "C" int bsls_csr_spmv(int64_t m, const int64_t *d_indptr, const int32_t *
     if (d_sq_out && (!d_work || work_bytes < bsls_spmv_workspace_size(ntiles)))
         return BSLS_E_WORKSPACE;
     unsigned *ticket = d_work ? (unsigned *)d_work : nullptr;
-    double *part = d_work ? (double *)((char *)d_work + 16) : nullptr;
+    double *part = d_work ? (double *)((char *)d_work + TICKET_BYTES) : nullptr;
     hipStream_t st = (hipStream_t)stream;
-    const int grid = (int)ntiles;
+    const int grid = (int)(ntiles < MAX_TILE_WG ? ntiles : MAX_TILE_WG);
     switch (group) {
 #define SPMV_CASE(G)                                                                       \
     case G:                                                                                \
-        csr_spmv_tiles<G><<<grid, TB, 0, st>>>(d_tiles, d_indptr, d_indices, d_data, d_x,   \
+        csr_spmv_tiles<G><<<grid, TB, 0, st>>>(d_tiles, ntiles, d_indptr, d_indices, d_data, d_x,   \
                                                d_add, alpha, d_out, part, ticket, d_sq_out); \
         break;
         SPMV_CASE(1) SPMV_CASE(2) SPMV_CASE(4) SPMV_CASE(8) SPMV_CASE(16) SPMV_CASE(32)

@@ -16,6 +16,7 @@ namespace bsls {
 constexpr int TB = 256;        // threads per tile workgroup
 constexpr int NZT = 2048;      // nonzeros staged per chunk (16 KiB of products)
 constexpr int RMAX = 1024;     // rows per tile (capacity of wl)
+constexpr int MAX_TILE_WG = 1024;  // persistent grid: workgroups walk tiles round-robin
 
 template <int G>
 __device__ __forceinline__ void tile_rows(const int64_t *__restrict__ indptr,
@@ -24,6 +25,7 @@ __device__ __forceinline__ void tile_rows(const int64_t *__restrict__ indptr,
                                           const double *__restrict__ x, int64_t r0, int64_t r1,
                                           double *__restrict__ prod, double *__restrict__ wl) {
     const int nrows = (int)(r1 - r0);
+    __syncthreads();   // the previous tile's epilogue may still be reading wl
     for (int t = threadIdx.x; t < nrows; t += TB) wl[t] = 0.0;
     const int64_t e0 = indptr[r0], e1 = indptr[r1];
     const int gl = (int)(threadIdx.x % G);

@@ -9,11 +9,11 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 STEPS="${STEPS:-tests smoke bench prof}"
 
-fatal() {  # rc -> 0 if the next GPU step may run
-    case "$1" in
-        0|1) return 0 ;;
-        *) echo "step failed with rc=$1: stopping GPU work" | tee -a $OUT/status.txt; exit "$1" ;;
-    esac
+fatal() {  # timeouts (124/137), aborts (134), faults (139) and other signals end the session
+    if [ "$1" -eq 124 ] || [ "$1" -ge 128 ]; then
+        echo "step failed with rc=$1: stopping GPU work" | tee -a $OUT/status.txt; exit "$1"
+    fi
+    return 0
 }
 
 for s in $STEPS; do
@@ -34,6 +34,15 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
           -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline > $OUT/prof.log 2>&1
       rc=$?; echo "prof rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    pmc)
+      # one rocprofv3 pass per counter group (FETCH_SIZE and WRITE_SIZE cannot share a pass)
+      i=0
+      for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        i=$((i+1))
+        timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc \
+            -- python3 tools/kprof.py --iters 10 --proj 10 > $OUT/pmc$i.log 2>&1
+        rc=$?; echo "pmc$i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
+      done ;;
   esac
 done
 echo done | tee -a $OUT/status.txt
