@@ -38,15 +38,16 @@ _int = ctypes.c_int
 class BBProblem(ctypes.Structure):
     """Mirror of struct bsls_bb_problem (include/bsls_hip.h)."""
     _fields_ = [('m', _i64), ('n', _i64), ('nz', _i64), ('nblocks', _i64),
-                ('A_indptr', _vp), ('A_indices', _vp), ('A_data', _vp),
-                ('A_tiles', _vp), ('A_ntiles', _i64),
-                ('AT_indptr', _vp), ('AT_indices', _vp), ('AT_data', _vp),
-                ('AT_tiles', _vp), ('AT_ntiles', _i64),
+                ('A_sidx', _vp), ('A_sval', _vp), ('A_sptr', _vp), ('A_perm', _vp),
+                ('A_coff', _vp), ('A_nchunk', _i64), ('A_maxsl', _i64), ('rpart', _vp),
+                ('AT_sidx', _vp), ('AT_sval', _vp), ('AT_sptr', _vp),
                 ('target', _vp), ('xstarts', _vp), ('zstarts', _vp), ('xz', _vp),
+                ('pk_z0', _vp), ('pk_b0', _vp), ('pk_mask', _vp), ('pk_len', _vp),
+                ('npacks', _i64),
                 ('z', _vp * 2), ('g', _vp * 2), ('x', _vp), ('r', _vp), ('scal', _vp),
                 ('work', _vp),
                 ('max_zblock', _i64), ('max_iter', _i64), ('opt_tol', _dbl),
-                ('early_exit', _i32), ('a_group', _i32), ('at_group', _i32)]
+                ('early_exit', _i32), ('reserved', _i32)]
 
 
 _SIGS = {
@@ -66,7 +67,7 @@ _SIGS = {
     'bsls_spmv_workspace_size': (_sz, [_i64]),
     'bsls_csr_spmv': (_int, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _dbl, _vp, _vp, _int, _vp,
                              _sz, _vp]),
-    'bsls_bb_workspace_size': (_sz, [_i64, _i64, _i64, _i64]),
+    'bsls_bb_workspace_size': (_sz, [_i64, _i64, _i64]),
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),

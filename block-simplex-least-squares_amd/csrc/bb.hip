@@ -5,27 +5,29 @@
 //     g = N'A'(A N z + target);  dg = g - g_prev;  if sum(dg) == 0: break
 //     t = (z - z_prev).dg / dg.dg;  z <- clip01(PAVA(z - t g));  fx = f(z); stop?
 // One iteration here = three kernels, all HBM-bound, no host round trip:
-//   K2  g = N'(A' r) with an explicit A' CSR (deterministic, no atomics): CSR-
-//       stream tiles of A' that end at x-block ends, so the adjacent difference
-//       N'w = w_i - w_{i+1} never leaves LDS; fused: dg, the four BB sums, the
-//       store of g.
+//   K2  g = N'(A' r) with an explicit A' in SELL-C-64 (deterministic, no atomics):
+//       one lane per x-row, each wave owning 63 rows plus one halo row, so the
+//       adjacent difference N'w = w_i - w_{i+1} is a lane shuffle; fused: dg,
+//       the four BB sums, the store of g.
 //   K3  t from the sums; per z-block PAVA (v1 pooling order, bit-identical to
 //       isotonic_regression.h:13-58) + clip to [0,1] + the vector N z (per-block
 //       differences, last entry -z_last), one lane per block over an LDS-staged
 //       range.  N is never materialised.
 //   K1  r = A (N z) + target, target = A x0 - b, exactly the reference's
-//       A.dot(N.dot(z)) + target; ||r||^2 (next gradient's residual AND f(z)),
-//       and the stopping test of the iteration, in the last workgroup.
+//       A.dot(N.dot(z)) + target.  A in SELL-C-64 cut into column chunks, one
+//       per XCD group, so each XCD's L2 serves the x gather of one chunk
+//       (K1a: partial per chunk); K1b sums the chunk partials in chunk order,
+//       adds target, ||r||^2 (next gradient's residual AND f(z)) and runs the
+//       stopping test of the iteration in the last workgroup.
 // Every cross-workgroup sum is reduced in a fixed order by the last-arriving
 // workgroup (bsls_common.hpp last_block_sum), so runs are bit-reproducible.
 // Scalars live in device memory (scal[]); the host only polls them.
 #include "pava.hpp"
-#include "spmv.hpp"
+#include "pava_wave.hpp"
+#include "sell.hpp"
 
 namespace bsls {
 
-constexpr int K3_CAP = 1024;   // z entries staged per K3 wave
-constexpr int BPW = 16;        // z-blocks per K3 wave (one lane each)
 
 struct BBWork {
     unsigned *tk1, *tk2, *tkf;
@@ -36,7 +38,9 @@ struct BBWork {
 
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 
-static BBWork bb_layout(void *base, int64_t m, int64_t nz, int64_t max_tiles) {
+constexpr int K2_ROWS = 4 * (SELL_C - 1);   // own x-rows per K2 workgroup (4 waves)
+
+static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     BBWork w{};
     char *p = (char *)base;
     size_t off = 0;
@@ -45,9 +49,9 @@ static BBWork bb_layout(void *base, int64_t m, int64_t nz, int64_t max_tiles) {
     w.tkf = (unsigned *)(p + off + 2 * TICKET_BYTES);
     off += al16(3 * TICKET_BYTES);
     w.p1 = (double *)(p + off);
-    off += al16((size_t)(max_tiles + 1) * 8);
+    off += al16((size_t)((m + 255) / 256 + 1) * 8);
     w.p2 = (double *)(p + off);
-    off += al16((size_t)(max_tiles + 1) * 4 * 8);
+    off += al16((size_t)((n + K2_ROWS - 1) / K2_ROWS + 1) * 4 * 8);
     w.pf = (double *)(p + off);
     off += al16((size_t)((m + 255) / 256 + 1) * 8);
     w.wsc = (int32_t *)(p + off);
@@ -56,10 +60,7 @@ static BBWork bb_layout(void *base, int64_t m, int64_t nz, int64_t max_tiles) {
     return w;
 }
 
-static BBWork bb_layout(const bsls_bb_problem &P) {
-    const int64_t mt = P.A_ntiles > P.AT_ntiles ? P.A_ntiles : P.AT_ntiles;
-    return bb_layout(P.work, P.m, P.nz, mt);
-}
+static BBWork bb_layout(const bsls_bb_problem &P) { return bb_layout(P.work, P.m, P.n, P.nz); }
 
 __device__ __forceinline__ void bb_stop_check(const bsls_bb_problem &P, int64_t iter, double fx) {
     double *s = P.scal;
@@ -88,26 +89,37 @@ __device__ __forceinline__ void bb_record_f(const bsls_bb_problem &P, int64_t it
     }
 }
 
-// K1: r = A x (+ target); optional ||r||^2 and stopping test.  One workgroup
-// per A tile (spmv.hpp); the tiles' partial ||r||^2 are reduced in tile order
-// by the last workgroup.
-template <int G, bool ADD, bool REDUCE, bool ITER>
-__global__ __launch_bounds__(TB) void bb_k1(bsls_bb_problem P, int64_t iter, double *part,
-                                            unsigned *ticket) {
-    __shared__ double prod[NZT];
-    __shared__ double wl[RMAX];
+// K1a: per column chunk c, rpart[c][row] = sum over the row's entries in that
+// chunk (SELL, one wave per slice).  Workgroup b takes chunk b % nchunk.
+template <bool ITER>
+__global__ __launch_bounds__(256) void bb_k1a(bsls_bb_problem P) {
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    const int64_t nc = P.A_nchunk;
+    const int64_t c = blockIdx.x % nc;
+    const int64_t sl = P.A_coff[c] + (int64_t)(blockIdx.x / nc) * 4 + threadIdx.x / WAVE;
+    if (sl >= P.A_coff[c + 1]) return;
+    const int lane = lane_id();
+    const int32_t row = P.A_perm[sl * SELL_C + lane];
+    const int64_t s0 = P.A_sptr[sl];
+    const int W = (int)((P.A_sptr[sl + 1] - s0) / SELL_C);
+    const double v = sell_row(P.A_sidx, P.A_sval, P.x, s0 + lane, W, 0.0);
+    if (row >= 0) P.rpart[c * P.m + row] = v;
+}
+
+// K1b: r = sum_c rpart[c] (+ target); optional ||r||^2 and the stopping test.
+template <bool ADD, bool REDUCE, bool ITER>
+__global__ __launch_bounds__(256) void bb_k1b(bsls_bb_problem P, int64_t iter, double *part,
+                                              unsigned *ticket) {
     __shared__ double red[4];
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double sq[1] = {0.0};
-    for (int64_t tile = blockIdx.x; tile < P.A_ntiles; tile += gridDim.x) {
-        const int64_t r0 = P.A_tiles[tile], r1 = P.A_tiles[tile + 1];
-        tile_rows<G>(P.A_indptr, P.A_indices, P.A_data, P.x, r0, r1, prod, wl);
-        for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
-            double o = wl[t];
-            if (ADD) o += P.target[r0 + t];
-            P.r[r0 + t] = o;
-            sq[0] += o * o;
-        }
+    if (i < P.m) {
+        double o = P.rpart[i];
+        for (int64_t c = 1; c < P.A_nchunk; ++c) o += P.rpart[c * P.m + i];
+        if (ADD) o += P.target[i];
+        P.r[i] = o;
+        sq[0] = o * o;
     }
     if (!REDUCE) return;
     block_sum<1>(sq, red);
@@ -134,37 +146,50 @@ __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t it
         bb_record_f(P, iter, tot[0], iter > 0);
 }
 
-// K2: g = N'(A' r); with ITER also dg = g - g_prev and the BB sums.  A' tiles
-// end at x-block ends, so both rows of every N' difference sit in this
-// workgroup's LDS.
-template <int G, bool ITER>
-__global__ __launch_bounds__(TB) void bb_k2(bsls_bb_problem P, const double *__restrict__ zc,
-                                            const double *__restrict__ zp,
-                                            const double *__restrict__ gp,
-                                            double *__restrict__ gout, double *part,
-                                            unsigned *ticket) {
-    __shared__ double prod[NZT];
-    __shared__ double wl[RMAX];
+// K2: g = N'(A' r); with ITER also dg = g - g_prev and the BB sums.  Lane l of
+// wave w takes x-row i = 63 w + l; lane 63 is the halo (the next wave's first
+// row), so N' w = w_i - w_{i+1} is one shuffle.  The epilogue operands are
+// loaded before the row sum so their latency overlaps it.
+template <bool ITER>
+__global__ __launch_bounds__(256) void bb_k2(bsls_bb_problem P, const double *__restrict__ zc,
+                                             const double *__restrict__ zp,
+                                             const double *__restrict__ gp,
+                                             double *__restrict__ gout, double *part,
+                                             unsigned *ticket) {
     __shared__ double red[16];
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    const int lane = lane_id();
+    const int64_t wv = (int64_t)blockIdx.x * 4 + threadIdx.x / WAVE;
+    const int64_t i = wv * (SELL_C - 1) + lane;
+    int32_t j = -1;
+    double gpj = 0.0, zcj = 0.0, zpj = 0.0;
+    if (lane < SELL_C - 1 && i < P.n) {
+        j = P.xz[i];
+        if (ITER && j >= 0) {
+            gpj = gp[j];
+            zcj = zc[j];
+            zpj = zp[j];
+        }
+    }
+    double v = 0.0;
+    if (i < P.n) {
+        const int64_t sl = i / SELL_C;
+        const int64_t s0 = P.AT_sptr[sl];
+        const int W = (int)((P.AT_sptr[sl + 1] - s0) / SELL_C);
+        v = sell_row(P.AT_sidx, P.AT_sval, P.r, s0 + (i % SELL_C), W, 0.0);
+    }
+    const double vn = __shfl_down(v, 1, WAVE);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int64_t tile = blockIdx.x; tile < P.AT_ntiles; tile += gridDim.x) {
-        const int64_t r0 = P.AT_tiles[tile], r1 = P.AT_tiles[tile + 1];
-        tile_rows<G>(P.AT_indptr, P.AT_indices, P.AT_data, P.r, r0, r1, prod, wl);
-        for (int t = threadIdx.x; t < (int)(r1 - r0); t += TB) {
-            const int32_t j = P.xz[r0 + t];
-            if (j >= 0) {
-                const double g = wl[t] - wl[t + 1];
-                gout[j] = g;
-                if (ITER) {
-                    const double dg = g - gp[j];
-                    const double dz = zc[j] - zp[j];
-                    acc[0] += dg;
-                    acc[1] += dz * dg;
-                    acc[2] += dg * dg;
-                    acc[3] += g * g;
-                }
-            }
+    if (j >= 0) {
+        const double g = v - vn;
+        gout[j] = g;
+        if (ITER) {
+            const double dg = g - gpj;
+            const double dz = zcj - zpj;
+            acc[0] = dg;
+            acc[1] = dz * dg;
+            acc[2] = dg * dg;
+            acc[3] = g * g;
         }
     }
     if (!ITER) return;
@@ -186,93 +211,75 @@ __device__ __forceinline__ int64_t xend(const bsls_bb_problem &P, int64_t b) {
 }
 
 // K3: t, z_new = clip01(PAVA(z - t g)) per block, x = N z_new.  One wave per
-// BPW consecutive blocks: all 64 lanes stage the blocks' contiguous z range
-// into LDS (loads kept in flight), lanes 0..BPW-1 run the serial PAVA of one
-// block each, then the z and x ranges are written back coalesced.
-__global__ __launch_bounds__(WAVE) void bb_k3(bsls_bb_problem P, int64_t iter,
-                                              const double *__restrict__ zc,
-                                              const double *__restrict__ g,
-                                              double *__restrict__ zn,
-                                              int32_t *__restrict__ wsc) {
-    __shared__ double ly[K3_CAP];
-    __shared__ double lx[K3_CAP + BPW];
-    __shared__ int32_t lw[K3_CAP];
+// pack of whole z-blocks (<= 64 entries, one lane each): the PAVA passes run
+// wave-parallel (pava_wave.hpp, bit-identical to the serial reference); a
+// block longer than 64 entries gets a pack of its own and the serial PAVA.
+__device__ __forceinline__ bool bb_step_t(const bsls_bb_problem &P, int64_t iter, double &t) {
     double *s = P.scal;
-    if (s[BSLS_S_STOP] != 0.0) return;
+    if (s[BSLS_S_STOP] != 0.0) return false;
     if (P.early_exit && s[BSLS_S_SUMDG] == 0.0) {  // BB.py:22
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             s[BSLS_S_STOP] = (double)BSLS_STOP_NOCHANGE;
             s[BSLS_S_ITER] = (double)iter;
             s[BSLS_S_ZBUF] = (double)((iter - 1) & 1);
         }
-        return;
+        return false;
     }
-    const double t = s[BSLS_S_DZDG] / s[BSLS_S_DGDG];
+    t = s[BSLS_S_DZDG] / s[BSLS_S_DGDG];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         s[BSLS_S_T] = t;
         if (fabs(t) <= 1e-10 || fabs(t) > 1e10) s[BSLS_S_WARN] += 1.0;
     }
-    const int lane = lane_id();
-    const int64_t b0 = (int64_t)blockIdx.x * BPW;
-    const int64_t b = b0 + lane;
-    const bool valid = lane < BPW && b < P.nblocks;
-    const int64_t blast = (b0 + BPW - 1 < P.nblocks) ? b0 + BPW - 1 : P.nblocks - 1;
-    const int64_t Z0 = P.zstarts[b0], Z1 = zend(P, blast);
-    const int64_t X0 = P.xstarts[b0], X1 = xend(P, blast);
-    const int64_t zs = valid ? P.zstarts[b] : 0, ze = valid ? zend(P, b) : 0;
-    const int64_t xs = valid ? P.xstarts[b] : 0, xe = valid ? xend(P, b) : 0;
-    if (Z1 - Z0 <= K3_CAP) {
-        const int nzr = (int)(Z1 - Z0), nxr = (int)(X1 - X0);
-        constexpr int U = 4;
-        for (int j0 = 0; j0 < nzr; j0 += U * WAVE) {
-            double a[U], c[U];
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int j = j0 + lane + k * WAVE;
-                a[k] = (j < nzr) ? zc[Z0 + j] : 0.0;
-                c[k] = (j < nzr) ? g[Z0 + j] : 0.0;
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int j = j0 + lane + k * WAVE;
-                if (j < nzr) {
-                    ly[j] = a[k] - t * c[k];  // x_next = x - t * g (BB.py:29)
-                    lw[j] = 1;
-                }
-            }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
+                                             const double *__restrict__ zc,
+                                             const double *__restrict__ g,
+                                             double *__restrict__ zn,
+                                             int32_t *__restrict__ wsc) {
+    double t;
+    if (!bb_step_t(P, iter, t)) return;
+    const int64_t pk = (int64_t)blockIdx.x * 4 + threadIdx.x / WAVE;
+    if (pk >= P.npacks) return;
+    const int l = lane_id();
+    const int64_t z0 = P.pk_z0[pk], b0 = P.pk_b0[pk];
+    const int L = P.pk_len[pk];
+    if (L <= WAVE) {
+        const uint64_t B = (uint64_t)P.pk_mask[pk];
+        const bool act = l < L;
+        double y = act ? zc[z0 + l] - t * g[z0 + l] : 0.0;  // x_next = x - t g (BB.py:29)
+        int w = 1;
+        uint64_t heads;
+        pava_v1_wave(y, w, L, B, heads);
+        const double v = clip01(y);
+        const double vprev = shfl_d(v, l > 0 ? l - 1 : 0);
+        if (act) {
+            zn[z0 + l] = v;
+            const bool bstart = (B >> l) & 1ull;
+            const int64_t blk = b0 + __popcll(B & mask_le(l)) - 1;
+            const int64_t xi = z0 + l + blk;            // x index of this z entry
+            P.x[xi] = v - (bstart ? 0.0 : vprev);
+            const bool bend = (l == L - 1) || ((B >> (l + 1)) & 1ull);
+            if (bend) P.x[xi + 1] = 0.0 - v;            // (N z)_last = -z_last
         }
-        __syncthreads();
-        if (valid) {
-            const int lo = (int)(zs - Z0), hi = (int)(ze - Z0);
-            pava_v1(ly, lw, lo, hi, 1);
-            double prev = 0.0;
-            int xo = (int)(xs - X0);
-            for (int j = lo; j < hi; ++j) {
-                const double v = clip01(ly[j]);
-                ly[j] = v;
-                lx[xo++] = v - prev;
-                prev = v;
-            }
-            lx[xe - 1 - X0] = 0.0 - prev;   // (N z)_last = -z_last
-        }
-        __syncthreads();
-        for (int j = lane; j < nzr; j += WAVE) zn[Z0 + j] = ly[j];
-        for (int j = lane; j < nxr; j += WAVE) P.x[X0 + j] = lx[j];
-    } else if (valid) {
-        for (int64_t j = zs; j < ze; ++j) {
+    } else if (l == 0) {
+        // one block longer than a wave: serial PAVA in global memory
+        const int64_t xs = P.xstarts[b0];
+        for (int64_t j = z0; j < z0 + L; ++j) {
             zn[j] = zc[j] - t * g[j];
             wsc[j] = 1;
         }
-        pava_v1(zn, wsc, zs, ze, 1);
+        pava_v1(zn, wsc, z0, z0 + L, 1);
         double prev = 0.0;
         int64_t xo = xs;
-        for (int64_t j = zs; j < ze; ++j) {
+        for (int64_t j = z0; j < z0 + L; ++j) {
             const double v = clip01(zn[j]);
             zn[j] = v;
             P.x[xo++] = v - prev;
             prev = v;
         }
-        P.x[xe - 1] = 0.0 - prev;
+        P.x[xo] = 0.0 - prev;
     }
 }
 
@@ -299,45 +306,31 @@ __global__ __launch_bounds__(256) void bb_z2x(bsls_bb_problem P, const double *_
 
 template <bool ADD, bool REDUCE, bool ITER>
 static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, hipStream_t st) {
-    const int grid = (int)(P.A_ntiles < MAX_TILE_WG ? P.A_ntiles : MAX_TILE_WG);
-    switch (P.a_group) {
-#define K1CASE(G)                                                               \
-    case G:                                                                     \
-        bb_k1<G, ADD, REDUCE, ITER><<<grid, TB, 0, st>>>(P, iter, w.p1, w.tk1); \
-        break;
-        K1CASE(1) K1CASE(2) K1CASE(4) K1CASE(8) K1CASE(16) K1CASE(32) K1CASE(64)
-#undef K1CASE
-    }
+    const int ga = (int)(P.A_nchunk * ((P.A_maxsl + 3) / 4));
+    bb_k1a<ITER><<<ga, 256, 0, st>>>(P);
+    bb_k1b<ADD, REDUCE, ITER><<<grid_for(P.m, 256), 256, 0, st>>>(P, iter, w.p1, w.tk1);
 }
 
 template <bool ITER>
 static void launch_k2(const bsls_bb_problem &P, const double *zc, const double *zp,
                       const double *gp, double *gout, const BBWork &w, hipStream_t st) {
-    const int grid = (int)(P.AT_ntiles < MAX_TILE_WG ? P.AT_ntiles : MAX_TILE_WG);
-    switch (P.at_group) {
-#define K2CASE(G)                                                               \
-    case G:                                                                     \
-        bb_k2<G, ITER><<<grid, TB, 0, st>>>(P, zc, zp, gp, gout, w.p2, w.tk2);  \
-        break;
-        K2CASE(1) K2CASE(2) K2CASE(4) K2CASE(8) K2CASE(16) K2CASE(32) K2CASE(64)
-#undef K2CASE
-    }
+    bb_k2<ITER><<<grid_for(P.n, K2_ROWS), 256, 0, st>>>(P, zc, zp, gp, gout, w.p2, w.tk2);
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
                       double *zn, const BBWork &w, hipStream_t st) {
-    bb_k3<<<grid_for(P.nblocks, BPW), WAVE, 0, st>>>(P, iter, zc, g, zn, w.wsc);
+    bb_k3<<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.wsc);
 }
 
 static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
-    if (!p->A_indptr || !p->AT_indptr || !p->target || !p->xstarts || !p->zstarts || !p->xz)
+    if (!p->A_sidx || !p->A_sval || !p->A_sptr || !p->A_perm || !p->A_coff || !p->rpart)
         return BSLS_E_ARG;
-    if (!p->A_tiles || !p->AT_tiles || p->A_ntiles <= 0 || p->AT_ntiles <= 0) return BSLS_E_ARG;
+    if (p->A_nchunk < 1 || p->A_maxsl < 1) return BSLS_E_ARG;
+    if (!p->AT_sidx || !p->AT_sval || !p->AT_sptr) return BSLS_E_ARG;
+    if (!p->target || !p->xstarts || !p->zstarts || !p->xz) return BSLS_E_ARG;
+    if (!p->pk_z0 || !p->pk_b0 || !p->pk_mask || !p->pk_len || p->npacks < 1) return BSLS_E_ARG;
     if (!p->z[0] || !p->z[1] || !p->g[0] || !p->g[1] || !p->x || !p->r || !p->scal || !p->work)
-        return BSLS_E_ARG;
-    const int ag = p->a_group, tg = p->at_group;
-    if (ag < 1 || ag > 64 || (ag & (ag - 1)) || tg < 1 || tg > 64 || (tg & (tg - 1)))
         return BSLS_E_ARG;
     return BSLS_OK;
 }
@@ -346,9 +339,8 @@ static int check_problem(const bsls_bb_problem *p) {
 
 using namespace bsls;
 
-extern "C" size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz, int64_t max_tiles) {
-    (void)n;
-    return bb_layout(nullptr, m, nz, max_tiles).bytes;
+extern "C" size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz) {
+    return bb_layout(nullptr, m, n, nz).bytes;
 }
 
 extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream) {

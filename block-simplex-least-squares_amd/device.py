@@ -69,6 +69,87 @@ class DeviceCSR:
         return (out, sq) if want_sq else out
 
 
+def build_sell(A, window=0, col_lo=None, col_hi=None, C=64):
+    """SELL-C-64 image of the CSR matrix A (rows of A restricted to columns
+    [col_lo, col_hi), global column indices kept).  window > 0 sorts rows by
+    length (longest first) inside windows of that many rows to cut padding;
+    window = 0 keeps the row order.  Returns host arrays
+    (sidx int32 with -1 padding, sval f64, sptr int64 per slice, slot_row int32)."""
+    A = sps.csr_matrix(A)
+    A.sort_indices()
+    m, n = A.shape
+    if col_lo is not None:
+        A = A[:, col_lo:col_hi].tocsr()
+        A.sort_indices()
+        A.indices = A.indices + col_lo
+    ip = A.indptr.astype(np.int64)
+    lens = np.diff(ip)
+    if window > 0:
+        key = (np.arange(m) // window) * (int(lens.max(initial=0)) + 1) - lens
+        order = np.argsort(key, kind='stable')
+    else:
+        order = np.arange(m)
+    nsl = (m + C - 1) // C
+    slot_row = np.full(nsl * C, -1, dtype=np.int32)
+    slot_row[:m] = order
+    slot_len = np.zeros(nsl * C, dtype=np.int64)
+    slot_len[:m] = lens[order]
+    W = slot_len.reshape(nsl, C).max(axis=1)
+    sptr = np.concatenate(([0], np.cumsum(W * C))).astype(np.int64)
+    sidx = np.full(int(sptr[-1]), -1, dtype=np.int32)
+    sval = np.zeros(int(sptr[-1]), dtype=np.float64)
+    inv = np.empty(m, dtype=np.int64)
+    inv[order] = np.arange(m)
+    rows = np.repeat(np.arange(m, dtype=np.int64), lens)
+    k = np.arange(A.nnz, dtype=np.int64) - ip[rows]
+    slot = inv[rows]
+    dest = sptr[slot // C] + k * C + slot % C
+    sidx[dest] = A.indices
+    sval[dest] = A.data
+    return sidx, sval, sptr, slot_row
+
+
+class SellChunked:
+    """A for K1: SELL-C-64 per column chunk (rows length-sorted in windows),
+    concatenated; chunk c is processed by workgroups b with b % nchunk == c."""
+
+    def __init__(self, A, nchunk=8, window=4096):
+        torch = _torch()
+        A = sps.csr_matrix(A)
+        m, n = A.shape
+        nchunk = max(1, min(int(nchunk), n))
+        bounds = np.linspace(0, n, nchunk + 1).astype(np.int64)
+        parts = [build_sell(A, window, bounds[c], bounds[c + 1]) for c in range(nchunk)]
+        off = 0
+        sptrs, coff = [], [0]
+        for (_, _, sp, _) in parts:
+            sptrs.append(sp[:-1] + off)
+            off += int(sp[-1])
+            coff.append(coff[-1] + sp.shape[0] - 1)
+        sptr = np.concatenate(sptrs + [np.array([off], dtype=np.int64)])
+        self.nchunk = nchunk
+        self.maxsl = int(max(sp.shape[0] - 1 for (_, _, sp, _) in parts))
+        self.sidx = torch.from_numpy(np.concatenate([p[0] for p in parts])).cuda()
+        self.sval = torch.from_numpy(np.concatenate([p[1] for p in parts])).cuda()
+        self.sptr = torch.from_numpy(sptr).cuda()
+        self.perm = torch.from_numpy(np.concatenate([p[3] for p in parts])).cuda()
+        self.coff = torch.from_numpy(np.array(coff, dtype=np.int64)).cuda()
+        self.padded = off
+        self.nnz = int(A.nnz)
+
+
+class SellRows:
+    """A' for K2: SELL-C-64 with rows in order."""
+
+    def __init__(self, AT):
+        torch = _torch()
+        sidx, sval, sptr, _ = build_sell(AT, 0)
+        self.sidx = torch.from_numpy(sidx).cuda()
+        self.sval = torch.from_numpy(sval).cuda()
+        self.sptr = torch.from_numpy(sptr).cuda()
+        self.padded = int(sptr[-1])
+
+
 class BlockLayout:
     """Block structure of x (sizes k_b) and of z (sizes k_b - 1), on device."""
 
@@ -91,6 +172,38 @@ class BlockLayout:
         self.xz = torch.from_numpy(xz.astype(np.int32)).cuda()
         self.max_block = int(bs.max())
         self.max_zblock = self.max_block - 1
+        self._packs = None
+
+    def packs(self):
+        """K3 packs (csrc/bb.hip): consecutive whole z-blocks with <= 64 z entries
+        for one wave, or a single longer block.  Host-planned once."""
+        if self._packs is None:
+            torch = _torch()
+            kz = self.sizes - 1
+            z0, b0, mask, ln = [], [], [], []
+            b = 0
+            p = self.p
+            zst = self.zstarts_h
+            while b < p:
+                if kz[b] > 64:
+                    z0.append(zst[b]); b0.append(b); mask.append(1); ln.append(int(kz[b]))
+                    b += 1
+                    continue
+                tot, m_, e = 0, 0, b
+                while e < p and kz[e] <= 64 and tot + kz[e] <= 64:
+                    m_ |= 1 << tot
+                    tot += int(kz[e])
+                    e += 1
+                z0.append(zst[b]); b0.append(b); mask.append(m_); ln.append(tot)
+                b = e
+            mask = np.array(mask, dtype=np.uint64).view(np.int64)
+            self._packs = dict(
+                z0=torch.from_numpy(np.array(z0, dtype=np.int64)).cuda(),
+                b0=torch.from_numpy(np.array(b0, dtype=np.int64)).cuda(),
+                mask=torch.from_numpy(mask).cuda(),
+                len=torch.from_numpy(np.array(ln, dtype=np.int32)).cuda(),
+                n=len(z0))
+        return self._packs
 
 
 class BBEngine:
@@ -110,10 +223,12 @@ class BBEngine:
         A = sps.csr_matrix(A)
         if A.shape[1] != lay.n:
             raise ValueError('A has %d columns but the blocks cover %d' % (A.shape[1], lay.n))
+        AT = sps.csr_matrix(AT) if AT is not None else A.T.tocsr()
         self.A = A_dev or DeviceCSR(A)
-        # A' tiles end at x-block ends: the fused N' difference stays in LDS
-        self.AT = AT_dev or DeviceCSR(AT if AT is not None else A.T.tocsr(),
-                                      tile_ends=np.cumsum(lay.sizes))
+        self.AT = AT_dev or DeviceCSR(AT)
+        # the fused kernels' images: A chunked by columns (K1), A' by rows (K2)
+        self.A_sell = SellChunked(A)
+        self.AT_sell = SellRows(AT)
         self.m, self.n, self.nz = A.shape[0], lay.n, lay.nz
         opts = options or {}
         self.options = dict(opts)
@@ -138,21 +253,28 @@ class BBEngine:
         self.x = torch.empty(lay.n, **dev)
         self.r = torch.empty(self.m, **dev)
         self.scal = torch.zeros(_native.S_COUNT, **dev)
-        self.work = torch.zeros(L.bsls_bb_workspace_size(self.m, self.n, self.nz,
-                                                         max(self.A.ntiles, self.AT.ntiles)),
+        self.work = torch.zeros(L.bsls_bb_workspace_size(self.m, self.n, self.nz),
                                 dtype=torch.uint8, device='cuda')
+        self.rpart = torch.zeros(self.A_sell.nchunk * self.m, **dev)
         P = BBProblem()
         P.m, P.n, P.nz, P.nblocks = self.m, lay.n, lay.nz, lay.p
-        P.A_indptr, P.A_indices, P.A_data = (self.A.indptr.data_ptr(),
-                                             self.A.indices.data_ptr(), self.A.data.data_ptr())
-        P.A_tiles, P.A_ntiles = self.A.tiles.data_ptr(), self.A.ntiles
-        P.AT_indptr, P.AT_indices, P.AT_data = (self.AT.indptr.data_ptr(),
-                                                self.AT.indices.data_ptr(),
-                                                self.AT.data.data_ptr())
-        P.AT_tiles, P.AT_ntiles = self.AT.tiles.data_ptr(), self.AT.ntiles
+        S = self.A_sell
+        P.A_sidx, P.A_sval, P.A_sptr = S.sidx.data_ptr(), S.sval.data_ptr(), S.sptr.data_ptr()
+        P.A_perm, P.A_coff = S.perm.data_ptr(), S.coff.data_ptr()
+        P.A_nchunk, P.A_maxsl, P.rpart = S.nchunk, S.maxsl, self.rpart.data_ptr()
+        T = self.AT_sell
+        P.AT_sidx, P.AT_sval, P.AT_sptr = T.sidx.data_ptr(), T.sval.data_ptr(), T.sptr.data_ptr()
         P.target = self.target.data_ptr()
         P.xstarts, P.zstarts, P.xz = (lay.xstarts.data_ptr(), lay.zstarts.data_ptr(),
                                       lay.xz.data_ptr())
+        if np.any(lay.sizes < 2):
+            # a one-route block has no z coordinate; the reference's projection
+            # asserts on it too (strictly increasing z-starts, c_extensions.pyx:78)
+            raise ValueError('every block needs at least 2 routes')
+        pk = lay.packs()
+        P.pk_z0, P.pk_b0, P.pk_mask, P.pk_len = (pk['z0'].data_ptr(), pk['b0'].data_ptr(),
+                                                 pk['mask'].data_ptr(), pk['len'].data_ptr())
+        P.npacks = pk['n']
         P.z[0], P.z[1] = self.z[0].data_ptr(), self.z[1].data_ptr()
         P.g[0], P.g[1] = self.g[0].data_ptr(), self.g[1].data_ptr()
         P.x, P.r, P.scal, P.work = (self.x.data_ptr(), self.r.data_ptr(), self.scal.data_ptr(),
@@ -161,8 +283,6 @@ class BBEngine:
         P.max_iter = int(opts.get('max_iter', 300000))
         P.opt_tol = float(opts.get('opt_tol', 1e-6))
         P.early_exit = 1 if early_exit else 0
-        P.a_group = self.A.group
-        P.at_group = self.AT.group
         self.P = P
         self.z0 = None
 

@@ -110,8 +110,8 @@ int bsls_csr_spmv(int64_t m, const int64_t *d_indptr, const int32_t *d_indices,
  * Replaces, per iteration, BB.solve's loop body (python/BB.py:17-41) over the
  * closures of main.solve_in_z (python/main.py:53-65) and the stopping rule
  * solvers.stopping (python/solvers.py:40-63):
- *   K1  r = A x + target (= A N z + A x0 - b), ||r||^2, stop test (SpMV, A CSR)
- *   K2  g = N' A' r, dg = g - g_prev, BB dot products      (SpMV', explicit A' CSR)
+ *   K1  r = A x + target (= A N z + A x0 - b), ||r||^2, stop test (SpMV, A SELL)
+ *   K2  g = N' A' r, dg = g - g_prev, BB dot products      (SpMV', explicit A' SELL)
  *   K3  z <- clip01(PAVA(z - t g)), x <- N z               (per-block projection)
  * The caller owns every buffer (see struct); bsls_bb_prologue() performs
  * BB.py:14-15 (g_prev = grad(z0 + 1)) and evaluates r(z0).  Iterations keep
@@ -139,20 +139,32 @@ enum {
 };
 typedef struct bsls_bb_problem {
     int64_t m, n, nz, nblocks;      /* rows, x length, z length (n - nblocks), blocks */
-    const int64_t *A_indptr;        /* m+1 */
-    const int32_t *A_indices;       /* nnz */
-    const double *A_data;           /* nnz */
-    const int64_t *A_tiles;         /* A_ntiles+1 row starts (bsls_csr_plan_tiles) */
-    int64_t A_ntiles;
-    const int64_t *AT_indptr;       /* n+1 (CSR of A transposed) */
-    const int32_t *AT_indices;
-    const double *AT_data;
-    const int64_t *AT_tiles;        /* tiles of A' that END AT x-BLOCK ENDS (fused N') */
-    int64_t AT_ntiles;
+    /* A for K1: sliced ELLPACK (SELL-C-64, column-major slices, padding column
+     * -1), split into A_nchunk column chunks; workgroup b works on chunk
+     * b % A_nchunk so each XCD's L2 holds one chunk of x (speed only). */
+    const int32_t *A_sidx;
+    const double *A_sval;
+    const int64_t *A_sptr;          /* global slice starts (entries), total slices + 1 */
+    const int32_t *A_perm;          /* row of slot s*64 + lane (-1 = empty slot) */
+    const int64_t *A_coff;          /* A_nchunk + 1 slice offsets of the chunks */
+    int64_t A_nchunk;
+    int64_t A_maxsl;                /* most slices in one chunk */
+    double *rpart;                  /* A_nchunk x m partial residuals */
+    /* A' for K2: SELL-C-64 with rows in order (row i at slice i/64, lane i%64) */
+    const int32_t *AT_sidx;
+    const double *AT_sval;
+    const int64_t *AT_sptr;         /* ceil(n/64) + 1 */
     const double *target;           /* m: A x0 - b (python/main.py:48) */
     const int64_t *xstarts;         /* nblocks, x-space block starts, xstarts[0] = 0 */
     const int64_t *zstarts;         /* nblocks, z-space block starts (xstarts[b] - b) */
     const int32_t *xz;              /* n: z index of x entry i, or -1 for a block's last entry */
+    /* K3 packs: runs of whole z-blocks with <= 64 z entries (one wave each), or
+     * one block with more (pk_len > 64, serial fallback) */
+    const int64_t *pk_z0;           /* first z entry */
+    const int64_t *pk_b0;           /* first block */
+    const int64_t *pk_mask;         /* block-start bits relative to pk_z0 (uint64) */
+    const int32_t *pk_len;          /* z entries */
+    int64_t npacks;
     double *z[2];                   /* ping-pong iterate buffers, nz each */
     double *g[2];                   /* ping-pong gradient buffers, nz each */
     double *x;                      /* n: N z of the current iterate (x0 is in target) */
@@ -163,10 +175,10 @@ typedef struct bsls_bb_problem {
     int64_t max_iter;               /* options['max_iter'] */
     double opt_tol;                 /* options['opt_tol'] */
     int32_t early_exit;             /* 0 disables every early exit (fixed-count timing) */
-    int32_t a_group, at_group;      /* lanes per row in the tile reduce (power of 2, <= 64) */
+    int32_t reserved;
 } bsls_bb_problem;
 
-size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz, int64_t max_tiles);
+size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
 /* BB.py:14-15 and the first f(z0): resets scal/tickets, g[0] = grad(z0 + 1),
  * r = r(z0), scal[FX] = f(z0).  z[0] must hold z0. */
 int bsls_bb_prologue(const bsls_bb_problem *p, void *stream);

@@ -47,15 +47,15 @@ def test_host_only_entry_points(native):
     assert L.bsls_proj_workspace_size(3_200_000, 100_000, 60) > 0
     assert L.bsls_proj_workspace_size(100, 2, 50) < L.bsls_proj_workspace_size(100_000, 2, 50_000)
     assert L.bsls_isotonic_workspace_size(1000) >= 4000
-    assert L.bsls_bb_workspace_size(100_000, 1_000_000, 950_000, 8000) > 4 * 950_000
+    assert L.bsls_bb_workspace_size(100_000, 1_000_000, 950_000) > 4 * 950_000
     assert L.bsls_spmv_workspace_size(8000) > 8 * 8000
     assert L.bsls_md_workspace_size(50_000) > 0
 
 
 def test_bb_struct_layout_matches_header(native):
-    # struct bsls_bb_problem: 4 int64; A (3 ptr + tiles ptr + int64); A' (same);
-    # 4 ptr; z[2], g[2], x, r, scal, work; 2 int64; 1 double; 3 int32 (+ pad)
-    assert ctypes.sizeof(native.BBProblem) == 32 + 40 + 40 + 32 + 64 + 16 + 8 + 12 + 4
+    # struct bsls_bb_problem: 4 int64; A SELL (5 ptr, 2 int64, rpart); A' SELL (3 ptr);
+    # 4 ptr; packs (4 ptr + int64); z[2], g[2], x, r, scal, work; 2 int64; 1 double; 2 int32
+    assert ctypes.sizeof(native.BBProblem) == 32 + 64 + 24 + 32 + 40 + 64 + 16 + 8 + 8
 
 
 def test_tile_planner(native):

@@ -89,3 +89,40 @@ def test_bb_deterministic(cuda):
         eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 30, 'opt_tol': 1e-30})
         outs.append(eng.solve(poll=30).cpu().numpy().copy())
     assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64))
+
+
+def test_k3_wave_pava_bit_exact(cuda, orc):
+    """K3 alone (stage 4): z_new = clip01(PAVA_v1(z - t g)) and x = N z_new, bit for
+    bit against the oracle, on blocks of 2..150 routes (wave packs and the
+    serial fallback for z-blocks longer than 64)."""
+    import torch
+    import _native
+    from device import BBEngine
+    rs = np.random.RandomState(7)
+    sizes = np.concatenate([rs.randint(2, 40, size=300), [66, 65, 130, 2, 150, 64, 3]])
+    rs.shuffle(sizes)
+    n = int(sizes.sum())
+    m = 200
+    A = sps.random(m, n, density=0.02, random_state=rs, format='csr')
+    eng = BBEngine(A, rs.randn(m), sizes, options={'max_iter': 10, 'opt_tol': 1e-30})
+    nz = eng.nz
+    for trial in range(3):
+        zc = np.cumsum(rs.rand(nz)) * 0.01 if trial == 0 else rs.randn(nz)
+        g = rs.randn(nz) * (0.5 if trial < 2 else 50.0)
+        t = [1.0, 0.37, 3.0][trial]
+        eng.z[0][:nz].copy_(torch.from_numpy(zc))
+        eng.g[1][:nz].copy_(torch.from_numpy(g))
+        sc = np.zeros(_native.S_COUNT)
+        sc[_native.S_SUMDG] = 1.0
+        sc[_native.S_DZDG] = t
+        sc[_native.S_DGDG] = 1.0
+        eng.scal.copy_(torch.from_numpy(sc))
+        eng.stage(4, 1)
+        got = eng.z[1][:nz].cpu().numpy()
+        ref = zc - t * g
+        zst = eng.layout.zstarts_h
+        orc.isotonic_regression_multi_c(ref, zst)
+        ref = np.maximum(np.minimum(ref, 1.0), 0.0)
+        assert np.array_equal(got.view(np.int64), ref.view(np.int64)), trial
+        xr = orc.block_sizes_to_N(sizes).dot(ref)
+        assert np.array_equal(eng.x.cpu().numpy(), xr), trial

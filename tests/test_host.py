@@ -150,3 +150,33 @@ def test_partition_blocks_balanced():
         assert max(loads) - min(loads) <= 2 * bs.max()
     with pytest.raises(ValueError):
         partition_blocks(bs, bs, 501)
+
+
+def test_sell_image_roundtrip():
+    """The SELL-C-64 image (device.build_sell) holds every CSR entry once, in row
+    order inside each row, padding marked -1."""
+    import device
+    rs = np.random.RandomState(SEED)
+    A = sps.random(300, 500, density=0.05, random_state=rs, format='csr')
+    for window, lo, hi in ((0, None, None), (64, None, None), (128, 100, 260)):
+        sidx, sval, sptr, slot_row = device.build_sell(A, window, lo, hi)
+        ref = A if lo is None else A[:, lo:hi]
+        rec = sps.lil_matrix(A.shape)
+        for s in range(sptr.shape[0] - 1):
+            W = (sptr[s + 1] - sptr[s]) // 64
+            for p in range(64):
+                row = slot_row[s * 64 + p]
+                cols = [sidx[sptr[s] + k * 64 + p] for k in range(W)]
+                vals = [sval[sptr[s] + k * 64 + p] for k in range(W)]
+                valid = [c for c in cols if c >= 0]
+                if row < 0:
+                    assert not valid
+                    continue
+                assert valid == sorted(valid)
+                for c, v in zip(cols, vals):
+                    if c >= 0:
+                        rec[row, c] = v
+        want = sps.csr_matrix(A.shape)
+        want = A.copy() if lo is None else sps.hstack([sps.csr_matrix((300, lo)), ref,
+                                                       sps.csr_matrix((300, 500 - hi))]).tocsr()
+        assert (sps.csr_matrix(rec) != want).nnz == 0
