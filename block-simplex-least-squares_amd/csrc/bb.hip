@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
             const int64_t blk = b0 + __popcll(B & mask_le(l)) - 1;
             const int64_t xi = z0 + l + blk;            // x index of this z entry
             P.x[xi] = v - (bstart ? 0.0 : vprev);
-            const bool bend = (l == L - 1) || ((B >> (l + 1)) & 1ull);
+            const bool bend = (l == L - 1) || (l < 63 && ((B >> (l + 1)) & 1ull));
             if (bend) P.x[xi + 1] = 0.0 - v;            // (N z)_last = -z_last
         }
     } else if (l == 0) {

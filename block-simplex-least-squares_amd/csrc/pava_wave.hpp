@@ -19,7 +19,10 @@
 
 namespace bsls {
 
-__device__ __forceinline__ uint64_t mask_lt(int l) { return (1ull << l) - 1ull; }
+// bits [0, l); l may be 64 (a 64-bit shift by 64 is undefined, and wraps on the GPU)
+__device__ __forceinline__ uint64_t mask_lt(int l) {
+    return (l >= 64) ? ~0ull : ((1ull << l) - 1ull);
+}
 __device__ __forceinline__ uint64_t mask_le(int l) {
     return (l >= 63) ? ~0ull : ((2ull << l) - 1ull);
 }
