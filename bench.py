@@ -35,11 +35,25 @@ HBM_PEAK = 8.0e12   # MI355X_MICROARCH.md chip table (spec)
 
 
 def kernel_bytes(m, n, nz, p, nnz_a, nnz_at):
-    """Algorithmic HBM bytes per launch."""
+    """Algorithmic HBM bytes per launch, general fp64 CSR (SURVEY.md §8(d)'s
+    accounting split by kernel): 12 B per entry, 4-B row
+    pointers, each vector touched once."""
     return {
-        'K1_spmv_A': 12 * nnz_a + 8 * (m + 1) + 8 * n + 16 * m,
-        'K2_spmvT_Nt_dots': 12 * nnz_at + 8 * (n + 1) + 8 * m + 4 * n + 32 * nz,
-        'K3_pava_clip_z2x': 24 * nz + 8 * n + 16 * p,
+        'K1_spmv_A': 12 * nnz_a + 4 * (m + 1) + 8 * n + 16 * m,
+        'K2_spmvT_Nt_dots': 12 * nnz_at + 4 * (n + 1) + 8 * m + 32 * nz,
+        'K3_pava_clip_z2x': 24 * nz + 8 * n + 4 * p,
+    }
+
+
+def format_bytes(eng):
+    """Bytes the kernels actually stream with the panel images (the compressed
+    figure SURVEY.md §8(d) asks to state beside the general one)."""
+    m, n, nz = eng.m, eng.n, eng.nz
+    scale = 8 * n if eng.scaled else 0
+    return {
+        'K1_spmv_A': eng.A_pan.bytes() + 8 * n + 16 * m + 8 * m * (eng.A_pan.img['ngroups'] - 1) * 2,
+        'K2_spmvT_Nt_dots': eng.AT_pan.bytes() + 8 * m + 4 * n + 32 * nz + scale,
+        'K3_pava_clip_z2x': 24 * nz + 8 * n + 4 * eng.layout.p + scale,
     }
 
 
@@ -190,6 +204,7 @@ def main():
     out = None
     if rank == 0:
         kb = kernel_bytes(m, n_g, eng.nz, p_g, nnz, sh['AT'].nnz)
+        fb = format_bytes(eng)
         kern = {}
         if world == 1 and args.profile_iters > 0:
             # per-kernel HIP-event timing on the stream the kernels run on
@@ -209,7 +224,9 @@ def main():
                 us = float(np.mean(v))
                 kern[nm] = {'avg_us': us, 'alg_bytes': kb[nm],
                             'GB_s': kb[nm] / (us * 1e-6) / 1e9,
-                            'frac': kb[nm] / (us * 1e-6) / HBM_PEAK}
+                            'frac': kb[nm] / (us * 1e-6) / HBM_PEAK,
+                            'format_bytes': fb[nm],
+                            'format_GB_s': fb[nm] / (us * 1e-6) / 1e9}
         dom = max(kern, key=lambda k: kern[k]['avg_us']) if kern else None
         traffic = None
         tfile = os.path.join(ROOT, 'profiles', 'traffic_r01.json')

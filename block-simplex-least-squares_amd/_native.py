@@ -35,12 +35,22 @@ _sz = ctypes.c_size_t
 _int = ctypes.c_int
 
 
+PANEL_CHUNK = 15360      # BSLS_PANEL_CHUNK
+PANEL_ROWS = 255         # BSLS_PANEL_ROWS
+
+
+class Panels(ctypes.Structure):
+    """Mirror of struct bsls_panels (include/bsls_hip.h)."""
+    _fields_ = [('rows', _i64), ('cols', _i64), ('prow', _i64), ('halo', _i64),
+                ('npanels', _i64), ('nchunks', _i64), ('ngroups', _i64),
+                ('chunk_col', _vp), ('group_chunk', _vp), ('ent_off', _vp), ('perm_off', _vp),
+                ('dl_off', _vp), ('dlen', _vp), ('perm', _vp), ('ent', _vp), ('val', _vp)]
+
+
 class BBProblem(ctypes.Structure):
     """Mirror of struct bsls_bb_problem (include/bsls_hip.h)."""
     _fields_ = [('m', _i64), ('n', _i64), ('nz', _i64), ('nblocks', _i64),
-                ('A_sidx', _vp), ('A_sval', _vp), ('A_sptr', _vp), ('A_perm', _vp),
-                ('A_coff', _vp), ('A_nchunk', _i64), ('A_maxsl', _i64), ('rpart', _vp),
-                ('AT_sidx', _vp), ('AT_sval', _vp), ('AT_sptr', _vp),
+                ('A', Panels), ('AT', Panels), ('colv', _vp), ('rpart', _vp),
                 ('target', _vp), ('xstarts', _vp), ('zstarts', _vp), ('xz', _vp),
                 ('pk_z0', _vp), ('pk_b0', _vp), ('pk_mask', _vp), ('pk_len', _vp),
                 ('npacks', _i64),

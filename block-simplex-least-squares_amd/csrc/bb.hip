@@ -5,26 +5,31 @@
 //     g = N'A'(A N z + target);  dg = g - g_prev;  if sum(dg) == 0: break
 //     t = (z - z_prev).dg / dg.dg;  z <- clip01(PAVA(z - t g));  fx = f(z); stop?
 // One iteration here = three kernels, all HBM-bound, no host round trip:
-//   K2  g = N'(A' r) with an explicit A' in SELL-C-64 (deterministic, no atomics):
-//       one lane per x-row, each wave owning 63 rows plus one halo row, so the
-//       adjacent difference N'w = w_i - w_{i+1} is a lane shuffle; fused: dg,
-//       the four BB sums, the store of g.
+//   K2  g = N'(A' r) with an explicit A' in panel format (panels.hpp): each
+//       workgroup stages r chunk by chunk into LDS and sums its rows there in
+//       CSR order (bit-identical to SciPy's csr_matvec); each panel carries the
+//       next panel's first row, so the adjacent difference N'w = w_i - w_{i+1}
+//       stays in the wave; fused: dg, the four BB sums, the store of g.
 //   K3  t from the sums; per z-block PAVA (v1 pooling order, bit-identical to
 //       isotonic_regression.h:13-58) + clip to [0,1] + the vector N z (per-block
 //       differences, last entry -z_last), one lane per block over an LDS-staged
 //       range.  N is never materialised.
 //   K1  r = A (N z) + target, target = A x0 - b, exactly the reference's
-//       A.dot(N.dot(z)) + target.  A in SELL-C-64 cut into column chunks, one
-//       per XCD group, so each XCD's L2 serves the x gather of one chunk
-//       (K1a: partial per chunk); K1b sums the chunk partials in chunk order,
-//       adds target, ||r||^2 (next gradient's residual AND f(z)) and runs the
-//       stopping test of the iteration in the last workgroup.
+//       A.dot(N.dot(z)) + target.  A in panel format with its column chunks
+//       split into 8 groups, group = blockIdx % 8 (one XCD: the group's slice
+//       of x stays in that XCD's L2 while its 32 workgroups stage it chunk by
+//       chunk into LDS); K1a writes one partial per (row, group); K1b sums the
+//       8 partials in group order, adds target, ||r||^2 (next gradient's
+//       residual AND f(z)) and runs the stopping test in the last workgroup.
+//   For a scaled incidence A (bsls_utils.py:494) the values are not stored:
+//   K3 writes colv * (N z) (the same products SciPy forms), K2 multiplies by
+//   the row's colv.
 // Every cross-workgroup sum is reduced in a fixed order by the last-arriving
 // workgroup (bsls_common.hpp last_block_sum), so runs are bit-reproducible.
 // Scalars live in device memory (scal[]); the host only polls them.
 #include "pava.hpp"
 #include "pava_wave.hpp"
-#include "sell.hpp"
+#include "panels.hpp"
 
 namespace bsls {
 
@@ -38,7 +43,6 @@ struct BBWork {
 
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 
-constexpr int K2_ROWS = 4 * (SELL_C - 1);   // own x-rows per K2 workgroup (4 waves)
 
 static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     BBWork w{};
@@ -51,7 +55,7 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     w.p1 = (double *)(p + off);
     off += al16((size_t)((m + 255) / 256 + 1) * 8);
     w.p2 = (double *)(p + off);
-    off += al16((size_t)((n + K2_ROWS - 1) / K2_ROWS + 1) * 4 * 8);
+    off += al16((size_t)((n + PANEL_WAVES - 1) / PANEL_WAVES + 1) * 4 * 8);
     w.pf = (double *)(p + off);
     off += al16((size_t)((m + 255) / 256 + 1) * 8);
     w.wsc = (int32_t *)(p + off);
@@ -89,21 +93,34 @@ __device__ __forceinline__ void bb_record_f(const bsls_bb_problem &P, int64_t it
     }
 }
 
-// K1a: per column chunk c, rpart[c][row] = sum over the row's entries in that
-// chunk (SELL, one wave per slice).  Workgroup b takes chunk b % nchunk.
-template <bool ITER>
-__global__ __launch_bounds__(256) void bb_k1a(bsls_bb_problem P) {
+// K1a: workgroup (group g = blockIdx % ngroups, panels 16 rb .. 16 rb + 15)
+// stages x chunk by chunk (the group's columns) and leaves, per row, the sum
+// over the group's columns in rpart[g][row].
+template <int MODE, bool ITER>
+__global__ __launch_bounds__(1024) void bb_k1a(bsls_bb_problem P) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
-    const int64_t nc = P.A_nchunk;
-    const int64_t c = blockIdx.x % nc;
-    const int64_t sl = P.A_coff[c] + (int64_t)(blockIdx.x / nc) * 4 + threadIdx.x / WAVE;
-    if (sl >= P.A_coff[c + 1]) return;
-    const int lane = lane_id();
-    const int32_t row = P.A_perm[sl * SELL_C + lane];
-    const int64_t s0 = P.A_sptr[sl];
-    const int W = (int)((P.A_sptr[sl + 1] - s0) / SELL_C);
-    const double v = sell_row(P.A_sidx, P.A_sval, P.x, s0 + lane, W, 0.0);
-    if (row >= 0) P.rpart[c * P.m + row] = v;
+    const bsls_panels &M = P.A;
+    const int64_t G = M.ngroups;
+    const int64_t g = blockIdx.x % G, rb = blockIdx.x / G;
+    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int64_t panel = rb * PANEL_WAVES + wv;
+    double *tab = lds;
+    double *acc = lds + BSLS_PANEL_CHUNK + wv * PANEL_ACC;
+    for (int i = lane; i < PANEL_ACC; i += WAVE) acc[i] = 0.0;
+    const int64_t c1 = M.group_chunk[g + 1];
+    for (int64_t c = M.group_chunk[g]; c < c1; ++c) {
+        const int64_t col0 = M.chunk_col[c];
+        __syncthreads();
+        panel_stage(tab, P.x + col0, (int)(M.chunk_col[c + 1] - col0));
+        __syncthreads();
+        if (panel < M.npanels) panel_segment<MODE>(M, panel * M.nchunks + c, tab, acc, nullptr);
+    }
+    if (panel >= M.npanels) return;
+    for (int i = lane; i < M.prow; i += WAVE) {
+        const int64_t row = panel * M.prow + i;
+        if (row < P.m) P.rpart[g * P.m + row] = acc[i];
+    }
 }
 
 // K1b: r = sum_c rpart[c] (+ target); optional ||r||^2 and the stopping test.
@@ -116,7 +133,7 @@ __global__ __launch_bounds__(256) void bb_k1b(bsls_bb_problem P, int64_t iter, d
     double sq[1] = {0.0};
     if (i < P.m) {
         double o = P.rpart[i];
-        for (int64_t c = 1; c < P.A_nchunk; ++c) o += P.rpart[c * P.m + i];
+        for (int64_t c = 1; c < P.A.ngroups; ++c) o += P.rpart[c * P.m + i];
         if (ADD) o += P.target[i];
         P.r[i] = o;
         sq[0] = o * o;
@@ -146,61 +163,81 @@ __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t it
         bb_record_f(P, iter, tot[0], iter > 0);
 }
 
-// K2: g = N'(A' r); with ITER also dg = g - g_prev and the BB sums.  Lane l of
-// wave w takes x-row i = 63 w + l; lane 63 is the halo (the next wave's first
-// row), so N' w = w_i - w_{i+1} is one shuffle.  The epilogue operands are
-// loaded before the row sum so their latency overlaps it.
-template <bool ITER>
-__global__ __launch_bounds__(256) void bb_k2(bsls_bb_problem P, const double *__restrict__ zc,
-                                             const double *__restrict__ zp,
-                                             const double *__restrict__ gp,
-                                             double *__restrict__ gout, double *part,
-                                             unsigned *ticket) {
-    __shared__ double red[16];
+// K2: g = N'(A' r); with ITER also dg = g - g_prev and the BB sums.  The
+// workgroup's 16 panels (x-rows) are summed over every chunk of r; then lane
+// position p of a panel has w_i in acc[p] and w_{i+1} in acc[p + 1] (the halo
+// row), so N'w = w_i - w_{i+1} needs no exchange.  The epilogue operands are
+// loaded before the chunk loop so their latency overlaps it.
+template <int MODE, bool ITER>
+__global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *__restrict__ zc,
+                                              const double *__restrict__ zp,
+                                              const double *__restrict__ gp,
+                                              double *__restrict__ gout, double *part,
+                                              unsigned *ticket) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
-    const int lane = lane_id();
-    const int64_t wv = (int64_t)blockIdx.x * 4 + threadIdx.x / WAVE;
-    const int64_t i = wv * (SELL_C - 1) + lane;
-    int32_t j = -1;
-    double gpj = 0.0, zcj = 0.0, zpj = 0.0;
-    if (lane < SELL_C - 1 && i < P.n) {
-        j = P.xz[i];
-        if (ITER && j >= 0) {
-            gpj = gp[j];
-            zcj = zc[j];
-            zpj = zp[j];
+    const bsls_panels &M = P.AT;
+    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
+    const int64_t i0 = panel * M.prow;
+    double *tab = lds;
+    double *acc = lds + BSLS_PANEL_CHUNK + wv * PANEL_ACC;
+    for (int i = lane; i < PANEL_ACC; i += WAVE) acc[i] = 0.0;
+    int32_t j[4];
+    double gpj[4], zcj[4], zpj[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int pos = lane + 64 * q;
+        const int64_t i = i0 + pos;
+        j[q] = (panel < M.npanels && pos < M.prow && i < P.n) ? P.xz[i] : -1;
+        gpj[q] = zcj[q] = zpj[q] = 0.0;
+        if (ITER && j[q] >= 0) {
+            gpj[q] = gp[j[q]];
+            zcj[q] = zc[j[q]];
+            zpj[q] = zp[j[q]];
         }
     }
-    double v = 0.0;
-    if (i < P.n) {
-        const int64_t sl = i / SELL_C;
-        const int64_t s0 = P.AT_sptr[sl];
-        const int W = (int)((P.AT_sptr[sl + 1] - s0) / SELL_C);
-        v = sell_row(P.AT_sidx, P.AT_sval, P.r, s0 + (i % SELL_C), W, 0.0);
+    const double *rs = (MODE == 2) ? P.colv + i0 : nullptr;
+    for (int64_t c = 0; c < M.nchunks; ++c) {
+        const int64_t col0 = M.chunk_col[c];
+        __syncthreads();
+        panel_stage(tab, P.r + col0, (int)(M.chunk_col[c + 1] - col0));
+        __syncthreads();
+        if (panel < M.npanels) panel_segment<MODE>(M, panel * M.nchunks + c, tab, acc, rs);
     }
-    const double vn = __shfl_down(v, 1, WAVE);
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    if (j >= 0) {
-        const double g = v - vn;
-        gout[j] = g;
-        if (ITER) {
-            const double dg = g - gpj;
-            const double dz = zcj - zpj;
-            acc[0] = dg;
-            acc[1] = dz * dg;
-            acc[2] = dg * dg;
-            acc[3] = g * g;
+    __syncthreads();   // tab becomes the reduction scratch below
+    double sums[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (j[q] >= 0) {
+            const int pos = lane + 64 * q;
+            const double g = acc[pos] - acc[pos + 1];
+            gout[j[q]] = g;
+            if (ITER) {
+                const double dg = g - gpj[q];
+                const double dz = zcj[q] - zpj[q];
+                sums[0] += dg;
+                sums[1] += dz * dg;
+                sums[2] += dg * dg;
+                sums[3] += g * g;
+            }
         }
     }
     if (!ITER) return;
-    block_sum<4>(acc, red);
+    block_sum<4>(sums, tab);
     double tot[4];
-    if (last_block_sum<4>(acc, part, ticket, tot, red) && threadIdx.x == 0) {
+    if (last_block_sum<4>(sums, part, ticket, tot, tab) && threadIdx.x == 0) {
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
         P.scal[BSLS_S_GG] = tot[3];
     }
+}
+
+// x entry i of N z; for a scaled incidence K1 gathers colv[i] * x_i instead,
+// the product SciPy's csr_matvec forms for every entry of column i.
+__device__ __forceinline__ void x_put(const bsls_bb_problem &P, int64_t i, double v) {
+    P.x[i] = P.colv ? P.colv[i] * v : v;
 }
 
 __device__ __forceinline__ int64_t zend(const bsls_bb_problem &P, int64_t b) {
@@ -259,9 +296,9 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
             const bool bstart = (B >> l) & 1ull;
             const int64_t blk = b0 + __popcll(B & mask_le(l)) - 1;
             const int64_t xi = z0 + l + blk;            // x index of this z entry
-            P.x[xi] = v - (bstart ? 0.0 : vprev);
+            x_put(P, xi, v - (bstart ? 0.0 : vprev));
             const bool bend = (l == L - 1) || (l < 63 && ((B >> (l + 1)) & 1ull));
-            if (bend) P.x[xi + 1] = 0.0 - v;            // (N z)_last = -z_last
+            if (bend) x_put(P, xi + 1, 0.0 - v);        // (N z)_last = -z_last
         }
     } else if (l == 0) {
         // one block longer than a wave: serial PAVA in global memory
@@ -276,10 +313,10 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
         for (int64_t j = z0; j < z0 + L; ++j) {
             const double v = clip01(zn[j]);
             zn[j] = v;
-            P.x[xo++] = v - prev;
+            x_put(P, xo++, v - prev);
             prev = v;
         }
-        P.x[xo] = 0.0 - prev;
+        x_put(P, xo, 0.0 - prev);
     }
 }
 
@@ -298,23 +335,52 @@ __global__ __launch_bounds__(256) void bb_z2x(bsls_bb_problem P, const double *_
     int64_t xo = xs;
     for (int64_t j = zs; j < ze; ++j) {
         const double v = z[j];
-        P.x[xo++] = v - prev;
+        x_put(P, xo++, v - prev);
         prev = v;
     }
-    P.x[xo] = 0.0 - prev;
+    x_put(P, xo, 0.0 - prev);
+}
+
+// 155 KB of dynamic LDS (one chunk + the 16 waves' row sums): opt in once per
+// kernel instance.
+template <typename K>
+static void allow_lds(K kernel) {
+    static bool done = false;
+    if (!done) {
+        (void)hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)PANEL_LDS);
+        done = true;
+    }
+}
+
+template <int MODE, bool ADD, bool REDUCE, bool ITER>
+static void launch_k1_mode(const bsls_bb_problem &P, int64_t iter, const BBWork &w,
+                           hipStream_t st) {
+    const int64_t rbs = (P.A.npanels + PANEL_WAVES - 1) / PANEL_WAVES;
+    allow_lds(bb_k1a<MODE, ITER>);
+    bb_k1a<MODE, ITER><<<(int)(P.A.ngroups * rbs), 1024, PANEL_LDS, st>>>(P);
+    bb_k1b<ADD, REDUCE, ITER><<<grid_for(P.m, 256), 256, 0, st>>>(P, iter, w.p1, w.tk1);
 }
 
 template <bool ADD, bool REDUCE, bool ITER>
 static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, hipStream_t st) {
-    const int ga = (int)(P.A_nchunk * ((P.A_maxsl + 3) / 4));
-    bb_k1a<ITER><<<ga, 256, 0, st>>>(P);
-    bb_k1b<ADD, REDUCE, ITER><<<grid_for(P.m, 256), 256, 0, st>>>(P, iter, w.p1, w.tk1);
+    if (P.colv) launch_k1_mode<0, ADD, REDUCE, ITER>(P, iter, w, st);
+    else launch_k1_mode<1, ADD, REDUCE, ITER>(P, iter, w, st);
+}
+
+template <int MODE, bool ITER>
+static void launch_k2_mode(const bsls_bb_problem &P, const double *zc, const double *zp,
+                           const double *gp, double *gout, const BBWork &w, hipStream_t st) {
+    allow_lds(bb_k2<MODE, ITER>);
+    bb_k2<MODE, ITER><<<grid_for(P.AT.npanels, PANEL_WAVES), 1024, PANEL_LDS, st>>>(
+        P, zc, zp, gp, gout, w.p2, w.tk2);
 }
 
 template <bool ITER>
 static void launch_k2(const bsls_bb_problem &P, const double *zc, const double *zp,
                       const double *gp, double *gout, const BBWork &w, hipStream_t st) {
-    bb_k2<ITER><<<grid_for(P.n, K2_ROWS), 256, 0, st>>>(P, zc, zp, gp, gout, w.p2, w.tk2);
+    if (P.colv) launch_k2_mode<2, ITER>(P, zc, zp, gp, gout, w, st);
+    else launch_k2_mode<1, ITER>(P, zc, zp, gp, gout, w, st);
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
@@ -322,12 +388,24 @@ static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, 
     bb_k3<<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.wsc);
 }
 
+static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t halo,
+                      bool need_val) {
+    if (M.rows != rows || M.cols != cols || M.halo != halo) return false;
+    if (M.prow < 1 || M.prow + halo > PANEL_ACC || M.npanels != (rows + M.prow - 1) / M.prow)
+        return false;
+    if (M.nchunks < 1 || M.ngroups < 1 || M.ngroups > M.nchunks) return false;
+    if (!M.chunk_col || !M.group_chunk || !M.ent_off || !M.perm_off || !M.dl_off || !M.dlen ||
+        !M.perm || !M.ent)
+        return false;
+    return need_val ? M.val != nullptr : true;
+}
+
 static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
-    if (!p->A_sidx || !p->A_sval || !p->A_sptr || !p->A_perm || !p->A_coff || !p->rpart)
+    const bool general = p->colv == nullptr;
+    if (!panels_ok(p->A, p->m, p->n, 0, general) || !panels_ok(p->AT, p->n, p->m, 1, general) ||
+        p->AT.ngroups != 1 || !p->rpart)
         return BSLS_E_ARG;
-    if (p->A_nchunk < 1 || p->A_maxsl < 1) return BSLS_E_ARG;
-    if (!p->AT_sidx || !p->AT_sval || !p->AT_sptr) return BSLS_E_ARG;
     if (!p->target || !p->xstarts || !p->zstarts || !p->xz) return BSLS_E_ARG;
     if (!p->pk_z0 || !p->pk_b0 || !p->pk_mask || !p->pk_len || p->npacks < 1) return BSLS_E_ARG;
     if (!p->z[0] || !p->z[1] || !p->g[0] || !p->g[1] || !p->x || !p->r || !p->scal || !p->work)

@@ -69,85 +69,213 @@ class DeviceCSR:
         return (out, sq) if want_sq else out
 
 
-def build_sell(A, window=0, col_lo=None, col_hi=None, C=64):
-    """SELL-C-64 image of the CSR matrix A (rows of A restricted to columns
-    [col_lo, col_hi), global column indices kept).  window > 0 sorts rows by
-    length (longest first) inside windows of that many rows to cut padding;
-    window = 0 keeps the row order.  Returns host arrays
-    (sidx int32 with -1 padding, sval f64, sptr int64 per slice, slot_row int32)."""
-    A = sps.csr_matrix(A)
-    A.sort_indices()
-    m, n = A.shape
-    if col_lo is not None:
-        A = A[:, col_lo:col_hi].tocsr()
-        A.sort_indices()
-        A.indices = A.indices + col_lo
-    ip = A.indptr.astype(np.int64)
-    lens = np.diff(ip)
-    if window > 0:
-        key = (np.arange(m) // window) * (int(lens.max(initial=0)) + 1) - lens
-        order = np.argsort(key, kind='stable')
+def even_bounds(lo, hi, parts):
+    """parts + 1 increasing even column bounds from lo to hi (hi itself may be odd):
+    chunk starts stay 16-B aligned for the LDS staging (panels.hpp)."""
+    b = np.round(np.linspace(lo, hi, parts + 1) / 2.0).astype(np.int64) * 2
+    b[0], b[-1] = lo, hi
+    return np.unique(b)
+
+
+def chunk_plan(ncols, ngroups, chunk=None):
+    """Column chunks (<= chunk wide) nested in `ngroups` groups of near-equal
+    width.  Returns (chunk_col, group_chunk)."""
+    chunk = int(chunk or _native.PANEL_CHUNK)
+    ngroups = max(1, min(int(ngroups), (ncols + 1) // 2))
+    gb = even_bounds(0, ncols, ngroups)
+    cols, gch = [0], [0]
+    for g in range(gb.size - 1):
+        w = int(gb[g + 1] - gb[g])
+        k = max(1, -(-w // chunk))
+        cb = even_bounds(int(gb[g]), int(gb[g + 1]), k)
+        while np.any(np.diff(cb) > chunk):
+            k += 1
+            cb = even_bounds(int(gb[g]), int(gb[g + 1]), k)
+        cols.extend(cb[1:].tolist())
+        gch.append(len(cols) - 1)
+    return np.array(cols, dtype=np.int64), np.array(gch, dtype=np.int64)
+
+
+def build_panels(M, prow, halo=False, chunk_col=None, group_chunk=None, values=True):
+    """Panel image of the CSR matrix M (include/bsls_hip.h struct bsls_panels,
+    csrc/panels.hpp).  Host arrays in a dict; `values=False` drops the entry
+    values (scaled incidence).  Vectorised: two sorts over the entries."""
+    M = sps.csr_matrix(M)
+    M.sort_indices()
+    R, C = M.shape
+    prow = int(prow)
+    if not 1 <= prow <= _native.PANEL_ROWS or prow + int(halo) > 256:
+        raise ValueError('prow out of range')
+    if chunk_col is None:
+        chunk_col, group_chunk = chunk_plan(C, 1)
+    chunk_col = np.asarray(chunk_col, dtype=np.int64)
+    group_chunk = np.asarray(group_chunk, dtype=np.int64)
+    if np.any(np.diff(chunk_col) > _native.PANEL_CHUNK) or np.any(chunk_col[:-1] % 2):
+        raise ValueError('bad chunk plan')
+    nch = chunk_col.size - 1
+    npan = max(1, -(-R // prow))
+    ip = M.indptr.astype(np.int64)
+    rows = np.repeat(np.arange(R, dtype=np.int64), np.diff(ip))
+    cols = M.indices.astype(np.int64)
+    vals = M.data
+    pn = rows // prow
+    lr = rows - pn * prow
+    if halo:
+        # row 0 of panel p > 0 is also local row prow of panel p - 1
+        h = np.nonzero((lr == 0) & (pn > 0))[0]
+        pn = np.concatenate([pn, pn[h] - 1])
+        lr = np.concatenate([lr, np.full(h.size, prow, dtype=np.int64)])
+        cols = np.concatenate([cols, cols[h]])
+        vals = np.concatenate([vals, vals[h]])
+    ch = np.searchsorted(chunk_col, cols, side='right') - 1
+    seg = pn * nch + ch
+    W = prow + 1
+    key = seg * W + lr
+    order = np.argsort(key, kind='stable')      # keeps column order inside a row
+    key = key[order]
+    cols = cols[order]
+    ch = ch[order]
+    vals = vals[order]
+    E = key.size
+    nsegs = npan * nch
+    if E:
+        newp = np.empty(E, dtype=bool)
+        newp[0] = True
+        np.not_equal(key[1:], key[:-1], out=newp[1:])
+        pstart = np.nonzero(newp)[0]
+        pid = np.cumsum(newp) - 1
+        k = np.arange(E, dtype=np.int64) - pstart[pid]
+        cnt = np.diff(np.append(pstart, E))
+        pkey = key[pstart]
+        pseg = pkey // W
+        plr = pkey - pseg * W
+        porder = np.lexsort((plr, -cnt, pseg))
+        pseg_s = pseg[porder]
+        seg_first = np.searchsorted(pseg_s, np.arange(nsegs + 1))
+        pos = np.empty(pstart.size, dtype=np.int64)
+        pos[porder] = np.arange(pstart.size) - seg_first[pseg_s]
+        D = np.zeros(nsegs, dtype=np.int64)
+        nonempty = seg_first[1:] > seg_first[:-1]
+        D[nonempty] = cnt[porder[seg_first[:-1][nonempty]]]
+        dl_off = np.concatenate(([0], np.cumsum(D)))
+        seg_e = pseg[pid]
+        di = dl_off[seg_e] + k
+        dlen = np.bincount(di, minlength=int(dl_off[-1]))
+        G = np.concatenate(([0], np.cumsum(dlen)))
+        dest = G[di] + pos[pid]
+        ent = np.empty(E, dtype=np.uint16)
+        ent[dest] = (cols - chunk_col[ch]).astype(np.uint16)
+        val = None
+        if values:
+            val = np.empty(E, dtype=np.float64)
+            val[dest] = vals
+        perm = plr[porder].astype(np.uint8)
+        ent_off = G[dl_off]
+        perm_off = seg_first.astype(np.int64)
     else:
-        order = np.arange(m)
-    nsl = (m + C - 1) // C
-    slot_row = np.full(nsl * C, -1, dtype=np.int32)
-    slot_row[:m] = order
-    slot_len = np.zeros(nsl * C, dtype=np.int64)
-    slot_len[:m] = lens[order]
-    W = slot_len.reshape(nsl, C).max(axis=1)
-    sptr = np.concatenate(([0], np.cumsum(W * C))).astype(np.int64)
-    sidx = np.full(int(sptr[-1]), -1, dtype=np.int32)
-    sval = np.zeros(int(sptr[-1]), dtype=np.float64)
-    inv = np.empty(m, dtype=np.int64)
-    inv[order] = np.arange(m)
-    rows = np.repeat(np.arange(m, dtype=np.int64), lens)
-    k = np.arange(A.nnz, dtype=np.int64) - ip[rows]
-    slot = inv[rows]
-    dest = sptr[slot // C] + k * C + slot % C
-    sidx[dest] = A.indices
-    sval[dest] = A.data
-    return sidx, sval, sptr, slot_row
+        dl_off = np.zeros(nsegs + 1, dtype=np.int64)
+        dlen = np.zeros(1, dtype=np.int64)
+        ent = np.zeros(1, dtype=np.uint16)
+        val = np.zeros(1) if values else None
+        perm = np.zeros(1, dtype=np.uint8)
+        ent_off = np.zeros(nsegs + 1, dtype=np.int64)
+        perm_off = np.zeros(nsegs + 1, dtype=np.int64)
+    return dict(rows=R, cols=C, prow=prow, halo=int(bool(halo)), npanels=npan, nchunks=nch,
+                ngroups=group_chunk.size - 1, chunk_col=chunk_col, group_chunk=group_chunk,
+                ent_off=ent_off, perm_off=perm_off, dl_off=dl_off,
+                dlen=dlen.astype(np.uint16), perm=perm, ent=ent, val=val, nnz=E)
 
 
-class SellChunked:
-    """A for K1: SELL-C-64 per column chunk (rows length-sorted in windows),
-    concatenated; chunk c is processed by workgroups b with b % nchunk == c."""
+def panels_matvec(img, x, colv=None):
+    """Host restatement of the kernels' walk over a panel image (panel_segment
+    in csrc/panels.hpp): per chunk group, row sums entry by entry in storage
+    order; the group partials then added in group order (K1b).  Returns the
+    kernels' bit pattern and, for the last group, the per-panel sums including
+    halo rows.  Test helper (numpy, vectorised per diagonal)."""
+    R, prow, halo = img['rows'], img['prow'], img['halo']
+    nch = img['nchunks']
+    x = np.asarray(x, dtype=np.float64)
+    parts = []
+    for g in range(img['ngroups']):
+        acc = np.zeros((img['npanels'], prow + halo))
+        for c in range(img['group_chunk'][g], img['group_chunk'][g + 1]):
+            c0 = img['chunk_col'][c]
+            for p in range(img['npanels']):
+                sgi = p * nch + c
+                d0, d1 = img['dl_off'][sgi], img['dl_off'][sgi + 1]
+                if d0 == d1:
+                    continue
+                e = img['ent_off'][sgi]
+                n0 = int(img['dlen'][d0])
+                po = img['perm_off'][sgi]
+                rr = img['perm'][po:po + n0].astype(np.int64)
+                s = acc[p, rr].copy()
+                for d in range(d0, d1):
+                    ln = int(img['dlen'][d])
+                    t = x[c0 + img['ent'][e:e + ln].astype(np.int64)]
+                    if img['val'] is not None:
+                        s[:ln] = s[:ln] + img['val'][e:e + ln] * t
+                    elif colv is not None:
+                        s[:ln] = s[:ln] + colv[p * prow + rr[:ln]] * t
+                    else:
+                        s[:ln] = s[:ln] + t
+                    e += ln
+                acc[p, rr] = s
+        parts.append(acc)
+    out = parts[0][:, :prow].reshape(-1)[:R].copy()
+    for acc in parts[1:]:
+        out = out + acc[:, :prow].reshape(-1)[:R]
+    return out, parts[-1]
 
-    def __init__(self, A, nchunk=8, window=4096):
+
+def scaled_incidence_scale(A):
+    """colv with A[i, j] == colv[j] for every stored entry, or None
+    (bsls_utils.assert_scaled_incidence, bsls_utils.py:494-507, made exact)."""
+    C = sps.csc_matrix(A)
+    C.sort_indices()
+    n = C.shape[1]
+    lens = np.diff(C.indptr)
+    colv = np.zeros(n)
+    has = lens > 0
+    colv[has] = C.data[C.indptr[:-1][has]]
+    if C.nnz and not np.array_equal(C.data, np.repeat(colv, lens)):
+        return None
+    return colv
+
+
+class DevicePanels:
+    """A panel image on the device + the ctypes struct pointing at it."""
+
+    def __init__(self, M, prow, halo=False, ngroups=1, values=True):
         torch = _torch()
-        A = sps.csr_matrix(A)
-        m, n = A.shape
-        nchunk = max(1, min(int(nchunk), n))
-        bounds = np.linspace(0, n, nchunk + 1).astype(np.int64)
-        parts = [build_sell(A, window, bounds[c], bounds[c + 1]) for c in range(nchunk)]
-        off = 0
-        sptrs, coff = [], [0]
-        for (_, _, sp, _) in parts:
-            sptrs.append(sp[:-1] + off)
-            off += int(sp[-1])
-            coff.append(coff[-1] + sp.shape[0] - 1)
-        sptr = np.concatenate(sptrs + [np.array([off], dtype=np.int64)])
-        self.nchunk = nchunk
-        self.maxsl = int(max(sp.shape[0] - 1 for (_, _, sp, _) in parts))
-        self.sidx = torch.from_numpy(np.concatenate([p[0] for p in parts])).cuda()
-        self.sval = torch.from_numpy(np.concatenate([p[1] for p in parts])).cuda()
-        self.sptr = torch.from_numpy(sptr).cuda()
-        self.perm = torch.from_numpy(np.concatenate([p[3] for p in parts])).cuda()
-        self.coff = torch.from_numpy(np.array(coff, dtype=np.int64)).cuda()
-        self.padded = off
-        self.nnz = int(A.nnz)
+        ccol, gch = chunk_plan(M.shape[1], ngroups)
+        img = build_panels(M, prow, halo, ccol, gch, values)
+        self.img = img
+        self.nnz = img['nnz']
+        self.t = {}
+        for k in ('chunk_col', 'group_chunk', 'ent_off', 'perm_off', 'dl_off'):
+            self.t[k] = torch.from_numpy(np.ascontiguousarray(img[k], dtype=np.int64)).cuda()
+        self.t['dlen'] = torch.from_numpy(img['dlen'].view(np.int16)).cuda()
+        self.t['perm'] = torch.from_numpy(img['perm']).cuda()
+        self.t['ent'] = torch.from_numpy(img['ent'].view(np.int16)).cuda()
+        if img['val'] is not None:
+            self.t['val'] = torch.from_numpy(img['val']).cuda()
+        S = _native.Panels()
+        for k in ('rows', 'cols', 'prow', 'halo', 'npanels', 'nchunks', 'ngroups'):
+            setattr(S, k, int(img[k]))
+        for k, v in self.t.items():
+            setattr(S, k, v.data_ptr())
+        self.struct = S
+
+    def bytes(self):
+        return sum(v.numel() * v.element_size() for v in self.t.values())
 
 
-class SellRows:
-    """A' for K2: SELL-C-64 with rows in order."""
-
-    def __init__(self, AT):
-        torch = _torch()
-        sidx, sval, sptr, _ = build_sell(AT, 0)
-        self.sidx = torch.from_numpy(sidx).cuda()
-        self.sval = torch.from_numpy(sval).cuda()
-        self.sptr = torch.from_numpy(sptr).cuda()
-        self.padded = int(sptr[-1])
+def panel_rows(rows, workgroups_per_group, waves=16):
+    """Rows per panel so one launch is about `workgroups_per_group` workgroups of
+    16 panels per group (one per CU), within 64 .. BSLS_PANEL_ROWS."""
+    want = -(-rows // (workgroups_per_group * waves))
+    return int(min(_native.PANEL_ROWS, max(min(64, rows), want)))
 
 
 class BlockLayout:
@@ -216,7 +344,7 @@ class BBEngine:
     """
 
     def __init__(self, A, b, block_sizes, options=None, early_exit=True, A_dev=None,
-                 AT_dev=None, AT=None, target=None, x0=None):
+                 AT_dev=None, AT=None, target=None, x0=None, general=False):
         torch = _torch()
         L = _native.lib()
         self.layout = lay = BlockLayout(block_sizes)
@@ -226,10 +354,14 @@ class BBEngine:
         AT = sps.csr_matrix(AT) if AT is not None else A.T.tocsr()
         self.A = A_dev or DeviceCSR(A)
         self.AT = AT_dev or DeviceCSR(AT)
-        # the fused kernels' images: A chunked by columns (K1), A' by rows (K2)
-        self.A_sell = SellChunked(A)
-        self.AT_sell = SellRows(AT)
         self.m, self.n, self.nz = A.shape[0], lay.n, lay.nz
+        # the fused kernels' panel images: A with its column chunks in 8 XCD
+        # groups (K1), A' with halo rows (K2); values dropped for a scaled incidence
+        colv = None if general else scaled_incidence_scale(A)
+        self.scaled = colv is not None
+        self.A_pan = DevicePanels(A, panel_rows(self.m, 32), False, 8, values=not self.scaled)
+        self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), True, 1,
+                                   values=not self.scaled)
         opts = options or {}
         self.options = dict(opts)
         dev = dict(dtype=torch.float64, device='cuda')
@@ -255,15 +387,13 @@ class BBEngine:
         self.scal = torch.zeros(_native.S_COUNT, **dev)
         self.work = torch.zeros(L.bsls_bb_workspace_size(self.m, self.n, self.nz),
                                 dtype=torch.uint8, device='cuda')
-        self.rpart = torch.zeros(self.A_sell.nchunk * self.m, **dev)
+        self.rpart = torch.zeros(self.A_pan.img['ngroups'] * self.m, **dev)
+        self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
         P = BBProblem()
         P.m, P.n, P.nz, P.nblocks = self.m, lay.n, lay.nz, lay.p
-        S = self.A_sell
-        P.A_sidx, P.A_sval, P.A_sptr = S.sidx.data_ptr(), S.sval.data_ptr(), S.sptr.data_ptr()
-        P.A_perm, P.A_coff = S.perm.data_ptr(), S.coff.data_ptr()
-        P.A_nchunk, P.A_maxsl, P.rpart = S.nchunk, S.maxsl, self.rpart.data_ptr()
-        T = self.AT_sell
-        P.AT_sidx, P.AT_sval, P.AT_sptr = T.sidx.data_ptr(), T.sval.data_ptr(), T.sptr.data_ptr()
+        P.A, P.AT = self.A_pan.struct, self.AT_pan.struct
+        P.colv = self.colv.data_ptr() if self.scaled else None
+        P.rpart = self.rpart.data_ptr()
         P.target = self.target.data_ptr()
         P.xstarts, P.zstarts, P.xz = (lay.xstarts.data_ptr(), lay.zstarts.data_ptr(),
                                       lay.xz.data_ptr())

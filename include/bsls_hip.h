@@ -110,8 +110,8 @@ int bsls_csr_spmv(int64_t m, const int64_t *d_indptr, const int32_t *d_indices,
  * Replaces, per iteration, BB.solve's loop body (python/BB.py:17-41) over the
  * closures of main.solve_in_z (python/main.py:53-65) and the stopping rule
  * solvers.stopping (python/solvers.py:40-63):
- *   K1  r = A x + target (= A N z + A x0 - b), ||r||^2, stop test (SpMV, A SELL)
- *   K2  g = N' A' r, dg = g - g_prev, BB dot products      (SpMV', explicit A' SELL)
+ *   K1  r = A x + target (= A N z + A x0 - b), ||r||^2, stop test (SpMV, A panels)
+ *   K2  g = N' A' r, dg = g - g_prev, BB dot products      (SpMV', explicit A' panels)
  *   K3  z <- clip01(PAVA(z - t g)), x <- N z               (per-block projection)
  * The caller owns every buffer (see struct); bsls_bb_prologue() performs
  * BB.py:14-15 (g_prev = grad(z0 + 1)) and evaluates r(z0).  Iterations keep
@@ -137,23 +137,45 @@ enum {
     BSLS_STOP_GRAD = 3,       /* solvers.py:51-54 */
     BSLS_STOP_DG = 4          /* solvers.py:59-62 */
 };
+/* Panel image of a sparse matrix M (rows x cols) for the fused SpMVs: the
+ * LDS-chunked jagged-diagonal format of csrc/panels.hpp (built on the host by
+ * device.build_panels).  Rows are cut into panels of `prow` rows (one wave
+ * each; K2's panels also carry the next panel's first row, `halo` = 1),
+ * columns into chunks that fit the LDS (chunk c = columns
+ * [chunk_col[c], chunk_col[c+1]), at most BSLS_PANEL_CHUNK wide).  Segment
+ * s = panel * nchunks + chunk lists the panel's entries in that chunk: the
+ * rows present, sorted by their entry count (perm: row within the panel, per
+ * position), then diagonal d = every present row's d-th entry in that chunk,
+ * positions 0 .. dlen[d]-1.  An entry is its column offset in the chunk
+ * (ent, uint16) and, unless the matrix is a scaled incidence, its value. */
+#define BSLS_PANEL_CHUNK 15360
+#define BSLS_PANEL_ROWS 255
+typedef struct bsls_panels {
+    int64_t rows, cols;
+    int64_t prow;                   /* rows per panel, 1 .. BSLS_PANEL_ROWS */
+    int64_t halo;                   /* 1: segment rows are prow + 1 (row prow = next panel's row 0) */
+    int64_t npanels, nchunks;
+    int64_t ngroups;                /* chunk groups: K1 runs one workgroup per (group, 16 panels) */
+    const int64_t *chunk_col;       /* nchunks + 1 */
+    const int64_t *group_chunk;     /* ngroups + 1 */
+    const int64_t *ent_off;         /* npanels * nchunks + 1: first entry of each segment */
+    const int64_t *perm_off;        /* npanels * nchunks + 1: first perm byte of each segment */
+    const int64_t *dl_off;          /* npanels * nchunks + 1: first diagonal of each segment */
+    const uint16_t *dlen;           /* rows having a d-th entry, per diagonal */
+    const uint8_t *perm;
+    const uint16_t *ent;
+    const double *val;              /* per entry, or NULL when scaled (see colv) */
+} bsls_panels;
+
 typedef struct bsls_bb_problem {
     int64_t m, n, nz, nblocks;      /* rows, x length, z length (n - nblocks), blocks */
-    /* A for K1: sliced ELLPACK (SELL-C-64, column-major slices, padding column
-     * -1), split into A_nchunk column chunks; workgroup b works on chunk
-     * b % A_nchunk so each XCD's L2 holds one chunk of x (speed only). */
-    const int32_t *A_sidx;
-    const double *A_sval;
-    const int64_t *A_sptr;          /* global slice starts (entries), total slices + 1 */
-    const int32_t *A_perm;          /* row of slot s*64 + lane (-1 = empty slot) */
-    const int64_t *A_coff;          /* A_nchunk + 1 slice offsets of the chunks */
-    int64_t A_nchunk;
-    int64_t A_maxsl;                /* most slices in one chunk */
-    double *rpart;                  /* A_nchunk x m partial residuals */
-    /* A' for K2: SELL-C-64 with rows in order (row i at slice i/64, lane i%64) */
-    const int32_t *AT_sidx;
-    const double *AT_sval;
-    const int64_t *AT_sptr;         /* ceil(n/64) + 1 */
+    bsls_panels A;                  /* K1: A, chunks grouped per XCD (ngroups partials) */
+    bsls_panels AT;                 /* K2: A', halo = 1, one group */
+    /* scaled incidence (bsls_utils.assert_scaled_incidence, bsls_utils.py:494):
+     * every stored entry of column j equals colv[j]; then A.val / AT.val are NULL,
+     * x holds colv * (N z) and K2 multiplies by colv of its row.  NULL otherwise. */
+    const double *colv;
+    double *rpart;                  /* A.ngroups x m partial residuals */
     const double *target;           /* m: A x0 - b (python/main.py:48) */
     const int64_t *xstarts;         /* nblocks, x-space block starts, xstarts[0] = 0 */
     const int64_t *zstarts;         /* nblocks, z-space block starts (xstarts[b] - b) */
@@ -167,7 +189,7 @@ typedef struct bsls_bb_problem {
     int64_t npacks;
     double *z[2];                   /* ping-pong iterate buffers, nz each */
     double *g[2];                   /* ping-pong gradient buffers, nz each */
-    double *x;                      /* n: N z of the current iterate (x0 is in target) */
+    double *x;                      /* n: N z of the current iterate (x0 is in target), times colv if set */
     double *r;                      /* m: residual */
     double *scal;                   /* BSLS_S_COUNT doubles */
     void *work;                     /* bsls_bb_workspace_size() bytes */

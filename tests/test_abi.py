@@ -6,6 +6,8 @@ import subprocess
 
 import pytest
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 @pytest.fixture(scope='module')
 def native():
@@ -52,10 +54,32 @@ def test_host_only_entry_points(native):
     assert L.bsls_md_workspace_size(50_000) > 0
 
 
-def test_bb_struct_layout_matches_header(native):
-    # struct bsls_bb_problem: 4 int64; A SELL (5 ptr, 2 int64, rpart); A' SELL (3 ptr);
-    # 4 ptr; packs (4 ptr + int64); z[2], g[2], x, r, scal, work; 2 int64; 1 double; 2 int32
-    assert ctypes.sizeof(native.BBProblem) == 32 + 64 + 24 + 32 + 40 + 64 + 16 + 8 + 8
+def _c_layout(tmp_path, struct, fields):
+    """sizeof and offsetof as the C compiler lays the header's struct out."""
+    src = tmp_path / 'lay.c'
+    body = ''.join('printf("%%zu\\n", offsetof(%s, %s));' % (struct, f) for f in fields)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "bsls_hip.h"\n'
+                   'int main(void){printf("%%zu\\n", sizeof(%s));%s return 0;}\n' % (struct, body))
+    exe = tmp_path / 'lay'
+    subprocess.run(['gcc', '-I', os.path.join(ROOT, 'include'), str(src), '-o', str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    return [int(v) for v in out]
+
+
+@pytest.mark.parametrize('struct,cls', [('bsls_bb_problem', 'BBProblem'), ('bsls_panels', 'Panels')])
+def test_struct_layout_matches_header(native, tmp_path, struct, cls):
+    C = getattr(native, cls)
+    names = [f[0] for f in C._fields_]
+    want = _c_layout(tmp_path, struct, names)
+    got = [ctypes.sizeof(C)] + [getattr(C, f).offset for f in names]
+    assert got == want
+
+
+def test_panel_limits_match_header(native):
+    hdr = open(os.path.join(ROOT, 'include', 'bsls_hip.h')).read()
+    assert '#define BSLS_PANEL_CHUNK %d' % native.PANEL_CHUNK in hdr
+    assert '#define BSLS_PANEL_ROWS %d' % native.PANEL_ROWS in hdr
 
 
 def test_tile_planner(native):

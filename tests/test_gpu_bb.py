@@ -61,23 +61,67 @@ def test_bb_main_problems_converge(cuda, golden):
         assert abs(eng.iterations - ref_last) <= max(10, ref_last // 4), (eng.iterations, ref_last)
 
 
-def test_bb_fixed_iterations_match_oracle_at_scale(cuda, orc):
-    """A 100k-route synthetic problem, iterates at 1, 10, 50 vs the oracle."""
-    from device import BBEngine
+@pytest.fixture(scope='module')
+def shard100k(orc):
     from synthetic import make_shard, add_noise
     sh = make_shard(100_000, 5_000, 10_000, per_col=16, seed=11)
     b = add_noise(sh['Ax'], 0.02, seed=11)
-    want = [1, 10, 50]
     ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], 50, record_every=1)
-    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 50, 'opt_tol': 1e-30})
+    return sh, b, ref
+
+
+@pytest.mark.parametrize('general', [False, True])
+def test_bb_fixed_iterations_match_oracle_at_scale(cuda, shard100k, general):
+    """A 100k-route synthetic problem, iterates at 1, 10, 50 vs the oracle, with
+    the scaled-incidence panels (no values) and with stored values."""
+    from device import BBEngine
+    sh, b, ref = shard100k
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 50, 'opt_tol': 1e-30},
+                   general=general)
+    assert eng.scaled == (not general)
     rec = {}
 
     def log(i, s, dt):
         rec[i] = s
         return 0.0
     eng.solve(log=log, record_every=1, poll=1)
-    for i in want:
+    for i in (1, 10, 50):
         assert rel_err(rec[i], ref[i]) < 1e-6, (i, rel_err(rec[i], ref[i]))
+
+
+@pytest.mark.parametrize('general', [False, True])
+def test_k2_gradient_bit_exact_vs_scipy(cuda, shard100k, general):
+    """K2 alone (stage 3): w = A'r is summed in CSR order in LDS, so
+    g = N'(A'r) equals SciPy's N.T.dot(A.T.dot(r)) bit for bit."""
+    import torch
+    from device import BBEngine
+    from oracle import oracle as orc
+    sh, b, _ = shard100k
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 5, 'opt_tol': 1e-30},
+                   general=general)
+    r = np.random.RandomState(5).randn(eng.m)
+    eng.r.copy_(torch.from_numpy(r))
+    eng.stage(3, 0)
+    got = eng.g[0][:eng.nz].cpu().numpy()
+    N = orc.block_sizes_to_N(sh['block_sizes'])
+    want = N.T.tocsr().dot(sh['AT'].dot(r))
+    assert np.array_equal(got, want)
+
+
+def test_k1_residual_vs_scipy(cuda, shard100k):
+    """K1 alone (stage 7 at iteration 0): r = A x + target with 8 chunk-group
+    partials; equal to SciPy to rounding (1e-12 relative)."""
+    import torch
+    from device import BBEngine
+    sh, b, _ = shard100k
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 5, 'opt_tol': 1e-30})
+    x = np.random.RandomState(6).rand(eng.n)
+    xin = torch.from_numpy(eng.colv.cpu().numpy() * x if eng.scaled else x).cuda()
+    eng.x.copy_(xin)
+    eng.stage(7, 0)
+    got = eng.r.cpu().numpy()
+    want = sh['A'].dot(x) + eng.target.cpu().numpy()
+    assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
 
 
 def test_bb_deterministic(cuda):

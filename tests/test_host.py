@@ -152,31 +152,70 @@ def test_partition_blocks_balanced():
         partition_blocks(bs, bs, 501)
 
 
-def test_sell_image_roundtrip():
-    """The SELL-C-64 image (device.build_sell) holds every CSR entry once, in row
-    order inside each row, padding marked -1."""
+def _rand_csr(rs, R, C, dens):
+    return sps.random(R, C, density=dens, random_state=rs, format='csr')
+
+
+@pytest.mark.parametrize('R,C,dens,prow,halo,ngroups,chunk', [
+    (300, 500, 0.05, 64, False, 1, None),
+    (300, 500, 0.05, 7, True, 1, None),
+    (1000, 40000, 0.001, 64, False, 8, 4000),     # K1 shape: chunk groups
+    (2000, 70000, 0.0005, 100, True, 1, 4000),    # K2 shape: halo rows, many chunks
+    (1, 5, 1.0, 1, False, 1, None),
+    (64, 300, 0.9, 255, True, 1, 128),            # dense rows: > 64 diagonals per segment
+])
+def test_panel_image_walk_matches_scipy(R, C, dens, prow, halo, ngroups, chunk):
+    """The panel image (device.build_panels) walked in the kernels' order
+    (device.panels_matvec = panel_segment restated) gives SciPy's csr_matvec bit
+    for bit with one chunk group (K2), and to rounding with several (K1)."""
     import device
     rs = np.random.RandomState(SEED)
-    A = sps.random(300, 500, density=0.05, random_state=rs, format='csr')
-    for window, lo, hi in ((0, None, None), (64, None, None), (128, 100, 260)):
-        sidx, sval, sptr, slot_row = device.build_sell(A, window, lo, hi)
-        ref = A if lo is None else A[:, lo:hi]
-        rec = sps.lil_matrix(A.shape)
-        for s in range(sptr.shape[0] - 1):
-            W = (sptr[s + 1] - sptr[s]) // 64
-            for p in range(64):
-                row = slot_row[s * 64 + p]
-                cols = [sidx[sptr[s] + k * 64 + p] for k in range(W)]
-                vals = [sval[sptr[s] + k * 64 + p] for k in range(W)]
-                valid = [c for c in cols if c >= 0]
-                if row < 0:
-                    assert not valid
-                    continue
-                assert valid == sorted(valid)
-                for c, v in zip(cols, vals):
-                    if c >= 0:
-                        rec[row, c] = v
-        want = sps.csr_matrix(A.shape)
-        want = A.copy() if lo is None else sps.hstack([sps.csr_matrix((300, lo)), ref,
-                                                       sps.csr_matrix((300, 500 - hi))]).tocsr()
-        assert (sps.csr_matrix(rec) != want).nnz == 0
+    A = _rand_csr(rs, R, C, dens)
+    ccol, gch = device.chunk_plan(C, ngroups, chunk=chunk)
+    assert ccol[0] == 0 and ccol[-1] == C and np.all(ccol[:-1] % 2 == 0)
+    assert np.all(np.diff(ccol) <= (chunk or 15360)) and gch[-1] == ccol.size - 1
+    img = device.build_panels(A, prow, halo, ccol, gch)
+    assert img['nnz'] == A.nnz + (halo and sum(A[p * prow].nnz for p in range(1, img['npanels'])))
+    assert img['dlen'].max() <= prow + halo
+    x = rs.randn(C)
+    y, acc = device.panels_matvec(img, x)
+    ref = A.dot(x)
+    if img['ngroups'] == 1:
+        assert np.array_equal(y, ref)
+    else:
+        assert np.allclose(y, ref, rtol=1e-13, atol=1e-13)
+    if halo:
+        assert np.array_equal(acc[:-1, prow], acc[1:, 0])
+
+
+def test_panel_image_scaled_incidence():
+    """Scaled incidence: no values stored; K1 walks colv*x, K2 multiplies by its
+    row's colv, bit-identical to SciPy's A'r (the products are the same)."""
+    import device
+    rs = np.random.RandomState(SEED)
+    A = sps.random(500, 3000, density=0.01, random_state=rs, format='csc')
+    A.data[:] = np.repeat(np.floor(rs.rand(3000) * 1000) + 1, np.diff(A.indptr))
+    A = A.tocsr()
+    colv = device.scaled_incidence_scale(A)
+    assert colv is not None
+    B = A.copy()
+    B.data[0] += 1.0
+    assert device.scaled_incidence_scale(B) is None
+    x = rs.rand(3000)
+    img = device.build_panels(A, 64, False, *device.chunk_plan(3000, 1, chunk=256), values=False)
+    assert img['val'] is None
+    y, _ = device.panels_matvec(img, colv * x)
+    assert np.array_equal(y, A.dot(x))
+    AT = A.T.tocsr()
+    r = rs.randn(500)
+    img = device.build_panels(AT, 64, True, *device.chunk_plan(500, 1, chunk=128), values=False)
+    y, _ = device.panels_matvec(img, r, colv=colv)
+    assert np.array_equal(y, AT.dot(r))
+
+
+def test_panel_rows_choice():
+    import device
+    assert device.panel_rows(100_000, 32) == 196          # C3 K1: 8 groups x 32 workgroups
+    assert device.panel_rows(1_000_000, 256) == 245       # C3 K2: 256 workgroups
+    assert device.panel_rows(10, 256) == 10
+    assert device.panel_rows(10_000_000, 256) == 255
