@@ -35,16 +35,17 @@ _sz = ctypes.c_size_t
 _int = ctypes.c_int
 
 
-PANEL_CHUNK = 15360      # BSLS_PANEL_CHUNK
+PANEL_CHUNK = 20224      # BSLS_PANEL_CHUNK
 PANEL_ROWS = 255         # BSLS_PANEL_ROWS
+PANEL_WAVES = 16         # BSLS_PANEL_WAVES
 
 
 class Panels(ctypes.Structure):
     """Mirror of struct bsls_panels (include/bsls_hip.h)."""
     _fields_ = [('rows', _i64), ('cols', _i64), ('prow', _i64), ('halo', _i64),
-                ('npanels', _i64), ('nchunks', _i64), ('ngroups', _i64),
-                ('chunk_col', _vp), ('group_chunk', _vp), ('ent_off', _vp), ('perm_off', _vp),
-                ('dl_off', _vp), ('dlen', _vp), ('perm', _vp), ('ent', _vp), ('val', _vp)]
+                ('npanels', _i64), ('nchunks', _i64), ('ngroups', _i64), ('tab_cap', _i64),
+                ('chunk_col', _vp), ('group_chunk', _vp), ('ent_off', _vp), ('cnt_off', _vp),
+                ('seg_info', _vp), ('cnt', _vp), ('ent', _vp), ('val', _vp)]
 
 
 class BBProblem(ctypes.Structure):

@@ -105,21 +105,15 @@ __global__ __launch_bounds__(1024) void bb_k1a(bsls_bb_problem P) {
     const int64_t g = blockIdx.x % G, rb = blockIdx.x / G;
     const int wv = threadIdx.x / WAVE, lane = lane_id();
     const int64_t panel = rb * PANEL_WAVES + wv;
-    double *tab = lds;
-    double *acc = lds + BSLS_PANEL_CHUNK + wv * PANEL_ACC;
-    for (int i = lane; i < PANEL_ACC; i += WAVE) acc[i] = 0.0;
-    const int64_t c1 = M.group_chunk[g + 1];
-    for (int64_t c = M.group_chunk[g]; c < c1; ++c) {
-        const int64_t col0 = M.chunk_col[c];
-        __syncthreads();
-        panel_stage(tab, P.x + col0, (int)(M.chunk_col[c + 1] - col0));
-        __syncthreads();
-        if (panel < M.npanels) panel_segment<MODE>(M, panel * M.nchunks + c, tab, acc, nullptr);
-    }
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    const double sc[4] = {0.0, 0.0, 0.0, 0.0};
+    panel_chunks<MODE>(M, rb, wv, M.group_chunk[g], M.group_chunk[g + 1], P.x, lds, s, sc);
     if (panel >= M.npanels) return;
-    for (int i = lane; i < M.prow; i += WAVE) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = 64 * q + lane;
         const int64_t row = panel * M.prow + i;
-        if (row < P.m) P.rpart[g * P.m + row] = acc[i];
+        if (i < M.prow && row < P.m) P.rpart[g * P.m + row] = s[q];
     }
 }
 
@@ -180,42 +174,39 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
     const int wv = threadIdx.x / WAVE, lane = lane_id();
     const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
     const int64_t i0 = panel * M.prow;
-    double *tab = lds;
-    double *acc = lds + BSLS_PANEL_CHUNK + wv * PANEL_ACC;
-    for (int i = lane; i < PANEL_ACC; i += WAVE) acc[i] = 0.0;
-    int32_t j[4];
-    double gpj[4], zcj[4], zpj[4];
+    const bool live = panel < M.npanels;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    double sc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (MODE == 2 && live) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int pos = lane + 64 * q;
-        const int64_t i = i0 + pos;
-        j[q] = (panel < M.npanels && pos < M.prow && i < P.n) ? P.xz[i] : -1;
-        gpj[q] = zcj[q] = zpj[q] = 0.0;
-        if (ITER && j[q] >= 0) {
-            gpj[q] = gp[j[q]];
-            zcj[q] = zc[j[q]];
-            zpj[q] = zp[j[q]];
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i = i0 + 64 * q + lane;        // halo row included
+            if (64 * q + lane <= M.prow && i < P.n) sc[q] = P.colv[i];
         }
     }
-    const double *rs = (MODE == 2) ? P.colv + i0 : nullptr;
-    for (int64_t c = 0; c < M.nchunks; ++c) {
-        const int64_t col0 = M.chunk_col[c];
-        __syncthreads();
-        panel_stage(tab, P.r + col0, (int)(M.chunk_col[c + 1] - col0));
-        __syncthreads();
-        if (panel < M.npanels) panel_segment<MODE>(M, panel * M.nchunks + c, tab, acc, rs);
+    panel_chunks<MODE>(M, blockIdx.x, wv, 0, M.nchunks, P.r, lds, s, sc);
+    // w_{i+1}: the next lane, or lane 0 of the next slice (the halo row is
+    // row prow of the panel)
+    double nx[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double dn = __shfl_down(s[q], 1, WAVE);
+        const double wrap = (q < 3) ? __shfl(s[q < 3 ? q + 1 : q], 0, WAVE) : 0.0;
+        nx[q] = (lane < 63) ? dn : wrap;
     }
-    __syncthreads();   // tab becomes the reduction scratch below
+    __syncthreads();   // the chunk table becomes the reduction scratch below
     double sums[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        if (j[q] >= 0) {
-            const int pos = lane + 64 * q;
-            const double g = acc[pos] - acc[pos + 1];
-            gout[j[q]] = g;
+        const int pos = 64 * q + lane;
+        const int64_t i = i0 + pos;
+        const int32_t j = (live && pos < M.prow && i < P.n) ? P.xz[i] : -1;
+        if (j >= 0) {
+            const double g = s[q] - nx[q];
+            gout[j] = g;
             if (ITER) {
-                const double dg = g - gpj[q];
-                const double dz = zcj[q] - zpj[q];
+                const double dg = g - gp[j];
+                const double dz = zc[j] - zp[j];
                 sums[0] += dg;
                 sums[1] += dz * dg;
                 sums[2] += dg * dg;
@@ -224,9 +215,9 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
         }
     }
     if (!ITER) return;
-    block_sum<4>(sums, tab);
+    block_sum<4>(sums, lds);
     double tot[4];
-    if (last_block_sum<4>(sums, part, ticket, tot, tab) && threadIdx.x == 0) {
+    if (last_block_sum<4>(sums, part, ticket, tot, lds) && threadIdx.x == 0) {
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
@@ -341,14 +332,14 @@ __global__ __launch_bounds__(256) void bb_z2x(bsls_bb_problem P, const double *_
     x_put(P, xo, 0.0 - prev);
 }
 
-// 155 KB of dynamic LDS (one chunk + the 16 waves' row sums): opt in once per
-// kernel instance.
+// Up to ~160 KB of dynamic LDS (panel_lds_bytes): opt in once per kernel instance.
+constexpr int PANEL_LDS_MAX = 163840 - 512;
 template <typename K>
 static void allow_lds(K kernel) {
     static bool done = false;
     if (!done) {
         (void)hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)PANEL_LDS);
+                                  PANEL_LDS_MAX);
         done = true;
     }
 }
@@ -358,7 +349,7 @@ static void launch_k1_mode(const bsls_bb_problem &P, int64_t iter, const BBWork 
                            hipStream_t st) {
     const int64_t rbs = (P.A.npanels + PANEL_WAVES - 1) / PANEL_WAVES;
     allow_lds(bb_k1a<MODE, ITER>);
-    bb_k1a<MODE, ITER><<<(int)(P.A.ngroups * rbs), 1024, PANEL_LDS, st>>>(P);
+    bb_k1a<MODE, ITER><<<(int)(P.A.ngroups * rbs), 1024, panel_lds_bytes(P.A), st>>>(P);
     bb_k1b<ADD, REDUCE, ITER><<<grid_for(P.m, 256), 256, 0, st>>>(P, iter, w.p1, w.tk1);
 }
 
@@ -372,7 +363,7 @@ template <int MODE, bool ITER>
 static void launch_k2_mode(const bsls_bb_problem &P, const double *zc, const double *zp,
                            const double *gp, double *gout, const BBWork &w, hipStream_t st) {
     allow_lds(bb_k2<MODE, ITER>);
-    bb_k2<MODE, ITER><<<grid_for(P.AT.npanels, PANEL_WAVES), 1024, PANEL_LDS, st>>>(
+    bb_k2<MODE, ITER><<<grid_for(P.AT.npanels, PANEL_WAVES), 1024, panel_lds_bytes(P.AT), st>>>(
         P, zc, zp, gp, gout, w.p2, w.tk2);
 }
 
@@ -391,11 +382,13 @@ static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, 
 static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t halo,
                       bool need_val) {
     if (M.rows != rows || M.cols != cols || M.halo != halo) return false;
-    if (M.prow < 1 || M.prow + halo > PANEL_ACC || M.npanels != (rows + M.prow - 1) / M.prow)
+    if (M.prow < 1 || M.prow + halo > 256 || M.npanels != (rows + M.prow - 1) / M.prow)
         return false;
     if (M.nchunks < 1 || M.ngroups < 1 || M.ngroups > M.nchunks) return false;
-    if (!M.chunk_col || !M.group_chunk || !M.ent_off || !M.perm_off || !M.dl_off || !M.dlen ||
-        !M.perm || !M.ent)
+    if (M.tab_cap < 64 || M.tab_cap > BSLS_PANEL_CHUNK || panel_lds_bytes(M) > (size_t)PANEL_LDS_MAX)
+        return false;
+    if (!M.chunk_col || !M.group_chunk || !M.ent_off || !M.cnt_off || !M.seg_info || !M.cnt ||
+        !M.ent)
         return false;
     return need_val ? M.val != nullptr : true;
 }

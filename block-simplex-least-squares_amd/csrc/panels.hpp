@@ -1,141 +1,210 @@
-// panels.hpp -- the fused SpMVs' matrix format: LDS-chunked jagged diagonals.
+// panels.hpp -- the fused SpMVs' matrix format: LDS-chunked row panels.
 //
 // Why: a random 8-B gather served by L2 costs a TA/L2 request per lane
 // (~0.24 T gathers/s chip-wide measured, tools/ubench_gather.hip), the same
 // gather from LDS ~1.3 T/s.  So the gathered vector is staged, one column
-// chunk (<= BSLS_PANEL_CHUNK doubles, ~120 KB) at a time, into the LDS of the
-// workgroup, and the matrix is stored so every chunk's entries of a wave's
-// rows can be walked without padding:
-//   panel   = prow consecutive rows (+1 halo row for K2), one wave;
-//   segment = (panel, chunk): the panel's rows having entries in the chunk,
-//             sorted by that count (descending; perm[] = row in panel per
-//             position), then "diagonal" d = the d-th entry of each of those
-//             rows, at positions 0 .. dlen[d]-1 (a prefix, since sorted);
+// chunk (<= tab_cap doubles, ~158 KB) at a time, into the LDS of the
+// workgroup, and the matrix is cut to match (include/bsls_hip.h, struct
+// bsls_panels):
+//   panel   = prow consecutive rows (+1 halo row for K2), one wave; row r in
+//             lane r % 64 of slice r / 64, its running sum in a register of
+//             that lane for the whole launch;
+//   segment = (panel, chunk): per live slice, the 64 rows' entry counts in
+//             the chunk and their entries, row after row in column order;
 //   entry   = uint16 column offset inside the chunk (+ f64 value unless the
 //             matrix is a scaled incidence, where the column's scale is applied
 //             outside: K1 gathers colv*x, K2 multiplies by colv of its row).
-// A lane owns positions lane + 64q (q < 4); its row's running sum lives in LDS
-// across chunks, so every row is summed in CSR order, entry after entry,
-// exactly like SciPy's csr_matvec (bit-identical when one workgroup sees all
-// chunks, as K2 does).
+// Lane l walks diagonal k of slice q (its row's k-th entry in the chunk) if
+// k < cnt: one compare; the entry sits at slice_base + rowstart + k (rowstart
+// and cnt from the stored running counts by one DPP shift), so the loads of a
+// segment use one address register per slice and immediate offsets.  Every row is summed in CSR order, entry after entry, exactly like
+// SciPy's csr_matvec (bit-identical when one workgroup sees all chunks, as K2
+// does).  Measured before this layout (jagged diagonals sorted per chunk,
+// sums in LDS): VALU-bound, ~1 VALU wave-instruction per entry; here ~4 per
+// diagonal of 64 rows.
+//
+// Latency: the 16 waves move in lockstep between the per-chunk barriers, and
+// a chunk's entries depend on its running counts (their addresses).  Counts
+// are loaded two chunks ahead, entries one chunk ahead, so both round trips
+// hide behind a whole walk + barrier + LDS-DMA (measured with
+// tools/panel_ubench.py: loads issued just before the next barrier left
+// 32 of 45 us exposed).
 #pragma once
 #include "bsls_common.hpp"
 
 namespace bsls {
 
-constexpr int PANEL_WAVES = 16;                 // panels per workgroup (1024 threads)
-constexpr int PANEL_ACC = 256;                  // LDS row sums per wave (prow + halo <= 256)
-constexpr size_t PANEL_LDS = (size_t)BSLS_PANEL_CHUNK * 8 + (size_t)PANEL_WAVES * PANEL_ACC * 8;
+constexpr int PANEL_WAVES = BSLS_PANEL_WAVES;   // panels per workgroup (1024 threads)
 
 __device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
-// Stage src[0, w) into tab (w <= BSLS_PANEL_CHUNK); src 16-B aligned (chunk
-// starts are even columns).  LDS-DMA (global_load_lds_dwordx4): wave-instruction
-// k of wave v moves the 1-KB piece p = 16 k + v straight into LDS, no VGPRs.
-// The caller brackets it with barriers (__syncthreads drains the DMA).
-__device__ __forceinline__ void panel_stage(double *tab, const double *__restrict__ src, int w) {
-    const int lane = lane_id(), wv = threadIdx.x / WAVE;
-    const int w2 = w >> 1;                       // 16-B units
-    const int npieces = (w2 + 63) >> 6;
-    for (int p = wv; p < npieces; p += PANEL_WAVES) {
-        const int i = p * 64 + lane;
-        if (i < w2)
-            __builtin_amdgcn_global_load_lds((const void *)(src + 2 * (int64_t)i),
-                                             (__attribute__((address_space(3))) void *)(tab + p * 128),
+// Dynamic LDS of a panel kernel: the chunk table (tab_cap doubles; K2 reuses
+// it as reduction scratch, hence >= 64).
+__host__ __device__ inline size_t panel_lds_bytes(const bsls_panels &M) {
+    return (size_t)M.tab_cap * 8;
+}
+
+// LDS-DMA (global_load_lds_dwordx4) of n16 16-byte units from src to LDS dst:
+// wave-instruction k of wave v moves the 1-KB piece p = nwaves k + v, no VGPRs.
+// Completion: the next __syncthreads (it drains vmcnt).
+__device__ __forceinline__ void lds_dma(void *dst, const void *src, int64_t n16) {
+    const int lane = lane_id(), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    const int64_t npieces = (n16 + 63) >> 6;
+    const char *s = (const char *)src;
+    char *d = (char *)dst;
+    for (int64_t p = wv; p < npieces; p += nw) {
+        const int64_t i = p * 64 + lane;
+        if (i < n16)
+            __builtin_amdgcn_global_load_lds((const void *)(s + 16 * i),
+                                             (__attribute__((address_space(3))) void *)(d + 1024 * p),
                                              16, 0, 0);
     }
+}
+
+// Stage src[0, w) into tab (w <= tab_cap); src 16-B aligned (chunk starts are
+// even columns).
+__device__ __forceinline__ void panel_stage(double *tab, const double *__restrict__ src, int w) {
+    lds_dma(tab, src, w >> 1);
     if ((w & 1) && threadIdx.x == 0) tab[w - 1] = src[w - 1];
 }
 
-// One segment by one wave.  acc: the wave's row sums (LDS); tab: the staged
-// chunk; rowscale: colv of the panel's row 0 (MODE 2 only).
-// MODE 0: s += tab[c]                (K1, scaled incidence: tab = colv * x)
-// MODE 1: s += val[e] * tab[c]       (general matrix)
-// MODE 2: s += rowscale[row] * tab[c] (K2, scaled incidence)
-// Diagonals go in blocks of DB: the entry loads of all DB diagonals and 4
-// position slices are issued before the first gather (one memory round trip
-// per block; a segment rarely has more than DB diagonals).  Diagonal lengths
-// never increase, so whole (slice, diagonal) pairs drop out uniformly.
+// lane l - 1's value (0 in lane 0): DPP wave_shr:1
+__device__ __forceinline__ int wave_shr1(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false);
+}
+
+// A segment's first round trip: slice depths D_q (uniform) and each lane's
+// running count per live slice (inclusive prefix over the slice's rows).
+struct SegHead {
+    int D[4];
+    int incl[4];
+    int64_t e0;
+
+    __device__ __forceinline__ void load(const bsls_panels &M, int64_t seg, bool live) {
+        const int lane = lane_id();
+        const int64_t info = live ? M.seg_info[seg] : 0;
+        int64_t co = live ? M.cnt_off[seg] : 0;
+        e0 = live ? M.ent_off[seg] : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            D[q] = (int)((info >> (16 * q)) & 0xFFFF);
+            incl[q] = 0;
+            if (D[q] > 0) {
+                incl[q] = (int)M.cnt[co + lane];
+                co += 64;
+            }
+        }
+    }
+};
+
+// A segment's entries (second round trip) and the walk.
 template <int MODE>
-__device__ __forceinline__ void panel_segment(const bsls_panels &M, int64_t seg,
-                                              const double *tab, double *acc,
-                                              const double *__restrict__ rowscale) {
-    const int64_t d0 = M.dl_off[seg], d1 = M.dl_off[seg + 1];
-    if (d0 == d1) return;
-    constexpr int DB = (MODE == 1) ? 4 : 8;
-    const int lane = lane_id();
-    // wave-uniform bases + 32-bit lane offsets (saddr + voffset addressing)
-    const int64_t e0 = M.ent_off[seg];
-    const uint16_t *__restrict__ ent = M.ent + e0;
-    const double *__restrict__ val = M.val + e0;
-    const int64_t pb = M.perm_off[seg];
-    uint32_t e = 0;
-    const int n0 = (int)M.dlen[d0];
-    int row[4];
-    double s[4], sc[4];
+struct SegBody {
+    static constexpr int DBK = (MODE == 1) ? 2 : 8;   // diagonals held per slice
+    int D[4];            // uniform
+    int cnt[4];          // this lane's row count per slice
+    uint32_t base[4];    // this lane's first entry per slice (relative to e0)
+    int64_t e0;
+    uint32_t c2[4][DBK / 2];   // column offsets of diagonals 2j, 2j+1 (low, high half)
+    double v[4][DBK];    // values (MODE 1)
+
+    __device__ __forceinline__ void load(const bsls_panels &M, const SegHead &h) {
+        const uint16_t *ent = M.ent + h.e0;
+        const double *val = M.val + h.e0;
+        e0 = h.e0;
+        uint32_t e = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int pos = lane + 64 * q;
-        row[q] = (pos < n0) ? (int)M.perm[pb + pos] : 0;
-    }
+        for (int q = 0; q < 4; ++q) {
+            D[q] = h.D[q];
+            cnt[q] = 0;
+            base[q] = 0;
+            if (D[q] > 0) {
+                // stored: running total of even-padded run lengths | (own count odd)
+                const int inc = h.incl[q] & ~1;
+                const int ex = wave_shr1(h.incl[q]) & ~1;
+                cnt[q] = inc - ex - (h.incl[q] & 1);
+                base[q] = e + (uint32_t)ex;
+                e += (uint32_t)(readlane_i(h.incl[q], 63) & ~1);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int pos = lane + 64 * q;
-        s[q] = (pos < n0) ? acc[row[q]] : 0.0;
-        sc[q] = (MODE == 2 && pos < n0) ? rowscale[row[q]] : 0.0;
-    }
-    for (int64_t dg = d0; dg < d1; dg += 64) {
-        const int nd = (int)((d1 - dg) < 64 ? (d1 - dg) : 64);
-        const int len = (lane < nd) ? (int)M.dlen[dg + lane] : 0;
-        int incl = len;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o, WAVE);
-            if (lane >= o) incl += t;
-        }
-        const int excl = incl - len;
-        for (int d = 0; d < nd; d += DB) {
-            int ln[DB];
-            uint32_t eo[DB];
-#pragma unroll
-            for (int k = 0; k < DB; ++k) {
-                ln[k] = (d + k < nd) ? readlane_i(len, d + k) : 0;
-                eo[k] = e + (uint32_t)((d + k < nd) ? readlane_i(excl, d + k) : 0);
-            }
-            int c[4][DB];
-            double v[4][DB];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int pos = lane + 64 * q;
-#pragma unroll
-                for (int k = 0; k < DB; ++k) {
-                    c[q][k] = 0;
-                    v[q][k] = 0.0;
-                    if (64 * q < ln[k] && pos < ln[k]) {
-                        c[q][k] = ent[eo[k] + (uint32_t)pos];
-                        if (MODE == 1) v[q][k] = val[eo[k] + (uint32_t)pos];
-                    }
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int pos = lane + 64 * q;
-#pragma unroll
-                for (int k = 0; k < DB; ++k) {
-                    if (64 * q < ln[k] && pos < ln[k]) {
-                        const double a = tab[c[q][k]];
-                        if (MODE == 0) s[q] += a;
-                        else if (MODE == 1) s[q] += v[q][k] * a;
-                        else s[q] += sc[q] * a;
+                for (int j = 0; j < DBK / 2; ++j) {
+                    // a row's run is even-padded: two entries per aligned 32-bit load;
+                    // lanes past their row's end read the next row's: harmless
+                    if (2 * j < D[q]) {
+                        c2[q][j] = *reinterpret_cast<const uint32_t *>(
+                            reinterpret_cast<const char *>(ent) + (base[q] + 2 * j) * 2u);
+                        if (MODE == 1) {
+                            v[q][2 * j] = val[base[q] + 2 * j];
+                            v[q][2 * j + 1] = val[base[q] + 2 * j + 1];
+                        }
                     }
                 }
             }
         }
-        e += (uint32_t)readlane_i(incl, 63);
     }
+
+    // MODE 0: s += tab[c]; 1: s += val * tab[c]; 2: s += sc * tab[c]
+    __device__ __forceinline__ void walk(const bsls_panels &M, const double *tab, double (&s)[4],
+                                         const double (&sc)[4]) const {
+        const uint16_t *ent = M.ent + e0;
+        const double *val = M.val + e0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        if (lane + 64 * q < n0) acc[row[q]] = s[q];
+        for (int q = 0; q < 4; ++q) {
+            if (D[q] == 0) continue;
+#pragma unroll
+            for (int k = 0; k < DBK; ++k) {
+                if (k < D[q] && k < cnt[q]) {
+                    const uint32_t w = c2[q][k >> 1];
+                    const double a = tab[(k & 1) ? (w >> 16) : (w & 0xFFFFu)];
+                    if (MODE == 0) s[q] += a;
+                    else if (MODE == 1) s[q] += v[q][k] * a;
+                    else s[q] += sc[q] * a;
+                }
+            }
+            for (int k = DBK; k < D[q]; ++k) {      // long rows: loads on demand
+                if (k < cnt[q]) {
+                    const double a = tab[ent[base[q] + k]];
+                    if (MODE == 0) s[q] += a;
+                    else if (MODE == 1) s[q] += val[base[q] + k] * a;
+                    else s[q] += sc[q] * a;
+                }
+            }
+        }
+    }
+};
+
+// The chunk loop shared by K1a and K2: chunks [c0, c1) of panel 16 rb + wv,
+// each staged from src (column chunk_col[c] at src[chunk_col[c]]) into tab,
+// then walked by this wave into s[q] (row 64 q + lane).  Every wave of the
+// workgroup calls it (barriers).  Pipeline: during the step of chunk c the
+// wave holds chunk c's entries (walked now), loads chunk c+1's entries and
+// chunk c+2's running counts; the loop is unrolled twice so the two register
+// sets swap roles without copies.
+template <int MODE>
+__device__ __forceinline__ void panel_chunks(const bsls_panels &M, int64_t rb, int wv, int64_t c0,
+                                             int64_t c1, const double *src, double *tab,
+                                             double (&s)[4], const double (&sc)[4]) {
+    const bool live = rb * PANEL_WAVES + wv < M.npanels;
+    const int64_t seg0 = (rb * M.nchunks) * PANEL_WAVES + wv;
+    auto seg = [&](int64_t c) { return seg0 + c * PANEL_WAVES; };
+    SegHead ha, hb;
+    SegBody<MODE> ba, bb;
+    ha.load(M, seg(c0), live);
+    ba.load(M, ha);
+    if (c0 + 1 < c1) hb.load(M, seg(c0 + 1), live);
+    auto step = [&](int64_t c, const SegBody<MODE> &cur, SegHead &hn, SegBody<MODE> &bn,
+                    SegHead &hn2) {
+        const int64_t col0 = M.chunk_col[c];
+        __syncthreads();
+        panel_stage(tab, src + col0, (int)(M.chunk_col[c + 1] - col0));
+        __syncthreads();
+        if (c + 1 < c1) bn.load(M, hn);
+        if (c + 2 < c1) hn2.load(M, seg(c + 2), live);
+        if (live) cur.walk(M, tab, s, sc);
+    };
+    for (int64_t c = c0; c < c1; c += 2) {
+        step(c, ba, hb, bb, ha);
+        if (c + 1 < c1) step(c + 1, bb, ha, ba, hb);
+    }
 }
 
 }  // namespace bsls

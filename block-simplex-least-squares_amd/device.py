@@ -103,6 +103,7 @@ def build_panels(M, prow, halo=False, chunk_col=None, group_chunk=None, values=T
     M = sps.csr_matrix(M)
     M.sort_indices()
     R, C = M.shape
+    PW = _native.PANEL_WAVES
     prow = int(prow)
     if not 1 <= prow <= _native.PANEL_ROWS or prow + int(halo) > 256:
         raise ValueError('prow out of range')
@@ -110,10 +111,13 @@ def build_panels(M, prow, halo=False, chunk_col=None, group_chunk=None, values=T
         chunk_col, group_chunk = chunk_plan(C, 1)
     chunk_col = np.asarray(chunk_col, dtype=np.int64)
     group_chunk = np.asarray(group_chunk, dtype=np.int64)
-    if np.any(np.diff(chunk_col) > _native.PANEL_CHUNK) or np.any(chunk_col[:-1] % 2):
+    widths = np.diff(chunk_col)
+    if np.any(widths > _native.PANEL_CHUNK) or np.any(chunk_col[:-1] % 2):
         raise ValueError('bad chunk plan')
     nch = chunk_col.size - 1
     npan = max(1, -(-R // prow))
+    nrb = -(-npan // PW)
+    nsegs = nrb * nch * PW
     ip = M.indptr.astype(np.int64)
     rows = np.repeat(np.arange(R, dtype=np.int64), np.diff(ip))
     cols = M.indices.astype(np.int64)
@@ -128,62 +132,46 @@ def build_panels(M, prow, halo=False, chunk_col=None, group_chunk=None, values=T
         cols = np.concatenate([cols, cols[h]])
         vals = np.concatenate([vals, vals[h]])
     ch = np.searchsorted(chunk_col, cols, side='right') - 1
-    seg = pn * nch + ch
-    W = prow + 1
-    key = seg * W + lr
-    order = np.argsort(key, kind='stable')      # keeps column order inside a row
-    key = key[order]
-    cols = cols[order]
-    ch = ch[order]
-    vals = vals[order]
+    seg = ((pn // PW) * nch + ch) * PW + pn % PW
+    # storage order: segment, row (slice-major), then the row's entries by
+    # column, each row's run padded to an even length (aligned pair loads)
+    key = seg * 256 + lr
+    order = np.argsort(key, kind='stable')
+    key, cols, ch, vals = key[order], cols[order], ch[order], vals[order]
     E = key.size
-    nsegs = npan * nch
+    cnt_all = np.bincount(key, minlength=nsegs * 256).reshape(nsegs, 4, 64)
+    D = cnt_all.max(axis=2)                       # nsegs x 4 (<= chunk width < 2^16)
+    live = D > 0
+    padc = cnt_all + (cnt_all & 1)
+    incl = np.cumsum(padc, axis=2)                # per slice, inclusive over lanes
+    if incl[:, :, 63].max(initial=0) > 0xFFFE:
+        raise ValueError('a 64-row slice has more than 65534 entries in one chunk')
+    cnt = (incl | (cnt_all & 1))[live].astype(np.uint16).reshape(-1)
+    cnt_off = np.concatenate(([0], np.cumsum(64 * live.sum(axis=1)))).astype(np.int64)
+    ne = padc.sum(axis=(1, 2))
+    ent_off = np.concatenate(([0], np.cumsum(ne))).astype(np.int64)
+    seg_info = (D[:, 0] | (D[:, 1] << 16) | (D[:, 2] << 32) | (D[:, 3] << 48)).astype(np.int64)
+    Ep = int(ent_off[-1])
+    slack = 64
+    ent = np.zeros(Ep + slack, dtype=np.uint16)
+    val = np.zeros(Ep + slack, dtype=np.float64) if values else None
     if E:
+        flat = padc.reshape(nsegs, 256)
+        excl = (np.cumsum(flat, axis=1) - flat).reshape(-1)       # per (seg, row)
         newp = np.empty(E, dtype=bool)
         newp[0] = True
         np.not_equal(key[1:], key[:-1], out=newp[1:])
         pstart = np.nonzero(newp)[0]
-        pid = np.cumsum(newp) - 1
-        k = np.arange(E, dtype=np.int64) - pstart[pid]
-        cnt = np.diff(np.append(pstart, E))
-        pkey = key[pstart]
-        pseg = pkey // W
-        plr = pkey - pseg * W
-        porder = np.lexsort((plr, -cnt, pseg))
-        pseg_s = pseg[porder]
-        seg_first = np.searchsorted(pseg_s, np.arange(nsegs + 1))
-        pos = np.empty(pstart.size, dtype=np.int64)
-        pos[porder] = np.arange(pstart.size) - seg_first[pseg_s]
-        D = np.zeros(nsegs, dtype=np.int64)
-        nonempty = seg_first[1:] > seg_first[:-1]
-        D[nonempty] = cnt[porder[seg_first[:-1][nonempty]]]
-        dl_off = np.concatenate(([0], np.cumsum(D)))
-        seg_e = pseg[pid]
-        di = dl_off[seg_e] + k
-        dlen = np.bincount(di, minlength=int(dl_off[-1]))
-        G = np.concatenate(([0], np.cumsum(dlen)))
-        dest = G[di] + pos[pid]
-        ent = np.empty(E, dtype=np.uint16)
+        k = np.arange(E, dtype=np.int64) - np.repeat(pstart, np.diff(np.append(pstart, E)))
+        dest = ent_off[key >> 8] + excl[key] + k
         ent[dest] = (cols - chunk_col[ch]).astype(np.uint16)
-        val = None
         if values:
-            val = np.empty(E, dtype=np.float64)
             val[dest] = vals
-        perm = plr[porder].astype(np.uint8)
-        ent_off = G[dl_off]
-        perm_off = seg_first.astype(np.int64)
-    else:
-        dl_off = np.zeros(nsegs + 1, dtype=np.int64)
-        dlen = np.zeros(1, dtype=np.int64)
-        ent = np.zeros(1, dtype=np.uint16)
-        val = np.zeros(1) if values else None
-        perm = np.zeros(1, dtype=np.uint8)
-        ent_off = np.zeros(nsegs + 1, dtype=np.int64)
-        perm_off = np.zeros(nsegs + 1, dtype=np.int64)
     return dict(rows=R, cols=C, prow=prow, halo=int(bool(halo)), npanels=npan, nchunks=nch,
-                ngroups=group_chunk.size - 1, chunk_col=chunk_col, group_chunk=group_chunk,
-                ent_off=ent_off, perm_off=perm_off, dl_off=dl_off,
-                dlen=dlen.astype(np.uint16), perm=perm, ent=ent, val=val, nnz=E)
+                ngroups=group_chunk.size - 1, tab_cap=max(64, int(widths.max(initial=2))),
+                chunk_col=chunk_col, group_chunk=group_chunk, ent_off=ent_off, cnt_off=cnt_off,
+                seg_info=seg_info, cnt=np.concatenate([cnt, np.zeros(64, np.uint16)]),
+                ent=ent, val=val, nnz=E, stored=Ep)
 
 
 def panels_matvec(img, x, colv=None):
@@ -194,38 +182,44 @@ def panels_matvec(img, x, colv=None):
     halo rows.  Test helper (numpy, vectorised per diagonal)."""
     R, prow, halo = img['rows'], img['prow'], img['halo']
     nch = img['nchunks']
+    PW = _native.PANEL_WAVES
     x = np.asarray(x, dtype=np.float64)
     parts = []
     for g in range(img['ngroups']):
-        acc = np.zeros((img['npanels'], prow + halo))
+        acc = np.zeros((img['npanels'], 256))
         for c in range(img['group_chunk'][g], img['group_chunk'][g + 1]):
             c0 = img['chunk_col'][c]
             for p in range(img['npanels']):
-                sgi = p * nch + c
-                d0, d1 = img['dl_off'][sgi], img['dl_off'][sgi + 1]
-                if d0 == d1:
-                    continue
-                e = img['ent_off'][sgi]
-                n0 = int(img['dlen'][d0])
-                po = img['perm_off'][sgi]
-                rr = img['perm'][po:po + n0].astype(np.int64)
-                s = acc[p, rr].copy()
-                for d in range(d0, d1):
-                    ln = int(img['dlen'][d])
-                    t = x[c0 + img['ent'][e:e + ln].astype(np.int64)]
-                    if img['val'] is not None:
-                        s[:ln] = s[:ln] + img['val'][e:e + ln] * t
-                    elif colv is not None:
-                        s[:ln] = s[:ln] + colv[p * prow + rr[:ln]] * t
-                    else:
-                        s[:ln] = s[:ln] + t
-                    e += ln
-                acc[p, rr] = s
+                sgi = ((p // PW) * nch + c) * PW + p % PW
+                info = int(img['seg_info'][sgi])
+                e = int(img['ent_off'][sgi])
+                co = int(img['cnt_off'][sgi])
+                for q in range(4):
+                    Dq = (info >> (16 * q)) & 0xFFFF
+                    if Dq == 0:
+                        continue
+                    st = img['cnt'][co:co + 64].astype(np.int64)
+                    co += 64
+                    inc = st & ~1
+                    cnp = np.diff(np.concatenate(([0], inc)))          # padded counts
+                    start = e + inc - cnp
+                    cn = cnp - (st & 1)
+                    rr = 64 * q + np.arange(64)
+                    for k in range(Dq):
+                        a = cn > k
+                        t = x[c0 + img['ent'][start[a] + k].astype(np.int64)]
+                        if img['val'] is not None:
+                            acc[p, rr[a]] = acc[p, rr[a]] + img['val'][start[a] + k] * t
+                        elif colv is not None:
+                            acc[p, rr[a]] = acc[p, rr[a]] + colv[p * prow + rr[a]] * t
+                        else:
+                            acc[p, rr[a]] = acc[p, rr[a]] + t
+                    e += int(cnp.sum())
         parts.append(acc)
     out = parts[0][:, :prow].reshape(-1)[:R].copy()
     for acc in parts[1:]:
         out = out + acc[:, :prow].reshape(-1)[:R]
-    return out, parts[-1]
+    return out, parts[-1][:, :prow + halo]
 
 
 def scaled_incidence_scale(A):
@@ -246,22 +240,21 @@ def scaled_incidence_scale(A):
 class DevicePanels:
     """A panel image on the device + the ctypes struct pointing at it."""
 
-    def __init__(self, M, prow, halo=False, ngroups=1, values=True):
+    def __init__(self, M, prow, halo=False, ngroups=1, values=True, img=None, chunk=None):
         torch = _torch()
-        ccol, gch = chunk_plan(M.shape[1], ngroups)
-        img = build_panels(M, prow, halo, ccol, gch, values)
+        img = img or build_panels(M, prow, halo, *chunk_plan(M.shape[1], ngroups, chunk=chunk),
+                                  values=values)
         self.img = img
         self.nnz = img['nnz']
         self.t = {}
-        for k in ('chunk_col', 'group_chunk', 'ent_off', 'perm_off', 'dl_off'):
+        for k in ('chunk_col', 'group_chunk', 'ent_off', 'cnt_off', 'seg_info'):
             self.t[k] = torch.from_numpy(np.ascontiguousarray(img[k], dtype=np.int64)).cuda()
-        self.t['dlen'] = torch.from_numpy(img['dlen'].view(np.int16)).cuda()
-        self.t['perm'] = torch.from_numpy(img['perm']).cuda()
+        self.t['cnt'] = torch.from_numpy(img['cnt'].view(np.int16)).cuda()
         self.t['ent'] = torch.from_numpy(img['ent'].view(np.int16)).cuda()
         if img['val'] is not None:
             self.t['val'] = torch.from_numpy(img['val']).cuda()
         S = _native.Panels()
-        for k in ('rows', 'cols', 'prow', 'halo', 'npanels', 'nchunks', 'ngroups'):
+        for k in ('rows', 'cols', 'prow', 'halo', 'npanels', 'nchunks', 'ngroups', 'tab_cap'):
             setattr(S, k, int(img[k]))
         for k, v in self.t.items():
             setattr(S, k, v.data_ptr())

@@ -137,34 +137,41 @@ enum {
     BSLS_STOP_GRAD = 3,       /* solvers.py:51-54 */
     BSLS_STOP_DG = 4          /* solvers.py:59-62 */
 };
-/* Panel image of a sparse matrix M (rows x cols) for the fused SpMVs: the
- * LDS-chunked jagged-diagonal format of csrc/panels.hpp (built on the host by
- * device.build_panels).  Rows are cut into panels of `prow` rows (one wave
- * each; K2's panels also carry the next panel's first row, `halo` = 1),
- * columns into chunks that fit the LDS (chunk c = columns
- * [chunk_col[c], chunk_col[c+1]), at most BSLS_PANEL_CHUNK wide).  Segment
- * s = panel * nchunks + chunk lists the panel's entries in that chunk: the
- * rows present, sorted by their entry count (perm: row within the panel, per
- * position), then diagonal d = every present row's d-th entry in that chunk,
- * positions 0 .. dlen[d]-1.  An entry is its column offset in the chunk
- * (ent, uint16) and, unless the matrix is a scaled incidence, its value. */
-#define BSLS_PANEL_CHUNK 15360
+/* Panel image of a sparse matrix M (rows x cols) for the fused SpMVs (layout
+ * and rationale: csrc/panels.hpp; built on the host by device.build_panels).
+ * Rows are cut into panels of `prow` rows (one wave each; K2's panels also
+ * carry the next panel's first row, `halo` = 1), 16 panels to a workgroup
+ * (row block rb); row r of a panel sits in lane r % 64 of slice r / 64.
+ * Columns are cut into chunks that fit the LDS (chunk c = columns
+ * [chunk_col[c], chunk_col[c+1]), at most tab_cap wide).  Segment
+ * s = (rb * nchunks + c) * 16 + w holds panel 16 rb + w's entries in chunk c:
+ * for each slice q with D_q > 0 (D_q = the slice's largest row count in the
+ * chunk, bits 16q .. 16q+15 of seg_info[s]), the rows' entries, row after row
+ * in column order, each row's run padded to an even length (from ent_off[s],
+ * slice after slice), and per row the running total of the padded lengths
+ * (inclusive, even) with bit 0 set when the row's own count is odd (cnt,
+ * uint16, at cnt_off[s], one group of 64 per such slice; a slice holds
+ * < 65535 entries).  An entry is
+ * its column offset in the chunk (ent, uint16) and, unless the matrix is a
+ * scaled incidence, its value (val). */
+#define BSLS_PANEL_CHUNK 20224
 #define BSLS_PANEL_ROWS 255
+#define BSLS_PANEL_WAVES 16
 typedef struct bsls_panels {
     int64_t rows, cols;
     int64_t prow;                   /* rows per panel, 1 .. BSLS_PANEL_ROWS */
-    int64_t halo;                   /* 1: segment rows are prow + 1 (row prow = next panel's row 0) */
-    int64_t npanels, nchunks;
-    int64_t ngroups;                /* chunk groups: K1 runs one workgroup per (group, 16 panels) */
+    int64_t halo;                   /* 1: panels hold prow + 1 rows (row prow = next panel's row 0) */
+    int64_t npanels, nchunks;       /* npanels counts the panels holding rows */
+    int64_t ngroups;                /* chunk groups: K1 runs one workgroup per (group, row block) */
+    int64_t tab_cap;                /* widest chunk (doubles), 64 .. BSLS_PANEL_CHUNK */
     const int64_t *chunk_col;       /* nchunks + 1 */
     const int64_t *group_chunk;     /* ngroups + 1 */
-    const int64_t *ent_off;         /* npanels * nchunks + 1: first entry of each segment */
-    const int64_t *perm_off;        /* npanels * nchunks + 1: first perm byte of each segment */
-    const int64_t *dl_off;          /* npanels * nchunks + 1: first diagonal of each segment */
-    const uint16_t *dlen;           /* rows having a d-th entry, per diagonal */
-    const uint8_t *perm;
-    const uint16_t *ent;
-    const double *val;              /* per entry, or NULL when scaled (see colv) */
+    const int64_t *ent_off;         /* nsegs + 1: first entry of each segment */
+    const int64_t *cnt_off;         /* nsegs + 1: first running count of each segment */
+    const int64_t *seg_info;        /* nsegs: D_0 | D_1 << 16 | D_2 << 32 | D_3 << 48 */
+    const uint16_t *cnt;
+    const uint16_t *ent;            /* + 64 entries of slack at the end */
+    const double *val;              /* per entry (+ slack), or NULL when scaled (see colv) */
 } bsls_panels;
 
 typedef struct bsls_bb_problem {

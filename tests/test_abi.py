@@ -80,6 +80,7 @@ def test_panel_limits_match_header(native):
     hdr = open(os.path.join(ROOT, 'include', 'bsls_hip.h')).read()
     assert '#define BSLS_PANEL_CHUNK %d' % native.PANEL_CHUNK in hdr
     assert '#define BSLS_PANEL_ROWS %d' % native.PANEL_ROWS in hdr
+    assert '#define BSLS_PANEL_WAVES %d' % native.PANEL_WAVES in hdr
 
 
 def test_tile_planner(native):

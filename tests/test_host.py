@@ -173,10 +173,19 @@ def test_panel_image_walk_matches_scipy(R, C, dens, prow, halo, ngroups, chunk):
     A = _rand_csr(rs, R, C, dens)
     ccol, gch = device.chunk_plan(C, ngroups, chunk=chunk)
     assert ccol[0] == 0 and ccol[-1] == C and np.all(ccol[:-1] % 2 == 0)
-    assert np.all(np.diff(ccol) <= (chunk or 15360)) and gch[-1] == ccol.size - 1
+    assert np.all(np.diff(ccol) <= (chunk or 20224)) and gch[-1] == ccol.size - 1
     img = device.build_panels(A, prow, halo, ccol, gch)
     assert img['nnz'] == A.nnz + (halo and sum(A[p * prow].nnz for p in range(1, img['npanels'])))
-    assert img['dlen'].max() <= prow + halo
+    assert np.all(img['ent_off'] % 2 == 0)                # pair loads stay 4-B aligned
+    # D_q = the slice's largest row count; one 64-byte count group per live slice
+    info = img['seg_info']
+    D = np.stack([(info >> (16 * q)) & 0xFFFF for q in range(4)], axis=1)
+    assert img['cnt_off'][-1] == 64 * np.count_nonzero(D)
+    groups = img['cnt'][:img['cnt_off'][-1]].astype(np.int64).reshape(-1, 64)
+    padded = np.diff(np.concatenate([np.zeros((groups.shape[0], 1), np.int64), groups & ~1],
+                                    axis=1), axis=1)
+    assert np.all(padded >= 0) and np.all(padded % 2 == 0)
+    assert (padded - (groups & 1)).sum() == img['nnz'] and padded.sum() == img['stored']
     x = rs.randn(C)
     y, acc = device.panels_matvec(img, x)
     ref = A.dot(x)
