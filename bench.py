@@ -208,18 +208,26 @@ def main():
         kern = {}
         if world == 1 and args.profile_iters > 0:
             # per-kernel HIP-event timing on the stream the kernels run on
+            # the stages of profile_iters further iterations, events between
+            # the kernels; the stream is held by a spin kernel while the host
+            # enqueues, so the GPU runs them back to back (no host gaps inside
+            # an event interval -- comparable with rocprofv3's kernel times)
             names = [(3, 'K2_spmvT_Nt_dots'), (4, 'K3_pava_clip_z2x'), (7, 'K1_spmv_A')]
             acc = {nm: [] for _, nm in names}
             it0 = 1 + args.warmup + args.steps
+            torch.cuda._sleep(int(2e8))
+            evs = []
             for it in range(it0, it0 + args.profile_iters):
-                evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-                evs[0].record()
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                ev[0].record()
                 for k, (stg, _) in enumerate(names):
                     eng.stage(stg, it)
-                    evs[k + 1].record()
-                torch.cuda.synchronize()
+                    ev[k + 1].record()
+                evs.append(ev)
+            torch.cuda.synchronize()
+            for ev in evs:
                 for k, (_, nm) in enumerate(names):
-                    acc[nm].append(evs[k].elapsed_time(evs[k + 1]) * 1e3)
+                    acc[nm].append(ev[k].elapsed_time(ev[k + 1]) * 1e3)
             for nm, v in acc.items():
                 us = float(np.mean(v))
                 kern[nm] = {'avg_us': us, 'alg_bytes': kb[nm],

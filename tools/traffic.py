@@ -1,0 +1,62 @@
+#!/usr/bin/env python
+"""Per-launch HBM traffic of the fused BB kernels from rocprofv3 PMC passes
+(tools/gpu_round.sh step `pmc`: FETCH_SIZE and WRITE_SIZE in separate passes
+over tools/kprof.py).  MI355X_MICROARCH.md "HBM / rocprofv3": FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
+coalesced reads, so traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes).
+Usage: python tools/traffic.py gpurun_out/pmc1 gpurun_out/pmc2 > profiles/traffic_r01.json"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+# bench.py kernel names -> device kernels (demangled prefixes) in one launch of the stage
+KERNELS = {
+    'K2_spmvT_Nt_dots': ['bsls::bb_k2<2, true>'],
+    'K3_pava_clip_z2x': ['bsls::bb_k3('],
+    'K1_spmv_A': ['bsls::bb_k1a<0, true>', 'bsls::bb_k1b<true, true, true>'],
+    'proj_simplex_C2': ['bsls::proj_small_kernel<false>'],
+}
+
+
+def load(dirs):
+    vals = defaultdict(lambda: defaultdict(list))
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
+            per = defaultdict(float)
+            for r in csv.DictReader(open(f)):
+                per[(r['Dispatch_Id'], r['Kernel_Name'], r['Counter_Name'])] += float(r['Counter_Value'])
+            for (_, kn, cn), v in per.items():
+                vals[kn][cn].append(v)
+    return vals
+
+
+def main():
+    vals = load(sys.argv[1:])
+    out = {}
+    for name, parts in KERNELS.items():
+        fetch = write = 0.0
+        ok = True
+        for pfx in parts:
+            hits = [k for k in vals if pfx in k]
+            if not hits:
+                ok = False
+                break
+            k = hits[0]
+            f, w = vals[k].get('FETCH_SIZE', []), vals[k].get('WRITE_SIZE', [])
+            if not f or not w:
+                ok = False
+                break
+            fetch += sum(f) / len(f)
+            write += sum(w) / len(w)
+        if ok:
+            out[name] = {'fetch_kib': fetch, 'write_kib': write,
+                         'hbm_bytes_per_launch': (2 * fetch + write) * 1024,
+                         'formula': '(2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH correction'}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == '__main__':
+    main()
