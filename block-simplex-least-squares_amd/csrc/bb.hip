@@ -126,8 +126,16 @@ __global__ __launch_bounds__(256) void bb_k1b(bsls_bb_problem P, int64_t iter, d
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double sq[1] = {0.0};
     if (i < P.m) {
-        double o = P.rpart[i];
-        for (int64_t c = 1; c < P.A.ngroups; ++c) o += P.rpart[c * P.m + i];
+        // all group partials in flight at once, summed in group order
+        const int64_t G = P.A.ngroups;
+        double v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = (c < G) ? P.rpart[c * P.m + i] : 0.0;
+        double o = v[0];
+#pragma unroll
+        for (int c = 1; c < 8; ++c)
+            if (c < G) o += v[c];
+        for (int64_t c = 8; c < G; ++c) o += P.rpart[c * P.m + i];
         if (ADD) o += P.target[i];
         P.r[i] = o;
         sq[0] = o * o;

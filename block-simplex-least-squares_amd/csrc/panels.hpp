@@ -129,6 +129,7 @@ struct SegBody {
                 for (int j = 0; j < DBK / 2; ++j) {
                     // a row's run is even-padded: two entries per aligned 32-bit load;
                     // lanes past their row's end read the next row's: harmless
+                    c2[q][j] = 0u;
                     if (2 * j < D[q]) {
                         c2[q][j] = *reinterpret_cast<const uint32_t *>(
                             reinterpret_cast<const char *>(ent) + (base[q] + 2 * j) * 2u);
@@ -150,22 +151,46 @@ struct SegBody {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if (D[q] == 0) continue;
+            // all gathers of the slice first (every held offset is a valid
+            // column of the chunk, or 0), then the adds in order; a lane past
+            // its row's end adds 0.0, which leaves its sum bit-for-bit unchanged
+            // (a sum started at +0.0 is never -0.0)
+            double a[DBK];
 #pragma unroll
             for (int k = 0; k < DBK; ++k) {
-                if (k < D[q] && k < cnt[q]) {
-                    const uint32_t w = c2[q][k >> 1];
-                    const double a = tab[(k & 1) ? (w >> 16) : (w & 0xFFFFu)];
-                    if (MODE == 0) s[q] += a;
-                    else if (MODE == 1) s[q] += v[q][k] * a;
-                    else s[q] += sc[q] * a;
+                const uint32_t w = c2[q][k >> 1];
+                a[k] = tab[(k & 1) ? (w >> 16) : (w & 0xFFFFu)];
+            }
+#pragma unroll
+            for (int k = 0; k < DBK; ++k) {
+                if (k < D[q]) {
+                    double t;
+                    if (MODE == 0) t = a[k];
+                    else if (MODE == 1) t = v[q][k] * a[k];
+                    else t = sc[q] * a[k];
+                    if (k < cnt[q]) s[q] += t;
                 }
             }
-            for (int k = DBK; k < D[q]; ++k) {      // long rows: loads on demand
-                if (k < cnt[q]) {
-                    const double a = tab[ent[base[q] + k]];
-                    if (MODE == 0) s[q] += a;
-                    else if (MODE == 1) s[q] += val[base[q] + k] * a;
-                    else s[q] += sc[q] * a;
+            // long rows (a slice deeper than DBK): further diagonals DBK at a time,
+            // all loads of a batch in flight together
+            for (int k0 = DBK; k0 < D[q]; k0 += DBK) {
+                int cc[DBK];
+                double vv[DBK];
+#pragma unroll
+                for (int k = 0; k < DBK; ++k) {
+                    const uint32_t i = base[q] + (uint32_t)(k0 + k);
+                    const bool in = k0 + k < cnt[q];
+                    cc[k] = in ? (int)ent[i] : 0;
+                    if (MODE == 1) vv[k] = in ? val[i] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < DBK; ++k) {
+                    const double a2 = tab[cc[k]];
+                    double t;
+                    if (MODE == 0) t = a2;
+                    else if (MODE == 1) t = vv[k] * a2;
+                    else t = sc[q] * a2;
+                    if (k0 + k < cnt[q]) s[q] += t;
                 }
             }
         }
@@ -188,14 +213,18 @@ __device__ __forceinline__ void panel_chunks(const bsls_panels &M, int64_t rb, i
     auto seg = [&](int64_t c) { return seg0 + c * PANEL_WAVES; };
     SegHead ha, hb;
     SegBody<MODE> ba, bb;
+    // chunk c0's DMA goes first, so it overlaps the prologue's two round trips
+    panel_stage(tab, src + M.chunk_col[c0], (int)(M.chunk_col[c0 + 1] - M.chunk_col[c0]));
     ha.load(M, seg(c0), live);
     ba.load(M, ha);
     if (c0 + 1 < c1) hb.load(M, seg(c0 + 1), live);
     auto step = [&](int64_t c, const SegBody<MODE> &cur, SegHead &hn, SegBody<MODE> &bn,
                     SegHead &hn2) {
         const int64_t col0 = M.chunk_col[c];
-        __syncthreads();
-        panel_stage(tab, src + col0, (int)(M.chunk_col[c + 1] - col0));
+        if (c > c0) {
+            __syncthreads();
+            panel_stage(tab, src + col0, (int)(M.chunk_col[c + 1] - col0));
+        }
         __syncthreads();
         if (c + 1 < c1) bn.load(M, hn);
         if (c + 2 < c1) hn2.load(M, seg(c + 2), live);

@@ -180,6 +180,91 @@ __global__ __launch_bounds__(1024) void k2_var(bsls_panels M, const double *__re
     }
 }
 
+// Timeline of the product chunk loop (copy of panel_chunks<2> with s_memtime
+// stamps): per chunk step, for wave 0 of every workgroup: [0] before loads,
+// [1] after body/head issue, [2] after the walk, [3] after barrier A,
+// [4] after the DMA issue, [5] after barrier B.
+__global__ __launch_bounds__(1024) void k2_trace(bsls_panels M, const double *__restrict__ r,
+                                                 const double *__restrict__ colv,
+                                                 double *__restrict__ out, long long *T) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, sc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < 4; ++q) {
+        const int64_t i = panel * M.prow + 64 * q + lane;
+        if (panel < M.npanels && 64 * q + lane <= M.prow && i < M.rows) sc[q] = colv[i];
+    }
+    long long *t = T + (int64_t)blockIdx.x * 64;
+    const bool rec = (wv == 0 && lane == 0);
+    if (rec) t[0] = wall_clock64();
+    const bool live = panel < M.npanels;
+    const int64_t c0 = 0, c1 = M.nchunks;
+    const int64_t seg0 = ((int64_t)blockIdx.x * M.nchunks) * PANEL_WAVES + wv;
+    auto seg = [&](int64_t c) { return seg0 + c * PANEL_WAVES; };
+    SegHead ha, hb;
+    SegBody<2> ba, bb;
+    panel_stage(lds, r + M.chunk_col[c0], (int)(M.chunk_col[c0 + 1] - M.chunk_col[c0]));
+    ha.load(M, seg(c0), live);
+    ba.load(M, ha);
+    if (c0 + 1 < c1) hb.load(M, seg(c0 + 1), live);
+    if (rec) t[1] = wall_clock64();
+    int ti = 2;
+    auto step = [&](int64_t c, const SegBody<2> &cur, SegHead &hn, SegBody<2> &bn, SegHead &hn2) {
+        const int64_t col0 = M.chunk_col[c];
+        if (c > c0) {
+            __syncthreads();
+            if (rec) t[ti++] = wall_clock64();
+            panel_stage(lds, r + col0, (int)(M.chunk_col[c + 1] - col0));
+        } else if (rec) {
+            t[ti++] = wall_clock64();
+        }
+        __syncthreads();
+        if (rec) t[ti++] = wall_clock64();
+        if (c + 1 < c1) bn.load(M, hn);
+        if (c + 2 < c1) hn2.load(M, seg(c + 2), live);
+        const long long tw0 = wall_clock64();
+        if (live) cur.walk(M, lds, s, sc);
+        {
+            double z = s[0] + s[1] + s[2] + s[3];
+            const long long tw1 = wall_clock64() + (z == 12345.678 ? 1 : 0);
+            int deep = 0;
+            for (int q = 0; q < 4; ++q) deep |= (cur.D[q] > 8) << q;
+            if (lane == 0 && c < 5) {
+                long long *u = T + 4096 * 64 + ((int64_t)blockIdx.x * 16 + wv) * 16;
+                u[2 * c] = tw1 - tw0;
+                u[2 * c + 1] = deep;
+            }
+        }
+        if (rec) {
+            // the walk's adds are done when s is: force it
+            double z = s[0] + s[1] + s[2] + s[3];
+            t[ti++] = wall_clock64() + (z == 12345.678 ? 1 : 0);
+        }
+    };
+    for (int64_t c = c0; c < c1; c += 2) {
+        step(c, ba, hb, bb, ha);
+        if (c + 1 < c1) step(c + 1, bb, ha, ba, hb);
+    }
+    if (rec) t[63] = wall_clock64();
+    if (panel >= M.npanels) return;
+    for (int q = 0; q < 4; ++q) {
+        const int i = 64 * q + lane;
+        const int64_t row = panel * M.prow + i;
+        if (i < M.prow && row < M.rows) out[row] = s[q];
+    }
+}
+
+extern "C" int panel_trace(const bsls_panels *M, const double *r, const double *colv, double *out,
+                           long long *T) {
+    hipFuncSetAttribute((const void *)k2_trace, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 512);
+    const int grid = (int)((M->npanels + PANEL_WAVES - 1) / PANEL_WAVES);
+    const size_t lds = panel_lds_bytes(*M);
+    for (int i = 0; i < 3; ++i) k2_trace<<<grid, 1024, lds>>>(*M, r, colv, out, T);
+    hipDeviceSynchronize();
+    return grid;
+}
+
 template <int VAR>
 static float run(const bsls_panels *M, const double *r, const double *colv, double *out, int reps) {
     auto k = k2_var<VAR>;

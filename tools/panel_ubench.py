@@ -43,6 +43,32 @@ def main():
             print('  %-12s %8.1f us' % (nm, us))
             if v == 0:
                 print('     bit-exact vs SciPy:', np.array_equal(out.cpu().numpy(), want))
+        T = torch.zeros(4096 * 64 + 4096 * 16 * 16, dtype=torch.int64, device='cuda')
+        lib.panel_trace.restype = ctypes.c_int
+        lib.panel_trace.argtypes = [ctypes.POINTER(_native.Panels), ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        grid = lib.panel_trace(ctypes.byref(pan.struct), r.data_ptr(), cv.data_ptr(),
+                               out.data_ptr(), T.data_ptr())
+        TT = T.cpu().numpy()
+        t = TT[:4096 * 64].reshape(-1, 64)[:grid]
+        u = TT[4096 * 64:].reshape(4096, 16, 16)[:grid]
+        nch = img['nchunks']
+        base = t[:, 0].min()
+        us = lambda v: (v - base) / 100.0          # wall_clock64: 100 MHz
+        print('  trace (us from first WG start; median over %d WGs):' % grid)
+        print('    start %.2f  prologue loads issued %.2f' % (np.median(us(t[:, 0])), np.median(us(t[:, 1]))))
+        for c in range(nch):
+            a, b_, w = t[:, 2 + 3 * c], t[:, 3 + 3 * c], t[:, 4 + 3 * c]
+            print('    chunk %d: barrierA %.2f  staged(barrierB) %.2f  walked %.2f   [stage %.2f walk %.2f]' % (
+                c, np.median(us(a)), np.median(us(b_)), np.median(us(w)),
+                np.median((b_ - a) / 100.0), np.median((w - b_) / 100.0)))
+        print('    end %.2f   (max end %.2f)' % (np.median(us(t[:, 63])), us(t[:, 63]).max()))
+        for c in range(min(nch, 5)):
+            wt = u[:, :, 2 * c] / 100.0
+            deep = u[:, :, 2 * c + 1] != 0
+            print('    chunk %d walk us per wave: median %.2f  p90 %.2f  max-per-WG median %.2f | deep waves %.0f%%: median %.2f, shallow median %.2f' % (
+                c, np.median(wt), np.percentile(wt, 90), np.median(wt.max(axis=1)), 100 * deep.mean(),
+                np.median(wt[deep]) if deep.any() else 0, np.median(wt[~deep])))
         lib.panel_ko.restype = ctypes.c_float
         lib.panel_ko.argtypes = lib.panel_ubench.argtypes
         names = {1: 'no gathers', 2: 'no entry loads', 4: 'no count loads', 8: 'no staging'}
