@@ -18,9 +18,10 @@
 //       A.dot(N.dot(z)) + target.  A in panel format with its column chunks
 //       split into 8 groups, group = blockIdx % 8 (one XCD: the group's slice
 //       of x stays in that XCD's L2 while its 32 workgroups stage it chunk by
-//       chunk into LDS); K1a writes one partial per (row, group); K1b sums the
-//       8 partials in group order, adds target, ||r||^2 (next gradient's
-//       residual AND f(z)) and runs the stopping test in the last workgroup.
+//       chunk into LDS) and publishes one partial per (row, group); the last
+//       of a row block's 8 workgroups sums them in group order, adds target,
+//       ||r||^2 (next gradient's residual AND f(z)); the last row block runs
+//       the stopping test.
 //   For a scaled incidence A (bsls_utils.py:494) the values are not stored:
 //   K3 writes colv * (N z) (the same products SciPy forms), K2 multiplies by
 //   the row's colv.
@@ -35,7 +36,7 @@ namespace bsls {
 
 
 struct BBWork {
-    unsigned *tk1, *tk2, *tkf;
+    unsigned *tk1, *tk2, *tkf, *tkrb;
     double *p1, *p2, *pf;
     int32_t *wsc;
     size_t bytes;
@@ -52,6 +53,8 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     w.tk2 = (unsigned *)(p + off + TICKET_BYTES);
     w.tkf = (unsigned *)(p + off + 2 * TICKET_BYTES);
     off += al16(3 * TICKET_BYTES);
+    w.tkrb = (unsigned *)(p + off);              // K1: one ticket per row block
+    off += al16((size_t)(m / 16 + 2) * 4);
     w.p1 = (double *)(p + off);
     off += al16((size_t)((m + 255) / 256 + 1) * 8);
     w.p2 = (double *)(p + off);
@@ -93,12 +96,17 @@ __device__ __forceinline__ void bb_record_f(const bsls_bb_problem &P, int64_t it
     }
 }
 
-// K1a: workgroup (group g = blockIdx % ngroups, panels 16 rb .. 16 rb + 15)
-// stages x chunk by chunk (the group's columns) and leaves, per row, the sum
-// over the group's columns in rpart[g][row].
-template <int MODE, bool ITER>
-__global__ __launch_bounds__(1024) void bb_k1a(bsls_bb_problem P) {
+// K1: workgroup (group g = blockIdx % ngroups, panels 16 rb .. 16 rb + 15)
+// stages x chunk by chunk (the group's columns) and publishes, per row, the
+// sum over the group's columns in rpart[g][row] (sc1: visible across XCDs).
+// The last of the row block's ngroups workgroups to arrive sums the partials
+// in group order (+ target), writes r, and (REDUCE) hands its share of
+// ||r||^2 to the last row block, which records f and runs the stopping test.
+template <int MODE, bool ITER, bool ADD, bool REDUCE>
+__global__ __launch_bounds__(1024) void bb_k1(bsls_bb_problem P, int64_t iter, unsigned *tkrb,
+                                              double *part, unsigned *ticket) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ int row_last;
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_panels &M = P.A;
     const int64_t G = M.ngroups;
@@ -108,42 +116,65 @@ __global__ __launch_bounds__(1024) void bb_k1a(bsls_bb_problem P) {
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     const double sc[4] = {0.0, 0.0, 0.0, 0.0};
     panel_chunks<MODE>(M, rb, wv, M.group_chunk[g], M.group_chunk[g + 1], P.x, lds, s, sc);
-    if (panel >= M.npanels) return;
+    if (panel < M.npanels) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int i = 64 * q + lane;
-        const int64_t row = panel * M.prow + i;
-        if (i < M.prow && row < P.m) P.rpart[g * P.m + row] = s[q];
+        for (int q = 0; q < 4; ++q) {
+            const int i = 64 * q + lane;
+            const int64_t row = panel * M.prow + i;
+            if (i < M.prow && row < P.m)
+                __hip_atomic_store(&P.rpart[g * P.m + row], s[q], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-}
-
-// K1b: r = sum_c rpart[c] (+ target); optional ||r||^2 and the stopping test.
-template <bool ADD, bool REDUCE, bool ITER>
-__global__ __launch_bounds__(256) void bb_k1b(bsls_bb_problem P, int64_t iter, double *part,
-                                              unsigned *ticket) {
-    __shared__ double red[4];
-    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev =
+            __hip_atomic_fetch_add(&tkrb[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        row_last = (prev == (unsigned)G - 1);
+        if (row_last) __hip_atomic_store(&tkrb[rb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!row_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t r0 = rb * PANEL_WAVES * M.prow;
+    const int64_t r1 = (r0 + PANEL_WAVES * M.prow < P.m) ? r0 + PANEL_WAVES * M.prow : P.m;
     double sq[1] = {0.0};
-    if (i < P.m) {
-        // all group partials in flight at once, summed in group order
-        const int64_t G = P.A.ngroups;
-        double v[8];
+    // up to RPT rows per thread, every partial load of them in flight at once
+    constexpr int RPT = 4;
+    for (int64_t row0 = r0 + threadIdx.x; row0 < r1; row0 += RPT * blockDim.x) {
+        double v[RPT][8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = (c < G) ? P.rpart[c * P.m + i] : 0.0;
-        double o = v[0];
+        for (int u = 0; u < RPT; ++u) {
+            const int64_t row = row0 + (int64_t)u * blockDim.x;
+            const int64_t rr = row < r1 ? row : r0;
 #pragma unroll
-        for (int c = 1; c < 8; ++c)
-            if (c < G) o += v[c];
-        for (int64_t c = 8; c < G; ++c) o += P.rpart[c * P.m + i];
-        if (ADD) o += P.target[i];
-        P.r[i] = o;
-        sq[0] = o * o;
+            for (int c = 0; c < 8; ++c)
+                v[u][c] = (c < G) ? __hip_atomic_load(&P.rpart[c * P.m + rr], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int64_t row = row0 + (int64_t)u * blockDim.x;
+            if (row >= r1) continue;
+            double o = v[u][0];
+#pragma unroll
+            for (int c = 1; c < 8; ++c)
+                if (c < G) o += v[u][c];
+            for (int64_t c = 8; c < G; ++c)
+                o += __hip_atomic_load(&P.rpart[c * P.m + row], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (ADD) o += P.target[row];
+            P.r[row] = o;
+            sq[0] += o * o;
+        }
     }
     if (!REDUCE) return;
-    block_sum<1>(sq, red);
+    const unsigned nrb = (unsigned)((M.npanels + PANEL_WAVES - 1) / PANEL_WAVES);
+    block_sum<1>(sq, lds);
     double tot[1];
-    if (last_block_sum<1>(sq, part, ticket, tot, red) && threadIdx.x == 0)
+    if (last_of_sum<1>(sq, part, (unsigned)rb, nrb, ticket, tot, lds) && threadIdx.x == 0)
         bb_record_f(P, iter, tot[0], ITER);
 }
 
@@ -281,13 +312,14 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
     const int l = lane_id();
     const int64_t z0 = P.pk_z0[pk], b0 = P.pk_b0[pk];
     const int L = P.pk_len[pk];
+    __shared__ double pv_y[4][64];
+    __shared__ int pv_p[4][64];
     if (L <= WAVE) {
         const uint64_t B = (uint64_t)P.pk_mask[pk];
         const bool act = l < L;
         double y = act ? zc[z0 + l] - t * g[z0 + l] : 0.0;  // x_next = x - t g (BB.py:29)
-        int w = 1;
-        uint64_t heads;
-        pava_v1_wave(y, w, L, B, heads);
+        const int wv = threadIdx.x / WAVE;
+        pava_v1_wave_c(y, L, B, pv_y[wv], pv_p[wv]);
         const double v = clip01(y);
         const double vprev = shfl_d(v, l > 0 ? l - 1 : 0);
         if (act) {
@@ -356,9 +388,9 @@ template <int MODE, bool ADD, bool REDUCE, bool ITER>
 static void launch_k1_mode(const bsls_bb_problem &P, int64_t iter, const BBWork &w,
                            hipStream_t st) {
     const int64_t rbs = (P.A.npanels + PANEL_WAVES - 1) / PANEL_WAVES;
-    allow_lds(bb_k1a<MODE, ITER>);
-    bb_k1a<MODE, ITER><<<(int)(P.A.ngroups * rbs), 1024, panel_lds_bytes(P.A), st>>>(P);
-    bb_k1b<ADD, REDUCE, ITER><<<grid_for(P.m, 256), 256, 0, st>>>(P, iter, w.p1, w.tk1);
+    allow_lds(bb_k1<MODE, ITER, ADD, REDUCE>);
+    bb_k1<MODE, ITER, ADD, REDUCE><<<(int)(P.A.ngroups * rbs), 1024, panel_lds_bytes(P.A), st>>>(
+        P, iter, w.tkrb, w.p1, w.tk1);
 }
 
 template <bool ADD, bool REDUCE, bool ITER>
@@ -432,7 +464,7 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
     switch (stage) {
         case 0:  // reset scalars and tickets
             BSLS_CHECK(hipMemsetAsync(P.scal, 0, BSLS_S_COUNT * sizeof(double), st));
-            BSLS_CHECK(hipMemsetAsync(P.work, 0, al16(3 * TICKET_BYTES), st));
+            BSLS_CHECK(hipMemsetAsync(P.work, 0, (size_t)((char *)w.p1 - (char *)P.work), st));
             return BSLS_OK;
         case 1:  // r_partial = A_g x_g
             if (iter > 0) launch_k1<false, false, true>(P, iter, w, st);

@@ -136,6 +136,44 @@ __device__ bool last_block_sum(const double (&mine)[NV], double *partials, unsig
     return true;
 }
 
+// Same hand-off for a subset of the workgroups: `count` participants, this
+// one publishing slot `idx`; one ticket word (few arrivals).  The last arriver
+// sums slots 0 .. count-1 in order and re-zeroes the ticket.
+template <int NV>
+__device__ bool last_of_sum(const double (&mine)[NV], double *partials, unsigned idx,
+                            unsigned count, unsigned *ticket, double (&tot)[NV], double *red) {
+    __shared__ int am_last_n;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            __hip_atomic_store(&partials[(size_t)idx * NV + k], mine[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev =
+            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        am_last_n = (prev == count - 1);
+    }
+    __syncthreads();
+    if (!am_last_n) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    for (unsigned i = threadIdx.x; i < count; i += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            acc[k] += __hip_atomic_load(&partials[(size_t)i * NV + k], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    }
+    block_sum<NV>(acc, red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) tot[k] = acc[k];
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+}
+
 // numpy.minimum(v, 1.) then numpy.maximum(., 0.) (python/main.py:65):
 // NaN propagates, -0.0 is kept.
 __device__ __forceinline__ double clip01(double v) {

@@ -91,4 +91,98 @@ __device__ __forceinline__ void pava_v1_wave(double &y, int &w, int L, uint64_t 
     if (act) y = yh;
 }
 
+// ---------------------------------------------------------------------------
+// Compacted form (what K3 runs).  The pass structure and every rounding are the
+// same as above; the state is kept per RUN instead of per element: lane t holds
+// run t of the pack (value Y, length W, block-start flag, first element O),
+// runs packed into lanes 0 .. nh-1 after every pass (a 768-B LDS scatter per
+// wave).  Then the previous run is lane t-1 (DPP shift), a chain is a range of
+// consecutive lanes, and its in-order pooled sum  num = ((0 + y0 w0) + y1 w1)
+// + ...  is a DPP scan, one step per chain member -- about half the VALU of
+// the element-lane form (whose searches are 64-bit mask ops and bpermutes).
+// Checked bit-for-bit against the reference PAVA (oracle) in
+// tests/test_gpu_bb.py::test_k3_wave_pava_bit_exact.
+
+// lane l - 1's value (lane 0: 0), DPP wave_shr:1
+__device__ __forceinline__ int dpp_shr1_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double dpp_shr1_d(double v) {
+    const int lo = dpp_shr1_i(__double2loint(v));
+    const int hi = dpp_shr1_i(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// y: this lane's element (lanes < L); B: block starts (bit 0 set).  ys / ps:
+// this wave's 64 doubles / 64 ints of LDS.  On return y = the expanded fit.
+__device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, double *ys,
+                                               int *ps) {
+    const int t = lane_id();
+    double Y = y;
+    int W = 1, BS = (int)((B >> t) & 1ull), O = t;
+    int nh = L;
+    for (int pass = 0; pass <= L; ++pass) {
+        const bool act = t < nh;
+        const double yp = dpp_shr1_d(Y);
+        const bool cs = act && (BS || !(Y <= yp));     // lane 0 is always a block start
+        const uint64_t CS = __ballot(cs);
+        const uint64_t above = CS & ~mask_le(t);
+        const int nxt = above ? lo_bit(above) : nh;    // next chain start
+        const int last = (nxt > 0 ? nxt : 1) - 1;      // this chain's last run
+        const double ylast = shfl_d(Y, last);
+        const bool pool = cs && (Y != ylast);
+        const uint64_t POOL = __ballot(pool);
+        if (!POOL) break;
+        const uint64_t csle = CS & mask_le(t);
+        const int mycs = csle ? hi_bit(csle) : 0;
+        const bool inpool = act && ((POOL >> mycs) & 1ull);
+        const int depth = t - mycs;
+        const double pr = Y * (double)W;
+        double num = 0.0 + pr;
+        int den = W;
+        const int maxd = wave_max(inpool ? depth : 0);
+        for (int k = 1; k <= maxd; ++k) {
+            const double np = dpp_shr1_d(num);
+            const int dp = dpp_shr1_i(den);
+            if (inpool && depth == k) {
+                num = np + pr;
+                den = dp + W;
+            }
+        }
+        const double tn = shfl_d(num, last);
+        const int td = shfl_i(den, last);
+        if (pool) {
+            Y = tn / (double)td;
+            W = td;
+        }
+        // pack the surviving runs into lanes 0 .. nh-1
+        const bool surv = act && !(inpool && depth > 0);
+        const uint64_t S = __ballot(surv);
+        if (surv) {
+            const int idx = mbcnt64(S);
+            ys[idx] = Y;
+            ps[idx] = W | (BS << 8) | (O << 9);
+        }
+        nh = __popcll(S);
+        if (t < nh) {
+            Y = ys[t];
+            const int pk = ps[t];
+            W = pk & 255;
+            BS = (pk >> 8) & 1;
+            O = pk >> 9;
+        }
+    }
+    // expand: element e takes the value of the last run starting at or before e
+    ps[t] = 0;
+    if (t < nh) ps[O] = 1;
+    const uint64_t RS = __ballot(t < L && ps[t] != 0);
+    const int idx = mbcnt64(RS) + (int)((RS >> t) & 1ull) - 1;
+    const double v = shfl_d(Y, idx < 0 ? 0 : idx);
+    if (t < L) y = v;
+}
+
 }  // namespace bsls

@@ -16,7 +16,7 @@ from collections import defaultdict
 KERNELS = {
     'K2_spmvT_Nt_dots': ['bsls::bb_k2<2, true>'],
     'K3_pava_clip_z2x': ['bsls::bb_k3('],
-    'K1_spmv_A': ['bsls::bb_k1a<0, true>', 'bsls::bb_k1b<true, true, true>'],
+    'K1_spmv_A': ['bsls::bb_k1<0, true, true, true>'],
     'proj_simplex_C2': ['bsls::proj_small_kernel<false>'],
 }
 
