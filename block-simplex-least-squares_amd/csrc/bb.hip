@@ -216,11 +216,14 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
     const bool live = panel < M.npanels;
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     double sc[4] = {0.0, 0.0, 0.0, 0.0};
-    if (MODE == 2 && live) {
+    if (MODE == 2) {
+        // unconditional loads at clamped rows (all in flight together)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t i = i0 + 64 * q + lane;        // halo row included
-            if (64 * q + lane <= M.prow && i < P.n) sc[q] = P.colv[i];
+            const bool ok = live && 64 * q + lane <= M.prow && i < P.n;
+            const double v = P.colv[ok ? i : 0];
+            sc[q] = ok ? v : 0.0;
         }
     }
     panel_chunks<MODE>(M, blockIdx.x, wv, 0, M.nchunks, P.r, lds, s, sc);
@@ -235,17 +238,34 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
     }
     __syncthreads();   // the chunk table becomes the reduction scratch below
     double sums[4] = {0.0, 0.0, 0.0, 0.0};
+    // epilogue operands: unconditional loads at clamped indices, all in flight
+    int32_t j[4];
+    double gpj[4], zcj[4], zpj[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int pos = 64 * q + lane;
         const int64_t i = i0 + pos;
-        const int32_t j = (live && pos < M.prow && i < P.n) ? P.xz[i] : -1;
-        if (j >= 0) {
+        const bool ok = live && pos < M.prow && i < P.n;
+        const int32_t jj = P.xz[ok ? i : 0];
+        j[q] = ok ? jj : -1;
+    }
+    if (ITER) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int32_t jc = j[q] >= 0 ? j[q] : 0;
+            gpj[q] = gp[jc];
+            zcj[q] = zc[jc];
+            zpj[q] = zp[jc];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (j[q] >= 0) {
             const double g = s[q] - nx[q];
-            gout[j] = g;
+            gout[j[q]] = g;
             if (ITER) {
-                const double dg = g - gp[j];
-                const double dz = zc[j] - zp[j];
+                const double dg = g - gpj[q];
+                const double dz = zcj[q] - zpj[q];
                 sums[0] += dg;
                 sums[1] += dz * dg;
                 sums[2] += dg * dg;

@@ -37,6 +37,12 @@ namespace bsls {
 constexpr int PANEL_WAVES = BSLS_PANEL_WAVES;   // panels per workgroup (1024 threads)
 
 __device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// a wave-uniform value the compiler cannot prove uniform, moved to SGPRs
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)v);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
 
 // Dynamic LDS of a panel kernel: the chunk table (tab_cap doubles; K2 reuses
 // it as reduction scratch, hence >= 64).
@@ -82,17 +88,18 @@ struct SegHead {
 
     __device__ __forceinline__ void load(const bsls_panels &M, int64_t seg, bool live) {
         const int lane = lane_id();
-        const int64_t info = live ? M.seg_info[seg] : 0;
-        int64_t co = live ? M.cnt_off[seg] : 0;
-        e0 = live ? M.ent_off[seg] : 0;
+        // seg is wave-uniform (padded panels have empty segments): scalar loads.
+        // Straight-line, unconditional vector loads (a dead slice reads the next
+        // group of counts, ignored), so the compiler can count them in vmcnt.
+        (void)live;
+        const int64_t info = M.seg_info[seg];
+        int64_t co = M.cnt_off[seg];
+        e0 = M.ent_off[seg];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             D[q] = (int)((info >> (16 * q)) & 0xFFFF);
-            incl[q] = 0;
-            if (D[q] > 0) {
-                incl[q] = (int)M.cnt[co + lane];
-                co += 64;
-            }
+            incl[q] = (int)M.cnt[co + lane];
+            co += (D[q] > 0) ? 64 : 0;
         }
     }
 };
@@ -115,29 +122,25 @@ struct SegBody {
         uint32_t e = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            // stored: running total of even-padded run lengths | (own count odd);
+            // straight-line and unconditional (a dead slice reads at the running
+            // offset: within the segments that follow, or the array's slack)
             D[q] = h.D[q];
-            cnt[q] = 0;
-            base[q] = 0;
-            if (D[q] > 0) {
-                // stored: running total of even-padded run lengths | (own count odd)
-                const int inc = h.incl[q] & ~1;
-                const int ex = wave_shr1(h.incl[q]) & ~1;
-                cnt[q] = inc - ex - (h.incl[q] & 1);
-                base[q] = e + (uint32_t)ex;
-                e += (uint32_t)(readlane_i(h.incl[q], 63) & ~1);
+            const bool on = D[q] > 0;
+            const int inc = h.incl[q] & ~1;
+            const int ex = wave_shr1(h.incl[q]) & ~1;
+            cnt[q] = on ? inc - ex - (h.incl[q] & 1) : 0;
+            base[q] = e + (on ? (uint32_t)ex : 0u);
+            e += on ? (uint32_t)(readlane_i(h.incl[q], 63) & ~1) : 0u;
 #pragma unroll
-                for (int j = 0; j < DBK / 2; ++j) {
-                    // a row's run is even-padded: two entries per aligned 32-bit load;
-                    // lanes past their row's end read the next row's: harmless
-                    c2[q][j] = 0u;
-                    if (2 * j < D[q]) {
-                        c2[q][j] = *reinterpret_cast<const uint32_t *>(
-                            reinterpret_cast<const char *>(ent) + (base[q] + 2 * j) * 2u);
-                        if (MODE == 1) {
-                            v[q][2 * j] = val[base[q] + 2 * j];
-                            v[q][2 * j + 1] = val[base[q] + 2 * j + 1];
-                        }
-                    }
+            for (int j = 0; j < DBK / 2; ++j) {
+                // a row's run is even-padded: two entries per aligned 32-bit load;
+                // lanes past their row's end read the next row's: harmless
+                c2[q][j] = *reinterpret_cast<const uint32_t *>(
+                    reinterpret_cast<const char *>(ent) + (base[q] + 2 * j) * 2u);
+                if (MODE == 1) {
+                    v[q][2 * j] = val[base[q] + 2 * j];
+                    v[q][2 * j + 1] = val[base[q] + 2 * j + 1];
                 }
             }
         }
@@ -208,6 +211,8 @@ template <int MODE>
 __device__ __forceinline__ void panel_chunks(const bsls_panels &M, int64_t rb, int wv, int64_t c0,
                                              int64_t c1, const double *src, double *tab,
                                              double (&s)[4], const double (&sc)[4]) {
+    wv = __builtin_amdgcn_readfirstlane(wv);              // uniform: scalar segment loads
+    rb = uni64(rb);
     const bool live = rb * PANEL_WAVES + wv < M.npanels;
     const int64_t seg0 = (rb * M.nchunks) * PANEL_WAVES + wv;
     auto seg = [&](int64_t c) { return seg0 + c * PANEL_WAVES; };
