@@ -25,10 +25,12 @@
 //
 // Latency: the 16 waves move in lockstep between the per-chunk barriers, and
 // a chunk's entries depend on its running counts (their addresses).  Counts
-// are loaded two chunks ahead, entries one chunk ahead, so both round trips
-// hide behind a whole walk + barrier + LDS-DMA (measured with
-// tools/panel_ubench.py: loads issued just before the next barrier left
-// 32 of 45 us exposed).
+// are loaded two chunks ahead, entries one chunk ahead, issued right after a
+// walk so they fly across the barrier and the LDS-DMA of the next chunk.  The
+// prefetch loads are straight-line and unconditional so the compiler can
+// count them in vmcnt; nothing is issued before a walk, whose own waits
+// (vmcnt is in order) would otherwise drain the prefetch (measured with
+// tools/panel_ubench.py's per-chunk timeline).
 #pragma once
 #include "bsls_common.hpp"
 
@@ -231,9 +233,12 @@ __device__ __forceinline__ void panel_chunks(const bsls_panels &M, int64_t rb, i
             panel_stage(tab, src + col0, (int)(M.chunk_col[c + 1] - col0));
         }
         __syncthreads();
+        // walk first: its long-row loads wait on vmcnt, which is in order, so
+        // no prefetch may be outstanding yet; the prefetch issued after it flies
+        // across the next barrier and DMA
+        if (live) cur.walk(M, tab, s, sc);
         if (c + 1 < c1) bn.load(M, hn);
         if (c + 2 < c1) hn2.load(M, seg(c + 2), live);
-        if (live) cur.walk(M, tab, s, sc);
     };
     for (int64_t c = c0; c < c1; c += 2) {
         step(c, ba, hb, bb, ha);

@@ -221,8 +221,6 @@ __global__ __launch_bounds__(1024) void k2_trace(bsls_panels M, const double *__
         }
         __syncthreads();
         if (rec) t[ti++] = wall_clock64();
-        if (c + 1 < c1) bn.load(M, hn);
-        if (c + 2 < c1) hn2.load(M, seg(c + 2), live);
         const long long tw0 = wall_clock64();
         if (live) cur.walk(M, lds, s, sc);
         {
@@ -236,6 +234,8 @@ __global__ __launch_bounds__(1024) void k2_trace(bsls_panels M, const double *__
                 u[2 * c + 1] = deep;
             }
         }
+        if (c + 1 < c1) bn.load(M, hn);
+        if (c + 2 < c1) hn2.load(M, seg(c + 2), live);
         if (rec) {
             // the walk's adds are done when s is: force it
             double z = s[0] + s[1] + s[2] + s[3];
