@@ -10,9 +10,12 @@
 // descending sort reproduces them; the S_i chain itself is sequential.
 //
 // Three size classes (host passes max_block; the small kernel routes the rest):
-//   k <= 64      one LANE per block: block in registers, bitonic network of
-//                8/16/32/64 (wave-uniform, chosen by the wave's largest block),
-//                the S_i chain in-lane -> 64 blocks progress per wave;
+//   k <= 64      one LANE per block (proj_lds_kernel): a wave stages its 64
+//                consecutive blocks in LDS (DMA), each lane sorts its block in
+//                registers with a flip-bitonic network pruned at compile time
+//                to the wave's largest block, runs the S_i chain (division-
+//                free test, the reference's division only within ulps) and
+//                writes back through LDS -- all straight-line code;
 //   64 < k <= 8192   one WORKGROUP per block: LDS bitonic sort, S_i by one
 //                thread into LDS, conditions + last-index search in parallel;
 //   k > 8192     one workgroup, sort in a global workspace (rare: the
@@ -62,12 +65,15 @@ __device__ __forceinline__ void bitonic_desc(double (&v)[N]) {
     }
 }
 
-template <int N>
+// proj_simplex.h:22-30 on u sorted descending, literally: S_i = sequential
+// sum, lambda = (1 - S_i)/(i + 1) at the LAST i with u_i + that > 0 (else
+// 1 - u_0).  Entries i >= KB are -inf padding and never reached.
+template <int N, int KB = N>
 __device__ __forceinline__ double lambda_sorted(const double (&u)[N], int k) {
     double run = u[0];
     double lam = 1. - run;
 #pragma unroll
-    for (int i = 1; i < N; ++i) {
+    for (int i = 1; i < KB; ++i) {
         if (i < k) {
             run = run + u[i];
             const double cand = (1. - run) / ((double)i + 1.);
@@ -77,8 +83,75 @@ __device__ __forceinline__ double lambda_sorted(const double (&u)[N], int k) {
     return lam;
 }
 
-template <int N, bool BALL>
-__device__ __forceinline__ void lane_block(double *__restrict__ y, int64_t s, int k) {
+// The same lambda without a division per i and without branches.  The test
+// u_i + fl(D_i/(i+1)) > 0 (D_i = fl(1 - S_i)) is decided by the sign of
+// E = fl((i+1) u_i + D_i) (one fma, sign-exact): E <= 0 -> false (the
+// quotient rounds to <= -u_i); E > T = (i+1)(|u_i| 2^-51 + 2^-1070) -> true
+// (the quotient clears -u_i by more than its rounding error).  In between
+// (within a few ulps) the lane reports `amb` and the caller redoes the lane
+// with lambda_sorted; one division per block remains (lambda itself).
+template <int N, int KB>
+__device__ __forceinline__ double lambda_fast(const double (&u)[N], int k, bool &amb) {
+    double run = u[0];
+    const double D0 = 1. - run;
+    double Drho = D0;
+    int rho = 0;
+    int a = 0;
+#pragma unroll
+    for (int i = 1; i < KB; ++i) {
+        run = run + u[i];
+        const double D = 1. - run;
+        const double ip1 = (double)i + 1.;
+        const double E = __builtin_fma(ip1, u[i], D);
+        const double T = ip1 * __builtin_fma(__builtin_fabs(u[i]), 0x1p-51, 0x1p-1070);
+        const bool live = i < k;
+        const bool c = live && (E > T);
+        a |= (live && (E > 0.0) && !(E > T)) ? 1 : 0;
+        rho = c ? i : rho;
+        Drho = c ? D : Drho;
+        // materialise the running selects every step: left alone, the
+        // compiler keeps every D_i and mask live and spills them
+        asm volatile("" : "+v"(Drho), "+v"(rho), "+v"(a), "+v"(run));
+    }
+    amb = a != 0;
+    return rho == 0 ? D0 : Drho / ((double)rho + 1.);
+}
+
+// Descending "flip" bitonic network: every comparator puts the max at the
+// lower index, so -inf padding at indices >= KB never moves and every
+// comparator that touches an index >= KB is dropped at compile time (the
+// wave's largest block picks KB).  Comparators are 2-instruction asm so the
+// scheduler keeps a stage's live ranges short (plain fmax/fmin: 255 VGPRs).
+template <int N, int KB>
+__device__ __forceinline__ void bitonic_flip(double (&v)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                int l;
+                if (j == (k >> 1)) {
+                    const int blk = i & ~(k - 1);
+                    l = ((i - blk) < (k >> 1)) ? blk + k - 1 - (i - blk) : -1;
+                } else {
+                    l = i ^ j;
+                }
+                if (l > i && l < KB) {
+                    double hi, lo;
+                    asm volatile("v_max_f64 %0, %2, %3\n\tv_min_f64 %1, %2, %3"
+                                 : "=&v"(hi), "=v"(lo)
+                                 : "v"(v[i]), "v"(v[l]));
+                    v[i] = hi;
+                    v[l] = lo;
+                }
+            }
+        }
+    }
+}
+
+template <int N, bool BALL, typename Ptr>
+__device__ __forceinline__ void lane_block(Ptr y, int64_t s, int k) {
     double v[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) v[j] = (j < k) ? y[s + j] : -INFINITY;
@@ -112,31 +185,151 @@ __device__ __forceinline__ void lane_block(double *__restrict__ y, int64_t s, in
     }
 }
 
+// Blocks <= 64 with the wave's contiguous range staged in LDS: one wave per
+// 64 consecutive blocks (one lane each).  The range is read and written with
+// coalesced 8-B-per-lane accesses; the lanes then sort / project their own
+// blocks out of LDS.  Without staging, every wave-instruction touched 64 cache
+// lines (one per block) -- measured 2.6x write amplification.  A wave whose
+// range exceeds PCAP doubles falls back to direct global access.
+constexpr int PCAP = 3072;
+constexpr int PBUF = PCAP + 2 * WAVE + 2;   // + read slack, + one dummy slot per lane
+
+__device__ __forceinline__ int64_t uni64(int64_t v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+
+// One lane, one block of k <= KB entries at buf[off ..): straight-line code.
+// Reads are unconditional (slack after the range), writes of j >= k go to the
+// lane's dummy slot, so no per-entry branches or per-entry waits.
+template <int N, int KB, bool BALL>
+__device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int lane) {
+    double v[N];
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        double t = -INFINITY;
+        if (j < KB) t = buf[off + j];
+        if (BALL) {
+            // proj_simplex.h:56-64: clamp negatives, sum the rest in order
+            // (adding the clamped 0.0 leaves acc's bits unchanged: acc >= +0)
+            t = (t < 0.0) ? 0.0 : t;
+            acc += (j < k) ? t : 0.0;
+        }
+        v[j] = (j < k) ? t : -INFINITY;
+    }
+    const bool need = BALL ? (acc > 1.0) : true;
+    double lam = 0.0;
+    if (!BALL || __builtin_amdgcn_ballot_w64(need)) {
+        bitonic_flip<N, KB>(v);
+        bool amb;
+        lam = lambda_fast<N, KB>(v, k, amb);
+        if (__builtin_amdgcn_ballot_w64(amb)) {
+            if (amb) lam = lambda_sorted<N, KB>(v, k);
+        }
+    }
+    asm volatile("" ::: "memory");   // keep the o[] loads after the sort (VGPRs)
+    double o[KB];
+#pragma unroll
+    for (int j = 0; j < KB; ++j) o[j] = buf[off + j];
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+        double t = o[j];
+        if (BALL) t = (t < 0.0) ? 0.0 : t;
+        const double r = need ? relu_ref(lam + t) : t;
+        buf[(j < k) ? off + j : PCAP + WAVE + 2 + lane] = r;
+    }
+}
+
+// (64, 2): at most 256 VGPRs so two waves fit per SIMD -- the whole C2 grid
+// (~6 waves per CU) is then resident at once.
 template <bool BALL>
-__global__ __launch_bounds__(256) void proj_small_kernel(double *__restrict__ y,
-                                                         const int64_t *__restrict__ starts,
-                                                         int64_t nb, int64_t n,
-                                                         int64_t *__restrict__ big_list,
-                                                         unsigned *__restrict__ big_count) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
+                                                      const int64_t *__restrict__ starts,
+                                                      int64_t nb, int64_t n,
+                                                      int64_t *__restrict__ big_list,
+                                                      unsigned *__restrict__ big_count,
+                                                      int allow_big) {
+    __shared__ __attribute__((aligned(16))) double buf[PBUF];
+    const int lane = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t b = b0 + lane;
     int k = 0;
-    int64_t s = 0;
+    int64_t s = 0, e = 0;
     if (b < nb) {
         s = starts[b];
-        const int64_t kk = block_end(starts, nb, b, n) - s;
+        e = block_end(starts, nb, b, n);
+        const int64_t kk = e - s;
         if (kk > SMALL_MAX) {
-            unsigned slot = atomicAdd(big_count, 1u);
-            big_list[slot] = b;
+            if (allow_big) {   // (a block > max_block breaks the contract: left as is)
+                unsigned slot = atomicAdd(big_count, 1u);
+                big_list[slot] = b;
+            }
         } else {
             k = (int)kk;
         }
     }
     const int kmax = wave_max(k);
     if (kmax == 0) return;
-    if (kmax <= 8) lane_block<8, BALL>(y, s, k);
-    else if (kmax <= 16) lane_block<16, BALL>(y, s, k);
-    else if (kmax <= 32) lane_block<32, BALL>(y, s, k);
-    else lane_block<64, BALL>(y, s, k);
+    const int lastl = (int)((nb - b0 < WAVE ? nb - b0 : WAVE) - 1);
+    const int64_t s0 = uni64(s, 0);
+    const int64_t e1 = uni64(e, lastl);
+    const int64_t total = e1 - s0;
+    if (total > PCAP) {
+        if (kmax <= 8) lane_block<8, BALL>(y, s, k);
+        else if (kmax <= 16) lane_block<16, BALL>(y, s, k);
+        else if (kmax <= 32) lane_block<32, BALL>(y, s, k);
+        else lane_block<64, BALL>(y, s, k);
+        return;
+    }
+    const int tot = (int)total;
+    // buf[sh + i] = y[s0 + i]: the 16-B pairs inside the range by LDS DMA
+    // (all in flight at once, no VGPRs), the unaligned head / odd tail by
+    // lane 0.  sh = 1 when y + s0 is not 16-B aligned.
+    const double *src = y + s0;
+    const int sh = (int)(((uintptr_t)src >> 3) & 1);
+    const int npair = (tot - sh) >> 1;
+    {
+        const char *gs = (const char *)(src + sh);
+        char *ls = (char *)(buf + 2 * sh);
+        for (int p = 0; p * WAVE < npair; ++p) {
+            const int i = p * WAVE + lane;
+            if (i < npair)
+                __builtin_amdgcn_global_load_lds((const void *)(gs + 16 * i),
+                                                 (__attribute__((address_space(3))) void *)(ls + 1024 * p),
+                                                 16, 0, 0);
+        }
+        if (lane == 0) {
+            if (sh) buf[1] = src[0];
+            if ((tot - sh) & 1) buf[sh + tot - 1] = src[tot - 1];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int off = (k > 0) ? (int)(s - s0) + sh : 0;
+    if (kmax <= 8) lane_block_lds<8, 8, BALL>(buf, off, k, lane);
+    else if (kmax <= 16) lane_block_lds<16, 16, BALL>(buf, off, k, lane);
+    else if (kmax <= 32) lane_block_lds<32, 32, BALL>(buf, off, k, lane);
+    else if (kmax <= 40) lane_block_lds<64, 40, BALL>(buf, off, k, lane);
+    else if (kmax <= 48) lane_block_lds<64, 48, BALL>(buf, off, k, lane);
+    else if (kmax <= 56) lane_block_lds<64, 56, BALL>(buf, off, k, lane);
+    else lane_block_lds<64, 64, BALL>(buf, off, k, lane);
+    __syncthreads();
+    constexpr int SB = 16;   // LDS reads in flight per lane before the stores
+    for (int c0 = 0; c0 < tot; c0 += SB * WAVE) {
+        double t[SB];
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+            const int i = c0 + q * WAVE + lane;
+            t[q] = buf[sh + (i < tot ? i : 0)];
+        }
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+            const int i = c0 + q * WAVE + lane;
+            if (i < tot) y[s0 + i] = t[q];
+        }
+    }
 }
 
 // In-place descending bitonic sort of u[0..P) by the whole workgroup
@@ -315,8 +508,12 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
     if (max_block < 1) return BSLS_E_ARG;
     ProjWork w = proj_layout(work, n, nb, max_block);
     if (work == nullptr || work_bytes < w.bytes) return BSLS_E_WORKSPACE;
-    BSLS_CHECK(hipMemsetAsync(w.count, 0, 16, st));
-    proj_small_kernel<BALL><<<grid_for(nb, 256), 256, 0, st>>>(y, starts, nb, n, w.list, w.count);
+    // the big-block list is only used when some block can exceed SMALL_MAX
+    // (max_block is the caller's bound on every block length, like the
+    // workspace size derived from it): otherwise no reset launch at all
+    if (max_block > SMALL_MAX) BSLS_CHECK(hipMemsetAsync(w.count, 0, 16, st));
+    proj_lds_kernel<BALL><<<grid_for(nb, WAVE), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                                  max_block > SMALL_MAX);
     BSLS_LAUNCH_CHECK();
     if (max_block > SMALL_MAX) {
         int64_t nbig = nb < (n / (SMALL_MAX + 1) + 1) ? nb : (n / (SMALL_MAX + 1) + 1);

@@ -95,6 +95,28 @@ def test_proj_ties_and_zeros(cx, orc):
         assert exact(a, r)
 
 
+def test_proj_borderline_decisions(cx, orc):
+    """Values on coarse dyadic grids make u_i + (1 - S_i)/(i + 1) land exactly
+    on, or within a few ulps of, zero for many i: the cases the kernel decides
+    with the reference's own division instead of the fma sign test."""
+    rs = np.random.RandomState(SEED + 5)
+    n = 60_000
+    sizes = rs.randint(1, 65, size=3000)
+    sizes = sizes[np.cumsum(sizes) <= n]
+    n = int(sizes.sum())
+    starts = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+    grids = [rs.randint(-16, 17, size=n) / 8.0,
+             rs.randint(-64, 65, size=n) / 64.0,
+             1.0 / rs.randint(1, 9, size=n) - rs.randint(0, 2, size=n) / 3.0,
+             np.repeat(rs.randint(-4, 5, size=sizes.size) / 4.0, sizes)
+             + rs.randint(-2, 3, size=n) * 2.0 ** -50]
+    for gi, y in enumerate(grids):
+        for name in ('proj_multi_simplex_c', 'proj_multi_ball_c'):
+            a = y.copy(); getattr(cx, name)(a, starts)
+            r = y.copy(); getattr(orc, name)(r, starts)
+            assert exact(a, r), (gi, name)
+
+
 # ------------------------------------------------------------------ PAVA
 
 def test_isotonic_golden(cx, golden):
