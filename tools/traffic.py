@@ -17,7 +17,7 @@ KERNELS = {
     'K2_spmvT_Nt_dots': ['bsls::bb_k2<2, true>'],
     'K3_pava_clip_z2x': ['bsls::bb_k3('],
     'K1_spmv_A': ['bsls::bb_k1<0, true, true, true>'],
-    'proj_simplex_C2': ['bsls::proj_small_kernel<false>'],
+    'proj_simplex_C2': ['bsls::proj_lds_kernel<false>'],
 }
 
 
