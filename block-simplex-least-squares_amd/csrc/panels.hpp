@@ -117,6 +117,13 @@ struct SegBody {
     uint32_t c2[4][DBK / 2];   // column offsets of diagonals 2j, 2j+1 (low, high half)
     double v[4][DBK];    // values (MODE 1)
 
+    // DBK entries of one row from its (even, i.e. 4-B aligned) entry index i:
+    // one 16-B load (dword alignment suffices for global dwordx4)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+    __device__ __forceinline__ static u32x4 ent8(const uint16_t *ent, uint32_t i) {
+        return *reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(ent) + i * 2u);
+    }
+
     __device__ __forceinline__ void load(const bsls_panels &M, const SegHead &h) {
         const uint16_t *ent = M.ent + h.e0;
         const double *val = M.val + h.e0;
@@ -134,15 +141,21 @@ struct SegBody {
             cnt[q] = on ? inc - ex - (h.incl[q] & 1) : 0;
             base[q] = e + (on ? (uint32_t)ex : 0u);
             e += on ? (uint32_t)(readlane_i(h.incl[q], 63) & ~1) : 0u;
+            // a row's run is even-padded; lanes past their row's end read the
+            // next rows' entries (or the array's 64-entry slack): harmless
+            if (DBK == 8) {
+                const u32x4 w = ent8(ent, base[q]);
 #pragma unroll
-            for (int j = 0; j < DBK / 2; ++j) {
-                // a row's run is even-padded: two entries per aligned 32-bit load;
-                // lanes past their row's end read the next row's: harmless
-                c2[q][j] = *reinterpret_cast<const uint32_t *>(
-                    reinterpret_cast<const char *>(ent) + (base[q] + 2 * j) * 2u);
-                if (MODE == 1) {
-                    v[q][2 * j] = val[base[q] + 2 * j];
-                    v[q][2 * j + 1] = val[base[q] + 2 * j + 1];
+                for (int j = 0; j < 4; ++j) c2[q][j] = w[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < DBK / 2; ++j) {
+                    c2[q][j] = *reinterpret_cast<const uint32_t *>(
+                        reinterpret_cast<const char *>(ent) + (base[q] + 2 * j) * 2u);
+                    if (MODE == 1) {
+                        v[q][2 * j] = val[base[q] + 2 * j];
+                        v[q][2 * j + 1] = val[base[q] + 2 * j + 1];
+                    }
                 }
             }
         }
@@ -181,12 +194,21 @@ struct SegBody {
             for (int k0 = DBK; k0 < D[q]; k0 += DBK) {
                 int cc[DBK];
                 double vv[DBK];
+                if (DBK == 8) {
+                    // one 16-B load per 8 diagonals; a lane whose row has ended
+                    // re-reads its first entries (any in-chunk offset will do)
+                    const u32x4 w = ent8(ent, base[q] + (k0 < cnt[q] ? (uint32_t)k0 : 0u));
 #pragma unroll
-                for (int k = 0; k < DBK; ++k) {
-                    const uint32_t i = base[q] + (uint32_t)(k0 + k);
-                    const bool in = k0 + k < cnt[q];
-                    cc[k] = in ? (int)ent[i] : 0;
-                    if (MODE == 1) vv[k] = in ? val[i] : 0.0;
+                    for (int k = 0; k < DBK; ++k)
+                        cc[k] = (int)((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xFFFFu));
+                } else {
+#pragma unroll
+                    for (int k = 0; k < DBK; ++k) {
+                        const uint32_t i = base[q] + (uint32_t)(k0 + k);
+                        const bool in = k0 + k < cnt[q];
+                        cc[k] = in ? (int)ent[i] : 0;
+                        if (MODE == 1) vv[k] = in ? val[i] : 0.0;
+                    }
                 }
 #pragma unroll
                 for (int k = 0; k < DBK; ++k) {
