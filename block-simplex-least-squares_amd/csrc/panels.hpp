@@ -81,6 +81,33 @@ __device__ __forceinline__ int wave_shr1(int v) {
     return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false);
 }
 
+// Uniform int64 metadata through the scalar unit: s_load waits on lgkmcnt,
+// not vmcnt.  As vector loads (what the compiler emits for pointers it cannot
+// prove read-only), the wait for them would, vmcnt being in order, also wait
+// for every prefetch issued before -- draining the entry loads of the next
+// chunk right after issuing them.
+__device__ __forceinline__ void sload2(const int64_t *a, const int64_t *b, int64_t &x, int64_t &y) {
+    asm volatile(
+        "s_load_dwordx2 %0, %2, 0x0\n\t"
+        "s_load_dwordx2 %1, %3, 0x0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(x), "=&s"(y)
+        : "s"(a), "s"(b)
+        : "memory");
+}
+
+__device__ __forceinline__ void sload3(const int64_t *a, const int64_t *b, const int64_t *c,
+                                       int64_t &x, int64_t &y, int64_t &z) {
+    asm volatile(
+        "s_load_dwordx2 %0, %3, 0x0\n\t"
+        "s_load_dwordx2 %1, %4, 0x0\n\t"
+        "s_load_dwordx2 %2, %5, 0x0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(x), "=&s"(y), "=&s"(z)
+        : "s"(a), "s"(b), "s"(c)
+        : "memory");
+}
+
 // A segment's first round trip: slice depths D_q (uniform) and each lane's
 // running count per live slice (inclusive prefix over the slice's rows).
 struct SegHead {
@@ -94,9 +121,8 @@ struct SegHead {
         // Straight-line, unconditional vector loads (a dead slice reads the next
         // group of counts, ignored), so the compiler can count them in vmcnt.
         (void)live;
-        const int64_t info = M.seg_info[seg];
-        int64_t co = M.cnt_off[seg];
-        e0 = M.ent_off[seg];
+        int64_t info, co;
+        sload3(M.seg_info + seg, M.cnt_off + seg, M.ent_off + seg, info, co, e0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             D[q] = (int)((info >> (16 * q)) & 0xFFFF);
@@ -243,16 +269,21 @@ __device__ __forceinline__ void panel_chunks(const bsls_panels &M, int64_t rb, i
     SegHead ha, hb;
     SegBody<MODE> ba, bb;
     // chunk c0's DMA goes first, so it overlaps the prologue's two round trips
-    panel_stage(tab, src + M.chunk_col[c0], (int)(M.chunk_col[c0 + 1] - M.chunk_col[c0]));
+    {
+        int64_t a, b;
+        sload2(M.chunk_col + c0, M.chunk_col + c0 + 1, a, b);
+        panel_stage(tab, src + a, (int)(b - a));
+    }
     ha.load(M, seg(c0), live);
     ba.load(M, ha);
     if (c0 + 1 < c1) hb.load(M, seg(c0 + 1), live);
     auto step = [&](int64_t c, const SegBody<MODE> &cur, SegHead &hn, SegBody<MODE> &bn,
                     SegHead &hn2) {
-        const int64_t col0 = M.chunk_col[c];
         if (c > c0) {
+            int64_t a, b;
+            sload2(M.chunk_col + c, M.chunk_col + c + 1, a, b);
             __syncthreads();
-            panel_stage(tab, src + col0, (int)(M.chunk_col[c + 1] - col0));
+            panel_stage(tab, src + a, (int)(b - a));
         }
         __syncthreads();
         // walk first: its long-row loads wait on vmcnt, which is in order, so
