@@ -108,6 +108,15 @@ __device__ __forceinline__ void sload3(const int64_t *a, const int64_t *b, const
         : "memory");
 }
 
+// An empty asm that "uses" the gathered values: every gather is issued before
+// it and none is sunk into the conditional adds after it (left alone, the
+// compiler moves each load under its lane predicate and waits on it there)
+__device__ __forceinline__ void pin8(double (&a)[8]) {
+    asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                 "+v"(a[6]), "+v"(a[7]));
+}
+__device__ __forceinline__ void pin8(double (&a)[2]) { asm volatile("" : "+v"(a[0]), "+v"(a[1])); }
+
 // A segment's first round trip: slice depths D_q (uniform) and each lane's
 // running count per live slice (inclusive prefix over the slice's rows).
 struct SegHead {
@@ -205,6 +214,7 @@ struct SegBody {
                 const uint32_t w = c2[q][k >> 1];
                 a[k] = tab[(k & 1) ? (w >> 16) : (w & 0xFFFFu)];
             }
+            pin8(a);
 #pragma unroll
             for (int k = 0; k < DBK; ++k) {
                 if (k < D[q]) {
@@ -236,13 +246,16 @@ struct SegBody {
                         if (MODE == 1) vv[k] = in ? val[i] : 0.0;
                     }
                 }
+                double a2[DBK];
+#pragma unroll
+                for (int k = 0; k < DBK; ++k) a2[k] = tab[cc[k]];
+                pin8(a2);
 #pragma unroll
                 for (int k = 0; k < DBK; ++k) {
-                    const double a2 = tab[cc[k]];
                     double t;
-                    if (MODE == 0) t = a2;
-                    else if (MODE == 1) t = vv[k] * a2;
-                    else t = sc[q] * a2;
+                    if (MODE == 0) t = a2[k];
+                    else if (MODE == 1) t = vv[k] * a2[k];
+                    else t = sc[q] * a2[k];
                     if (k0 + k < cnt[q]) s[q] += t;
                 }
             }

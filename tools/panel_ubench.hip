@@ -16,7 +16,7 @@ __global__ __launch_bounds__(1024) void k2_ko(bsls_panels M, const double *__res
                                               const double *__restrict__ colv,
                                               double *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
     const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, sc[4] = {0.0, 0.0, 0.0, 0.0};
     for (int q = 0; q < 4; ++q) {
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(1024) void k2_var(bsls_panels M, const double *__re
                                                const double *__restrict__ colv,
                                                double *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
     const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, sc[4] = {0.0, 0.0, 0.0, 0.0};
     for (int q = 0; q < 4; ++q) {
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(1024) void k2_trace(bsls_panels M, const double *__
                                                  const double *__restrict__ colv,
                                                  double *__restrict__ out, long long *T) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
     const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, sc[4] = {0.0, 0.0, 0.0, 0.0};
     for (int q = 0; q < 4; ++q) {
@@ -204,18 +204,23 @@ __global__ __launch_bounds__(1024) void k2_trace(bsls_panels M, const double *__
     auto seg = [&](int64_t c) { return seg0 + c * PANEL_WAVES; };
     SegHead ha, hb;
     SegBody<2> ba, bb;
-    panel_stage(lds, r + M.chunk_col[c0], (int)(M.chunk_col[c0 + 1] - M.chunk_col[c0]));
+    {
+        int64_t a, b;
+        sload2(M.chunk_col + c0, M.chunk_col + c0 + 1, a, b);
+        panel_stage(lds, r + a, (int)(b - a));
+    }
     ha.load(M, seg(c0), live);
     ba.load(M, ha);
     if (c0 + 1 < c1) hb.load(M, seg(c0 + 1), live);
     if (rec) t[1] = wall_clock64();
     int ti = 2;
     auto step = [&](int64_t c, const SegBody<2> &cur, SegHead &hn, SegBody<2> &bn, SegHead &hn2) {
-        const int64_t col0 = M.chunk_col[c];
         if (c > c0) {
+            int64_t a, b;
+            sload2(M.chunk_col + c, M.chunk_col + c + 1, a, b);
             __syncthreads();
             if (rec) t[ti++] = wall_clock64();
-            panel_stage(lds, r + col0, (int)(M.chunk_col[c + 1] - col0));
+            panel_stage(lds, r + a, (int)(b - a));
         } else if (rec) {
             t[ti++] = wall_clock64();
         }

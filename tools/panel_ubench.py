@@ -42,7 +42,10 @@ def main():
                                   out.data_ptr(), args.reps)
             print('  %-12s %8.1f us' % (nm, us))
             if v == 0:
-                print('     bit-exact vs SciPy:', np.array_equal(out.cpu().numpy(), want))
+                o = out.cpu().numpy()
+                bad = np.flatnonzero(o != want)
+                print('     bit-exact vs SciPy:', bad.size == 0, 'mismatches', bad.size,
+                      'first', bad[:5], 'max rel', float(np.max(np.abs(o - want) / (np.abs(want) + 1e-300))))
         T = torch.zeros(4096 * 64 + 4096 * 16 * 16, dtype=torch.int64, device='cuda')
         lib.panel_trace.restype = ctypes.c_int
         lib.panel_trace.argtypes = [ctypes.POINTER(_native.Panels), ctypes.c_void_p,

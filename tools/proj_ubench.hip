@@ -3,7 +3,7 @@
 //   0 full (same work as the product kernel)   1 no sort
 //   2 no lambda chain                          3 LDS stage in/out only
 //   4 regs in/out only (no sort, no lambda)    5 full, unpredicated LDS loads
-// Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC -I include -I <csrc> tools/proj_ubench.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -shared -fPIC -I include -I <csrc> tools/proj_ubench.hip
 #include "../block-simplex-least-squares_amd/csrc/proj.hip"
 
 namespace ub {
