@@ -117,6 +117,21 @@ __device__ __forceinline__ void pin8(double (&a)[8]) {
 }
 __device__ __forceinline__ void pin8(double (&a)[2]) { asm volatile("" : "+v"(a[0]), "+v"(a[1])); }
 
+__device__ __forceinline__ void sload5(const int64_t *a, const int64_t *b, const int64_t *c,
+                                       const int64_t *d, const int64_t *e, int64_t &x, int64_t &y,
+                                       int64_t &z, int64_t &u, int64_t &v) {
+    asm volatile(
+        "s_load_dwordx2 %0, %5, 0x0\n\t"
+        "s_load_dwordx2 %1, %6, 0x0\n\t"
+        "s_load_dwordx2 %2, %7, 0x0\n\t"
+        "s_load_dwordx2 %3, %8, 0x0\n\t"
+        "s_load_dwordx2 %4, %9, 0x0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(x), "=&s"(y), "=&s"(z), "=&s"(u), "=&s"(v)
+        : "s"(a), "s"(b), "s"(c), "s"(d), "s"(e)
+        : "memory");
+}
+
 // A segment's first round trip: slice depths D_q (uniform) and each lane's
 // running count per live slice (inclusive prefix over the slice's rows).
 struct SegHead {
@@ -125,13 +140,18 @@ struct SegHead {
     int64_t e0;
 
     __device__ __forceinline__ void load(const bsls_panels &M, int64_t seg, bool live) {
-        const int lane = lane_id();
         // seg is wave-uniform (padded panels have empty segments): scalar loads.
         // Straight-line, unconditional vector loads (a dead slice reads the next
         // group of counts, ignored), so the compiler can count them in vmcnt.
         (void)live;
         int64_t info, co;
         sload3(M.seg_info + seg, M.cnt_off + seg, M.ent_off + seg, info, co, e0);
+        load_counts(M, info, co);
+    }
+
+    // the vector half, from the segment's metadata (info, cnt_off)
+    __device__ __forceinline__ void load_counts(const bsls_panels &M, int64_t info, int64_t co) {
+        const int lane = lane_id();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             D[q] = (int)((info >> (16 * q)) & 0xFFFF);
@@ -290,21 +310,32 @@ __device__ __forceinline__ void panel_chunks(const bsls_panels &M, int64_t rb, i
     ha.load(M, seg(c0), live);
     ba.load(M, ha);
     if (c0 + 1 < c1) hb.load(M, seg(c0 + 1), live);
+    int64_t ca = 0, cb = 0;   // column bounds of the next chunk to stage
     auto step = [&](int64_t c, const SegBody<MODE> &cur, SegHead &hn, SegBody<MODE> &bn,
                     SegHead &hn2) {
         if (c > c0) {
-            int64_t a, b;
-            sload2(M.chunk_col + c, M.chunk_col + c + 1, a, b);
-            __syncthreads();
-            panel_stage(tab, src + a, (int)(b - a));
+            // barrier A: every wave is done reading the table (its LDS reads
+            // were consumed by its adds).  A bare s_barrier: __syncthreads'
+            // fence would also wait vmcnt(0), i.e. for the prefetch just issued.
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) (gfx9 encoding)
+            __builtin_amdgcn_s_barrier();
+            panel_stage(tab, src + ca, (int)(cb - ca));
         }
         __syncthreads();
         // walk first: its long-row loads wait on vmcnt, which is in order, so
         // no prefetch may be outstanding yet; the prefetch issued after it flies
-        // across the next barrier and DMA
+        // across the next barrier and DMA.  One scalar round trip per step:
+        // chunk c+2's segment metadata with chunk c+1's column bounds.
         if (live) cur.walk(M, tab, s, sc);
         if (c + 1 < c1) bn.load(M, hn);
-        if (c + 2 < c1) hn2.load(M, seg(c + 2), live);
+        {
+            const int64_t sg = seg(c + 2 < c1 ? c + 2 : c1 - 1);
+            const int64_t cn = c + 1 < c1 ? c + 1 : c;
+            int64_t info, co;
+            sload5(M.seg_info + sg, M.cnt_off + sg, M.ent_off + sg, M.chunk_col + cn,
+                   M.chunk_col + cn + 1, info, co, hn2.e0, ca, cb);
+            if (c + 2 < c1) hn2.load_counts(M, info, co);
+        }
     };
     for (int64_t c = c0; c < c1; c += 2) {
         step(c, ba, hb, bb, ha);
