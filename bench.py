@@ -8,10 +8,13 @@ A step = one full projected-BB iteration (python/BB.py:17-41 semantics, fused
 K2 -> K3 -> K1 on the device) over the whole problem, inputs resident in HBM.
 N = 1: config C3 (1M routes, 50k blocks, 100k links, 16M nnz, fp64).
 N > 1 (torchrun, one rank per GPU): weak scaling -- every rank owns a C3-sized
-column shard (1M routes) of an N x 1M-route problem whose m = N x 100k rows
-are shared; per iteration one RCCL all-reduce of the residual r (8 m bytes)
-and one of the four BB sums.  value = N x (iterations/s of the whole job),
-i.e. 1M-route-equivalent BB iterations per second.
+column shard (1M routes, 50k blocks, 16M nnz) of an N x 1M-route problem on
+the same 100k-link network (m stays 100k: more routes over one network, so
+every rank's shard has exactly the C3 shape); per iteration one RCCL
+all-reduce of the residual r (8 m = 800 kB) and one of the four BB sums.
+value = N x (iterations/s of the whole job), i.e. 1M-route-equivalent BB
+iterations per second.  BSLS_DIST_BACKEND=gloo rehearses the N > 1 path with
+several ranks on one GPU (RCCL refuses two ranks on one device).
 
 Early exits are disabled for timing: exactly K iterations run.
 """
@@ -144,16 +147,22 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    # (modulo: the gloo rehearsal puts several ranks on one GPU)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        backend = os.environ.get('BSLS_DIST_BACKEND', 'nccl')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
 
     from synthetic import make_shard, add_noise, SEED
     from device import BBEngine, DeviceCSR
     n_g, p_g, m_per, per_col = 1_000_000, 50_000, 100_000, 16
-    m = m_per * world
+    m = m_per   # weak scaling over routes: the network (rows) is shared, see the docstring
     sh = make_shard(n_g, p_g, m, per_col, seed=SEED, rank=rank)
     Ax = torch.from_numpy(sh['Ax']).cuda()
     if dist:

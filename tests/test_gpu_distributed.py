@@ -1,0 +1,107 @@
+"""Column-sharded BB (distributed.ShardedBB) over the real HIP stages.
+
+Two ranks share the one GPU of the test box (gloo moves the all-reduces through
+host memory: RCCL refuses two ranks on one device), plus one rank over RCCL
+(backend "nccl") so the collective path bench.py uses at N > 1 runs too.  Each
+rank builds a device BBEngine on its block-aligned column shard and drives the
+stages bsls_bb_stage(0..6) with the all-reduces between them; the concatenated
+iterates must follow the oracle's BB trajectory (python/BB.py semantics) to the
+north star's 1e-6 relative.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
+
+ITERS = 30
+CHECK = (1, 2, 7, 30)
+
+
+def _problem():
+    from synthetic import make_shard, add_noise
+    sh = make_shard(40_000, 2_000, 3_000, per_col=8, seed=33)
+    b = add_noise(sh['Ax'], 0.02, seed=33)
+    return sh, b
+
+
+def _run(rank, world, backend, port, out_q):
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    from device import BBEngine
+    from distributed import ShardedBB, partition_blocks, torch_all_reduce
+    if backend == 'nccl':
+        dist.init_process_group('nccl', rank=rank, world_size=world,
+                                device_id=torch.device('cuda', 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    sh, b = _problem()
+    sizes = sh['block_sizes']
+    bounds = partition_blocks(sizes, sizes.astype(np.float64), world)
+    xst = np.concatenate(([0], np.cumsum(sizes)))
+    c0, c1 = xst[bounds[rank]], xst[bounds[rank + 1]]
+    A_g = sh['A'][:, c0:c1].tocsr()
+    sz_g = sizes[bounds[rank]:bounds[rank + 1]]
+    x0 = np.zeros(c1 - c0)
+    x0[np.cumsum(sz_g) - 1] = 1.0
+    part = torch.from_numpy(A_g.dot(x0)).cuda()
+    dist.all_reduce(part)
+    target = part - torch.from_numpy(b).cuda()
+    eng = BBEngine(A_g, None, sz_g, options={'max_iter': 10 ** 9, 'opt_tol': 1e-30},
+                   early_exit=False, target=target)
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    drv = ShardedBB(eng, torch_all_reduce())
+    drv.prologue()
+    traj = {}
+    for i in range(1, ITERS + 1):
+        drv.iterate(i, 1)
+        if i in CHECK:
+            traj[i] = eng.current_z(i & 1).cpu().numpy().copy()
+    out_q.put((rank, traj))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(world, backend):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() % 500) + world
+    procs = [ctx.Process(target=_run, args=(r, world, backend, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return {i: np.concatenate([res[r][i] for r in range(world)]) for i in CHECK}
+
+
+def _check(got, orc):
+    sh, b = _problem()
+    ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], ITERS, record_every=1)
+    for i in CHECK:
+        d = np.max(np.abs(got[i] - ref[i])) / max(1.0, np.max(np.abs(ref[i])))
+        assert d < 1e-6, (i, d)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_sharded_bb_two_ranks_on_device(cuda, orc):
+    _check(_spawn(2, 'gloo'), orc)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_sharded_bb_rccl_one_rank(cuda, orc):
+    _check(_spawn(1, 'nccl'), orc)
