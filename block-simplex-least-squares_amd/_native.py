@@ -61,6 +61,30 @@ class BBProblem(ctypes.Structure):
                 ('early_exit', _i32), ('reserved', _i32)]
 
 
+class CSR(ctypes.Structure):
+    """Mirror of struct bsls_csr (include/bsls_hip.h)."""
+    _fields_ = [('rows', _i64), ('indptr', _vp), ('indices', _vp), ('data', _vp),
+                ('tiles', _vp), ('ntiles', _i64), ('group', _i64)]
+
+
+class XBBProblem(ctypes.Structure):
+    """Mirror of struct bsls_xbb_problem (include/bsls_hip.h)."""
+    _fields_ = [('m', _i64), ('n', _i64), ('nblocks', _i64), ('max_block', _i64),
+                ('ball', _i64), ('A', CSR), ('AT', CSR), ('neg_b', _vp), ('starts', _vp),
+                ('x', _vp), ('g', _vp), ('xn', _vp), ('gn', _vp), ('r', _vp), ('scal', _vp),
+                ('hist', _vp), ('hist_cap', _i64), ('proj_work', _vp), ('proj_work_bytes', _sz),
+                ('work', _vp), ('work_bytes', _sz), ('max_iter', _i64), ('opt_tol', _dbl),
+                ('prog_tol', _dbl), ('f_min', _dbl), ('has_fmin', _i64)]
+
+
+# x-space engine scal[] slots / modes / stop reasons (include/bsls_hip.h)
+(XS_MODE, XS_ITER, XS_F, XS_FOLD, XS_T, XS_TT, XS_REVERT, XS_GD, XS_DXDG, XS_DGDG, XS_STEPINF,
+ XS_SQ, XS_STOP, XS_ROUNDS, XS_BACKTRACKS) = range(15)
+XS_COUNT = 16
+XM_INIT, XM_STEP, XM_BACKTRACK, XM_STOPPED = range(4)
+XSTOP_MAXITER, XSTOP_OPT, XSTOP_PROG = 1, 2, 3
+
+
 _SIGS = {
     'bsls_proj_workspace_size': (_sz, [_i64, _i64, _i64]),
     'bsls_proj_multi_simplex': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
@@ -72,6 +96,10 @@ _SIGS = {
     'bsls_z2x': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     'bsls_n_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _int, _vp]),
     'bsls_nt_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    'bsls_xbb_workspace_size': (_sz, [_i64, _i64, _i64, _i64]),
+    'bsls_xbb_init': (_int, [ctypes.POINTER(XBBProblem), _vp]),
+    'bsls_xbb_rounds': (_int, [ctypes.POINTER(XBBProblem), _i64, _vp]),
+    'bsls_md_step': (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _dbl, _vp]),
     'bsls_quad_obj': (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     'bsls_line_search': (_int, [_vp, _dbl, _vp, _vp, _dbl, _vp, _vp, _vp, _i64, _vp, _vp]),
     'bsls_csr_plan_tiles': (_i64, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64]),

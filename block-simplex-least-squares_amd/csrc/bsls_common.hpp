@@ -174,6 +174,79 @@ __device__ bool last_of_sum(const double (&mine)[NV], double *partials, unsigned
     return true;
 }
 
+// last_block_sum with some slots reduced by max instead of sum (bit k of
+// MAXMASK): NaN-propagating max, fixed order like the sums.  `red` must hold
+// NV * (blockDim.x / 64) doubles.
+__device__ __forceinline__ double nan_max(double a, double b) {
+    return (b > a || b != b) ? b : a;
+}
+
+template <int NV, unsigned MAXMASK>
+__device__ __forceinline__ void block_reduce(double (&v)[NV], double *red) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        if ((MAXMASK >> k) & 1u) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v[k] = nan_max(v[k], __shfl_xor(v[k], o, WAVE));
+        } else {
+            v[k] = group_sum<WAVE>(v[k]);
+        }
+    }
+    const int w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[k * nw + w] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            double s = red[k * nw];
+            for (int i = 1; i < nw; ++i)
+                s = ((MAXMASK >> k) & 1u) ? nan_max(s, red[k * nw + i]) : s + red[k * nw + i];
+            v[k] = s;
+        }
+    }
+    __syncthreads();
+}
+
+template <int NV, unsigned MAXMASK>
+__device__ bool last_block_reduce(const double (&mine)[NV], double *partials, unsigned *tickets,
+                                  double (&tot)[NV], double *red) {
+    __shared__ int am_last_r;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            __hip_atomic_store(&partials[(size_t)blockIdx.x * NV + k], mine[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        am_last_r = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!am_last_r) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const double v = __hip_atomic_load(&partials[(size_t)i * NV + k], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            acc[k] = ((MAXMASK >> k) & 1u) ? nan_max(acc[k], v) : acc[k] + v;
+        }
+    }
+    block_reduce<NV, MAXMASK>(acc, red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) tot[k] = acc[k];
+        __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+}
+
 // numpy.minimum(v, 1.) then numpy.maximum(., 0.) (python/main.py:65):
 // NaN propagates, -0.0 is kept.
 __device__ __forceinline__ double clip01(double v) {

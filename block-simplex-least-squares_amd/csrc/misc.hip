@@ -216,6 +216,34 @@ __global__ __launch_bounds__(256) void md_kernel(double *__restrict__ x,
     }
 }
 
+// BATCH.solve_MD's update (python/BATCH.py:238-240) and
+// algorithm_utils.normalization (python/algorithm_utils.py:175-179):
+// y = x * exp((-t) * g) elementwise (y = x when g == NULL), then every block
+// [starts[b], end_b) divided by its sum (x[s:e] / np.sum(x[s:e])).  Entries
+// before starts[0] get the elementwise update only.  One lane per block; the
+// block sum is sequential (NumPy's pairwise sum differs from it only in the
+// last bits for blocks >= 8, and np.exp is not correctly rounded either).
+__global__ __launch_bounds__(256) void md_step_kernel(const double *x,
+                                                      const double *__restrict__ g,
+                                                      double *y,
+                                                      const int64_t *__restrict__ starts,
+                                                      int64_t nb, int64_t n, double t) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const double mt = -t;
+    if (b == 0) {
+        for (int64_t i = 0; i < starts[0]; ++i) y[i] = g ? x[i] * exp(mt * g[i]) : x[i];
+    }
+    const int64_t s = starts[b], e = block_end(starts, nb, b, n);
+    double acc = 0.0;
+    for (int64_t i = s; i < e; ++i) {
+        const double v = g ? x[i] * exp(mt * g[i]) : x[i];
+        y[i] = v;
+        acc += v;
+    }
+    for (int64_t i = s; i < e; ++i) y[i] = y[i] / acc;
+}
+
 }  // namespace bsls
 
 using namespace bsls;
@@ -286,6 +314,16 @@ extern "C" int bsls_md_update(double *d_x, const double *d_g, const int64_t *d_s
     double *part = (double *)((char *)d_work + TICKET_BYTES);
     md_kernel<<<grid_for(nblocks, 256), 256, 0, (hipStream_t)stream>>>(
         d_x, d_g, d_starts, nblocks, n, step_scale, d_dxinf, part, ticket);
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" int bsls_md_step(const double *d_x, const double *d_g, double *d_y,
+                            const int64_t *d_starts, int64_t nblocks, int64_t n, double t,
+                            void *stream) {
+    if (nblocks <= 0 || n <= 0 || !d_x || !d_y || !d_starts) return BSLS_E_ARG;
+    md_step_kernel<<<grid_for(nblocks, 256), 256, 0, (hipStream_t)stream>>>(d_x, d_g, d_y, d_starts,
+                                                                            nblocks, n, t);
     BSLS_LAUNCH_CHECK();
     return BSLS_OK;
 }

@@ -250,8 +250,12 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
                                                       int64_t nb, int64_t n,
                                                       int64_t *__restrict__ big_list,
                                                       unsigned *__restrict__ big_count,
-                                                      int allow_big) {
+                                                      int allow_big,
+                                                      const double *__restrict__ gate) {
     __shared__ __attribute__((aligned(16))) double buf[PBUF];
+    // gated launch (the x-space BB engine, xbb.hip): run only when *gate == 1
+    // (its STEP mode); the big-block kernels then find an empty list too
+    if (gate && *gate != 1.0) return;
     const int lane = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * WAVE;
     const int64_t b = b0 + lane;
@@ -503,7 +507,8 @@ static ProjWork proj_layout(void *base, int64_t n, int64_t nb, int64_t max_block
 
 template <bool BALL>
 static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
-                       int64_t max_block, void *work, size_t work_bytes, hipStream_t st) {
+                       int64_t max_block, void *work, size_t work_bytes, hipStream_t st,
+                       const double *gate = nullptr) {
     if (nb <= 0 || n <= 0 || y == nullptr || starts == nullptr) return BSLS_E_ARG;
     if (max_block < 1) return BSLS_E_ARG;
     ProjWork w = proj_layout(work, n, nb, max_block);
@@ -513,7 +518,7 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
     // workspace size derived from it): otherwise no reset launch at all
     if (max_block > SMALL_MAX) BSLS_CHECK(hipMemsetAsync(w.count, 0, 16, st));
     proj_lds_kernel<BALL><<<grid_for(nb, WAVE), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
-                                                                  max_block > SMALL_MAX);
+                                                                  max_block > SMALL_MAX, gate);
     BSLS_LAUNCH_CHECK();
     if (max_block > SMALL_MAX) {
         int64_t nbig = nb < (n / (SMALL_MAX + 1) + 1) ? nb : (n / (SMALL_MAX + 1) + 1);
@@ -533,6 +538,13 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
         BSLS_LAUNCH_CHECK();
     }
     return BSLS_OK;
+}
+
+int proj_launch_gated(bool ball, double *y, const int64_t *starts, int64_t nb, int64_t n,
+                      int64_t max_block, void *work, size_t work_bytes, hipStream_t st,
+                      const double *gate) {
+    return ball ? proj_launch<true>(y, starts, nb, n, max_block, work, work_bytes, st, gate)
+                : proj_launch<false>(y, starts, nb, n, max_block, work, work_bytes, st, gate);
 }
 
 }  // namespace bsls

@@ -1,0 +1,248 @@
+// xbb.hip -- fused x-space projected Barzilai-Borwein (BATCH.solve_BB,
+// python/BATCH.py:55-106) over the sparse least-squares objective
+// (algorithm_utils.sparse_least_squares_obj, python/algorithm_utils.py:88-94),
+// the block simplex / l1-ball projection and the backtracking line search
+// line_search_np (:113-137), with the stopping rule algorithm_utils.stopping
+// (:158-172) -- every decision on the device.
+//
+// A round (bsls_xbb_rounds) is five launches:
+//   xbb_step    mode STEP:      x <- x_new, g <- g_new (the accepted point),
+//                               x_new = x + (-t) g        (np.add(x, -t*g, x_new))
+//               mode BACKTRACK: x_new = (1-tt) x + tt x_new, or x_new = x when
+//                               the step became too small (the reference's
+//                               revert: obj(x) then reproduces f and g exactly,
+//                               every kernel here being deterministic)
+//               mode INIT:      x_new = x_init
+//   proj        gated on STEP:  proj_multi_simplex / proj_multi_ball on x_new
+//   spmv A      r = A x_new - b, ||r||^2
+//   spmv A'     g_new = A' r
+//   xbb_finish  g.(x_new - x), dx.dg, dg.dg, ||dx||_inf (deterministic
+//               last-workgroup reduction), then the Armijo test
+//               f_new > f + 1e-4 g.(x_new - x): reject -> next round
+//               BACKTRACK (tt *= .8), else accept (f_old = f, f = f_new, the
+//               BB step for the next iteration, i += 1) and the stopping test.
+// After the stop every launch returns at once (the SpMVs recompute the same
+// values), and the final iterate is x_new / g_new.
+//
+// Bytes per STEP round (n routes, m rows, nnz): step 40 n, projection 16 n,
+// the two SpMVs 24 nnz + 4 (m + n) + 8 (m + n) + 16 m, finish 32 n.
+#include "bsls_common.hpp"
+
+namespace bsls {
+
+int proj_launch_gated(bool ball, double *y, const int64_t *starts, int64_t nb, int64_t n,
+                      int64_t max_block, void *work, size_t work_bytes, hipStream_t st,
+                      const double *gate);
+
+constexpr int XT = 256;
+constexpr int XGRID = 1024;   // finish: partials per launch (one slot per workgroup)
+
+static size_t xalign(size_t v) { return (v + 255) & ~(size_t)255; }
+
+__global__ __launch_bounds__(64) void xbb_init_kernel(double *scal, double *hist,
+                                                      int64_t hist_cap) {
+    const int t = threadIdx.x;
+    if (t < BSLS_XS_COUNT) scal[t] = 0.0;
+    if (t == 0) {
+        scal[BSLS_XS_MODE] = BSLS_XM_INIT;
+        scal[BSLS_XS_TT] = 1.0;
+        scal[BSLS_XS_T] = 1.0;
+    }
+    (void)hist;
+    (void)hist_cap;
+}
+
+__global__ __launch_bounds__(XT) void xbb_step_kernel(double *__restrict__ x,
+                                                      double *__restrict__ g,
+                                                      double *__restrict__ xn,
+                                                      const double *__restrict__ gn, int64_t n,
+                                                      const double *__restrict__ scal) {
+    const int mode = (int)scal[BSLS_XS_MODE];
+    if (mode == BSLS_XM_STOPPED) return;
+    const int64_t stride = (int64_t)gridDim.x * XT;
+    int64_t i = (int64_t)blockIdx.x * XT + threadIdx.x;
+    if (mode == BSLS_XM_INIT) {
+        for (; i < n; i += stride) xn[i] = x[i];
+    } else if (mode == BSLS_XM_STEP) {
+        const double mt = -scal[BSLS_XS_T];   // i == 1: t = 1, (-1) * g == -g exactly
+        for (; i < n; i += stride) {
+            const double xv = xn[i], gv = gn[i];
+            x[i] = xv;
+            g[i] = gv;
+            const double d = mt * gv;
+            xn[i] = xv + d;
+        }
+    } else {   // BACKTRACK (algorithm_utils.py:124-135)
+        if (scal[BSLS_XS_REVERT] != 0.0) {
+            for (; i < n; i += stride) xn[i] = x[i];
+        } else {
+            const double tt = scal[BSLS_XS_TT];
+            const double om = 1.0 - tt;
+            for (; i < n; i += stride) {
+                const double a = om * x[i];
+                const double b = tt * xn[i];
+                xn[i] = a + b;
+            }
+        }
+    }
+}
+
+// algorithm_utils.stopping (:158-172): every test runs, the last true one names
+// the reason.
+__device__ __forceinline__ int xstop(double i, double max_iter, double f, double f_old,
+                                     double opt_tol, double prog_tol, double f_min,
+                                     int has_fmin) {
+    int reason = 0;
+    if (i == max_iter) reason = BSLS_XSTOP_MAXITER;
+    if (has_fmin && f - f_min < opt_tol) reason = BSLS_XSTOP_OPT;
+    if (fabs(f_old - f) < prog_tol) reason = BSLS_XSTOP_PROG;
+    return reason;
+}
+
+__global__ __launch_bounds__(XT) void xbb_finish_kernel(
+    const double *__restrict__ x, const double *__restrict__ g, const double *__restrict__ xn,
+    const double *__restrict__ gn, int64_t n, double *__restrict__ scal,
+    double *__restrict__ hist, int64_t hist_cap, double max_iter, double opt_tol,
+    double prog_tol, double f_min, int has_fmin, double *__restrict__ part,
+    unsigned *__restrict__ ticket) {
+    __shared__ double red[4 * XT / WAVE];
+    const int mode = (int)scal[BSLS_XS_MODE];
+    if (mode == BSLS_XM_STOPPED) return;
+    // gd = g.(x_new - x), dx.dg, dg.dg, ||dx||_inf
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    if (mode != BSLS_XM_INIT) {
+        const int64_t stride = (int64_t)gridDim.x * XT;
+        for (int64_t i = (int64_t)blockIdx.x * XT + threadIdx.x; i < n; i += stride) {
+            const double gv = g[i];
+            const double dx = xn[i] - x[i];
+            const double dg = gn[i] - gv;
+            v[0] += gv * dx;
+            v[1] += dx * dg;
+            v[2] += dg * dg;
+            v[3] = nan_max(v[3], fabs(dx));
+        }
+    }
+    block_reduce<4, 8u>(v, red);
+    double tot[4];
+    if (!last_block_reduce<4, 8u>(v, part, ticket, tot, red)) return;
+    if (threadIdx.x != 0) return;
+    const double f_new = .5 * scal[BSLS_XS_SQ];          // .5 * tmp.T.dot(tmp)
+    scal[BSLS_XS_ROUNDS] += 1.0;
+    if (mode == BSLS_XM_INIT) {                          // f = obj(x, g); i = 1
+        scal[BSLS_XS_F] = f_new;
+        scal[BSLS_XS_FOLD] = INFINITY;
+        scal[BSLS_XS_ITER] = 1.0;
+        scal[BSLS_XS_T] = 1.0;
+        scal[BSLS_XS_TT] = 1.0;
+        if (hist_cap > 0) hist[0] = f_new;
+        const int r = xstop(1.0, max_iter, f_new, INFINITY, opt_tol, prog_tol, f_min, has_fmin);
+        scal[BSLS_XS_STOP] = r;
+        scal[BSLS_XS_MODE] = r ? BSLS_XM_STOPPED : BSLS_XM_STEP;
+        return;
+    }
+    const double f = scal[BSLS_XS_F];
+    scal[BSLS_XS_GD] = tot[0];
+    scal[BSLS_XS_STEPINF] = tot[3];
+    const double upper = f + 1e-4 * tot[0];               // f + suffDec * g.dot(x_new - x)
+    if (f_new > upper) {                                  // while f_new > upper_line
+        scal[BSLS_XS_BACKTRACKS] += 1.0;
+        scal[BSLS_XS_TT] = scal[BSLS_XS_TT] * .8;         // t *= .8
+        scal[BSLS_XS_REVERT] = (tot[3] < 1e-12) ? 1.0 : 0.0;   // step < progTol
+        scal[BSLS_XS_MODE] = BSLS_XM_BACKTRACK;
+        return;
+    }
+    // accept: f_old = f; f = f_new; delta_x, delta_g; i += 1 (BATCH.py:99-104)
+    const double it = scal[BSLS_XS_ITER] + 1.0;
+    scal[BSLS_XS_FOLD] = f;
+    scal[BSLS_XS_F] = f_new;
+    scal[BSLS_XS_DXDG] = tot[1];
+    scal[BSLS_XS_DGDG] = tot[2];
+    scal[BSLS_XS_T] = tot[1] / tot[2];                    // delta_x.T.dot(delta_g) / ...
+    scal[BSLS_XS_TT] = 1.0;
+    scal[BSLS_XS_REVERT] = 0.0;
+    scal[BSLS_XS_ITER] = it;
+    const int64_t k = (int64_t)it - 1;
+    if (k < hist_cap) hist[k] = f_new;
+    const int r = xstop(it, max_iter, f_new, f, opt_tol, prog_tol, f_min, has_fmin);
+    scal[BSLS_XS_STOP] = r;
+    scal[BSLS_XS_MODE] = r ? BSLS_XM_STOPPED : BSLS_XM_STEP;
+}
+
+struct XWork {
+    void *spmv;
+    size_t spmv_bytes;
+    unsigned *ticket;
+    double *part;
+    size_t bytes;
+};
+
+static XWork xwork(void *base, int64_t A_ntiles) {
+    XWork w{};
+    char *p = (char *)base;
+    size_t off = 0;
+    w.spmv = p + off;
+    w.spmv_bytes = bsls_spmv_workspace_size(A_ntiles);
+    off += xalign(w.spmv_bytes);
+    w.ticket = (unsigned *)(p + off);
+    off += xalign(TICKET_BYTES);
+    w.part = (double *)(p + off);
+    off += xalign((size_t)XGRID * 4 * sizeof(double));
+    w.bytes = off;
+    return w;
+}
+
+static int xgrid(int64_t n) {
+    const int64_t g = (n + XT - 1) / XT;
+    return (int)(g < 1 ? 1 : (g > XGRID ? XGRID : g));
+}
+
+}  // namespace bsls
+
+using namespace bsls;
+
+extern "C" size_t bsls_xbb_workspace_size(int64_t m, int64_t n, int64_t A_ntiles,
+                                          int64_t AT_ntiles) {
+    (void)m;
+    (void)n;
+    (void)AT_ntiles;
+    return xwork(nullptr, A_ntiles).bytes;
+}
+
+extern "C" int bsls_xbb_init(const bsls_xbb_problem *p, void *stream) {
+    if (!p || !p->scal) return BSLS_E_ARG;
+    xbb_init_kernel<<<1, 64, 0, (hipStream_t)stream>>>(p->scal, p->hist, p->hist_cap);
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *stream) {
+    if (!p || p->n <= 0 || p->m <= 0 || p->nblocks <= 0 || !p->x || !p->g || !p->xn || !p->gn ||
+        !p->r || !p->scal || !p->neg_b || !p->starts || count < 0)
+        return BSLS_E_ARG;
+    if (p->A.rows != p->m || p->AT.rows != p->n) return BSLS_E_ARG;
+    XWork w = xwork(p->work, p->A.ntiles);
+    if (!p->work || p->work_bytes < w.bytes) return BSLS_E_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    const int gs = xgrid(p->n);
+    for (int64_t c = 0; c < count; ++c) {
+        xbb_step_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal);
+        BSLS_LAUNCH_CHECK();
+        int rc = proj_launch_gated(p->ball != 0, p->xn, p->starts, p->nblocks, p->n, p->max_block,
+                                   p->proj_work, p->proj_work_bytes, st, p->scal + BSLS_XS_MODE);
+        if (rc != BSLS_OK) return rc;
+        rc = bsls_csr_spmv(p->m, p->A.indptr, p->A.indices, p->A.data, p->A.tiles, p->A.ntiles,
+                           p->xn, p->neg_b, 1.0, p->r, p->scal + BSLS_XS_SQ, (int)p->A.group,
+                           w.spmv, w.spmv_bytes, stream);
+        if (rc != BSLS_OK) return rc;
+        rc = bsls_csr_spmv(p->n, p->AT.indptr, p->AT.indices, p->AT.data, p->AT.tiles,
+                           p->AT.ntiles, p->r, nullptr, 1.0, p->gn, nullptr, (int)p->AT.group,
+                           nullptr, 0, stream);
+        if (rc != BSLS_OK) return rc;
+        xbb_finish_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal, p->hist,
+                                             p->hist_cap, (double)p->max_iter, p->opt_tol,
+                                             p->prog_tol, p->f_min, (int)p->has_fmin, w.part,
+                                             w.ticket);
+        BSLS_LAUNCH_CHECK();
+    }
+    return BSLS_OK;
+}

@@ -538,3 +538,105 @@ class BBEngine:
     def run_fixed(self, iters):
         """Enqueue exactly `iters` iterations (no host sync, no logging)."""
         self.iterate(1, iters)
+
+
+class XBBEngine:
+    """Fused x-space projected BB (python/BATCH.py:55-106 over
+    algorithm_utils.get_solver_parts(is_sparse=True), python/algorithm_utils.py:
+    182-271): the step, projection, objective, Armijo backtracking
+    (line_search_np, :113-137) and stopping test (:158-172) run as device rounds
+    (csrc/xbb.hip, bsls_xbb_rounds); the host polls the mode every `poll`
+    rounds."""
+
+    def __init__(self, obj, proj, A_dev=None):
+        torch = _torch()
+        L = _native.lib()
+        self.obj, self.proj = obj, proj
+        m, n = obj.m, obj.n
+        if proj.n != n:
+            raise ValueError('projection covers %d entries, A has %d columns' % (proj.n, n))
+        dev = dict(dtype=torch.float64, device='cuda')
+        self.m, self.n = m, n
+        self.x = torch.zeros(n, **dev)
+        self.g = torch.zeros(n, **dev)
+        self.xn = torch.zeros(n, **dev)
+        self.gn = torch.zeros(n, **dev)
+        self.r = torch.zeros(m, **dev)
+        self.scal = torch.zeros(_native.XS_COUNT, **dev)
+        self.work = torch.zeros(L.bsls_xbb_workspace_size(m, n, obj.A.ntiles, obj.AT.ntiles),
+                                dtype=torch.uint8, device='cuda')
+        self.hist = None
+        P = _native.XBBProblem()
+        P.m, P.n, P.nblocks, P.max_block = m, n, proj.p, proj.max_block
+        P.ball = 1 if proj.kind == 'ball' else 0
+        for dst, M in ((P.A, obj.A), (P.AT, obj.AT)):
+            dst.rows = M.m
+            dst.indptr, dst.indices, dst.data = (M.indptr.data_ptr(), M.indices.data_ptr(),
+                                                 M.data.data_ptr())
+            dst.tiles, dst.ntiles, dst.group = M.tiles.data_ptr(), M.ntiles, M.group
+        P.neg_b = obj.neg_b.data_ptr()
+        P.starts = proj.starts.data_ptr()
+        P.x, P.g, P.xn, P.gn = (self.x.data_ptr(), self.g.data_ptr(), self.xn.data_ptr(),
+                                self.gn.data_ptr())
+        P.r, P.scal = self.r.data_ptr(), self.scal.data_ptr()
+        P.proj_work, P.proj_work_bytes = proj.ws.data_ptr(), proj.ws.numel()
+        P.work, P.work_bytes = self.work.data_ptr(), self.work.numel()
+        self.P = P
+
+    def start(self, x_init, f_min=None, opt_tol=1e-6, max_iter=2000, prog_tol=1e-12,
+              hist_cap=None):
+        torch = _torch()
+        x0 = torch.as_tensor(np.asarray(x_init, dtype=np.float64) if not hasattr(x_init, 'cpu')
+                             else x_init, dtype=torch.float64).cuda().reshape(-1)
+        if x0.numel() != self.n:
+            raise ValueError('x_init has %d entries, expected %d' % (x0.numel(), self.n))
+        self.x.copy_(x0)
+        cap = int(hist_cap if hist_cap is not None else min(max(int(max_iter), 1) + 1, 1 << 22))
+        if self.hist is None or self.hist.numel() < cap:
+            self.hist = torch.zeros(cap, dtype=torch.float64, device='cuda')
+        P = self.P
+        P.hist, P.hist_cap = self.hist.data_ptr(), cap
+        P.max_iter = int(min(max_iter, 2 ** 62))
+        P.opt_tol, P.prog_tol = float(opt_tol), float(prog_tol)
+        P.has_fmin = 0 if f_min is None else 1
+        P.f_min = 0.0 if f_min is None else float(f_min)
+        self.f_min = f_min
+        check(_native.lib().bsls_xbb_init(P, stream_handle()), 'bsls_xbb_init')
+
+    def rounds(self, count):
+        check(_native.lib().bsls_xbb_rounds(self.P, int(count), stream_handle()),
+              'bsls_xbb_rounds')
+
+    def scalars(self):
+        return self.scal.cpu().numpy()
+
+    def solve(self, x_init, f_min=None, opt_tol=1e-6, max_iter=2000, prog_tol=1e-12, poll=8):
+        """BATCH.solve_BB's result dict: f, x (NumPy), stop, iterations, progress
+        ([time, f] per iteration; the time is the wall clock of the poll that
+        saw the iteration finish), plus rounds / backtracks."""
+        self.start(x_init, f_min, opt_tol, max_iter, prog_tol)
+        t0 = time.time()
+        seen, times = 0, [0.0]
+        while True:
+            self.rounds(poll)
+            s = self.scalars()
+            it = int(s[_native.XS_ITER])
+            now = time.time() - t0
+            times.extend([now] * max(0, it - 1 - seen))
+            seen = max(seen, it - 1)
+            if int(s[_native.XS_MODE]) == _native.XM_STOPPED:
+                break
+        f, f_old = float(s[_native.XS_F]), float(s[_native.XS_FOLD])
+        reason = int(s[_native.XS_STOP])
+        if reason == _native.XSTOP_MAXITER:
+            stop = 'max_iter'
+        elif reason == _native.XSTOP_OPT:
+            stop = 'f-f_min = {} < opt_tol'.format(f - f_min)
+        else:
+            stop = '|f_old-f| = {} < prog_tol'.format(abs(f_old - f))
+        k = min(it, self.P.hist_cap)
+        fh = self.hist[:k].cpu().numpy()
+        progress = [[times[j] if j < len(times) else times[-1], float(fh[j])] for j in range(k)]
+        return {'f': f, 'x': self.xn.cpu().numpy(), 'stop': stop, 'iterations': it,
+                'progress': progress, 'rounds': int(s[_native.XS_ROUNDS]),
+                'backtracks': int(s[_native.XS_BACKTRACKS])}

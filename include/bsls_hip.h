@@ -229,6 +229,76 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  * bsls_bb_iterate runs 3, 4, 7. */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 
+/* ---- fused x-space Barzilai-Borwein engine ----------------------------------
+ * Replaces BATCH.solve_BB (python/BATCH.py:55-106) over the closures of
+ * algorithm_utils.get_solver_parts(is_sparse=True) (python/algorithm_utils.py:
+ * 182-271): obj = sparse_least_squares_obj (:88-94), proj = proj_multi_simplex
+ * / proj_multi_ball, line_search = line_search_np (:113-137), and the stopping
+ * rule algorithm_utils.stopping (:158-172).
+ * The device runs ROUNDS; a round is either one BB step (x_new = proj(x - t g),
+ * obj(x_new), Armijo test) or one backtracking step of the line search
+ * (x_new = (1-tt) x + tt x_new, obj(x_new), test) -- which one is decided on
+ * the device, so the host only enqueues rounds (5 launches each) and polls
+ * scal[XS_MODE] for BSLS_XM_STOPPED.  Rounds after the stop are no-ops.
+ * scal[] layout: BSLS_XS_*; hist[k] = f after iteration k (hist[0] = f(x0)),
+ * the reference's progress[k][1], for k < hist_cap. */
+enum {
+    BSLS_XS_MODE = 0,      /* BSLS_XM_* of the next round */
+    BSLS_XS_ITER = 1,      /* the reference's i */
+    BSLS_XS_F = 2,         /* f at x */
+    BSLS_XS_FOLD = 3,      /* f_old */
+    BSLS_XS_T = 4,         /* BB step of the next STEP round */
+    BSLS_XS_TT = 5,        /* line-search t of the next BACKTRACK round */
+    BSLS_XS_REVERT = 6,    /* 1: the next BACKTRACK round restores x (step too small) */
+    BSLS_XS_GD = 7,        /* g . (x_new - x) of the last round */
+    BSLS_XS_DXDG = 8,      /* delta_x . delta_g of the last accepted step */
+    BSLS_XS_DGDG = 9,      /* delta_g . delta_g of the last accepted step */
+    BSLS_XS_STEPINF = 10,  /* ||x_new - x||_inf of the last round */
+    BSLS_XS_SQ = 11,       /* ||A x_new - b||^2 of the last round */
+    BSLS_XS_STOP = 12,     /* BSLS_XSTOP_* (the LAST matching test, like the reference) */
+    BSLS_XS_ROUNDS = 13,   /* rounds run */
+    BSLS_XS_BACKTRACKS = 14,
+    BSLS_XS_COUNT = 16
+};
+enum { BSLS_XM_INIT = 0, BSLS_XM_STEP = 1, BSLS_XM_BACKTRACK = 2, BSLS_XM_STOPPED = 3 };
+enum { BSLS_XSTOP_MAXITER = 1, BSLS_XSTOP_OPT = 2, BSLS_XSTOP_PROG = 3 };
+
+typedef struct bsls_csr {           /* a CSR matrix for bsls_csr_spmv */
+    int64_t rows;
+    const int64_t *indptr;
+    const int32_t *indices;
+    const double *data;
+    const int64_t *tiles;           /* bsls_csr_plan_tiles */
+    int64_t ntiles;
+    int64_t group;
+} bsls_csr;
+
+typedef struct bsls_xbb_problem {
+    int64_t m, n, nblocks, max_block;
+    int64_t ball;                   /* 0: proj_multi_simplex, 1: proj_multi_ball */
+    bsls_csr A, AT;                 /* A (m x n) and A' (n x m), explicit */
+    const double *neg_b;            /* m: -b */
+    const int64_t *starts;          /* nblocks block starts (strictly increasing) */
+    double *x, *g, *xn, *gn;        /* n each: iterate, gradient, trial point, its gradient */
+    double *r;                      /* m */
+    double *scal;                   /* BSLS_XS_COUNT */
+    double *hist;                   /* hist_cap */
+    int64_t hist_cap;
+    void *proj_work;                /* bsls_proj_workspace_size(n, nblocks, max_block) */
+    size_t proj_work_bytes;
+    void *work;                     /* bsls_xbb_workspace_size() bytes, zeroed once */
+    size_t work_bytes;
+    int64_t max_iter;
+    double opt_tol, prog_tol, f_min;
+    int64_t has_fmin;
+} bsls_xbb_problem;
+
+size_t bsls_xbb_workspace_size(int64_t m, int64_t n, int64_t A_ntiles, int64_t AT_ntiles);
+/* x must hold x_init; resets scal (mode INIT) and the reduction tickets. */
+int bsls_xbb_init(const bsls_xbb_problem *p, void *stream);
+/* Enqueue `count` rounds (the first one after init evaluates obj(x_init)). */
+int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *stream);
+
 /* ---- mirror descent ---------------------------------------------------------
  * Replaces mirror_descent.least_squares's step (python/mirror_descent.py:37-47):
  * x <- x * exp(-t_k g) per coordinate, t_k = sqrt(2 ln k_b)/(sqrt(k) Lf), then
@@ -238,6 +308,14 @@ int bsls_md_update(double *d_x, const double *d_g, const int64_t *d_starts, int6
                    int64_t n, double step_scale, double *d_dxinf, void *d_work,
                    size_t work_bytes, void *stream);
 size_t bsls_md_workspace_size(int64_t nblocks);
+
+/* Replaces BATCH.solve_MD's update (python/BATCH.py:238-240) and
+ * algorithm_utils.normalization (python/algorithm_utils.py:175-179):
+ * d_y = d_x * exp(-t d_g) (d_y = d_x when d_g is NULL), then every block
+ * [starts[b], starts[b+1]) (last block to n) divided by its sum.  d_y may
+ * alias d_x. */
+int bsls_md_step(const double *d_x, const double *d_g, double *d_y, const int64_t *d_starts,
+                 int64_t nblocks, int64_t n, double t, void *stream);
 
 /* Library / device info (for the loader's self-check). */
 const char *bsls_version(void);

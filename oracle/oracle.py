@@ -18,6 +18,10 @@ Contents
       md_least_squares    python/mirror_descent.py:7-53
       solve_in_z_parts    python/main.py:41-65 (f, nabla_f, proj closures)
       lsv_operator        python/bsls_utils.py:334-369
+      batch_solve_bb      python/BATCH.py:55-106 over algorithm_utils.get_solver_parts
+                          (is_sparse=True), line_search_np, stopping
+                          (python/algorithm_utils.py:88-94,113-137,158-172,182-271)
+      batch_solve_md      python/BATCH.py:217-250 (+ normalization :175-179)
     SpMV inside them is SciPy csr_matvec, exactly what the reference calls.
 
 Parity status: pinned (tests/test_oracle_pinning.py checks every function
@@ -329,6 +333,113 @@ def bb_trace(A, b, block_sizes, iters, record_every=1, options=None):
     bb_solve(P['z0'], P['f'], P['nabla_f'], stopping, record_every=record_every,
              proj=P['proj'], log=log, options=opts)
     return rec
+
+
+def batch_stopping(i, max_iter, f, f_old, opt_tol, prog_tol, f_min=None):
+    """algorithm_utils.py:158-172."""
+    flag, stop = False, 'continue'
+    if i == max_iter:
+        stop, flag = 'max_iter', True
+    if f_min is not None and f - f_min < opt_tol:
+        stop, flag = 'f-f_min = {} < opt_tol'.format(f - f_min), True
+    if abs(f_old - f) < prog_tol:
+        stop, flag = '|f_old-f| = {} < prog_tol'.format(abs(f_old - f)), True
+    return flag, stop
+
+
+def sparse_parts(A, b, block_starts, lasso=False):
+    """get_solver_parts(data=(A, b), is_sparse=True, f=None) closures
+    (algorithm_utils.py:88-94,113-137,197-203,226-231,268-271)."""
+    A = sps.csr_matrix(A)
+    AT = sps.csr_matrix(A.T)
+    starts = np.asarray(block_starts, dtype=np.int64)
+
+    def obj(x, g):
+        tmp = A.dot(x) - b
+        np.copyto(g, AT.dot(tmp))
+        return .5 * tmp.T.dot(tmp)
+
+    def proj(x):
+        (proj_multi_ball_c if lasso else proj_multi_simplex_c)(x, starts)
+
+    def line_search(x, f, g, x_new, f_new, g_new, i):
+        t, suffDec, progTol = 1.0, 1e-4, 1e-12
+        upper_line = f + suffDec * g.dot(x_new - x)
+        while f_new > upper_line:
+            t *= .8
+            if la.norm(x_new - x, np.inf) < progTol:
+                f_new = f
+                np.copyto(g_new, g)
+                np.copyto(x_new, x)
+                break
+            np.copyto(x_new, (1.0 - t) * x + t * x_new)
+            f_new = obj(x_new, g_new)
+            upper_line = f + suffDec * g.dot(x_new - x)
+        return f_new
+    return obj, proj, line_search
+
+
+def batch_solve_bb(obj, proj, line_search, x_init, f_min=None, opt_tol=1e-6, max_iter=2000,
+                   prog_tol=1e-12):
+    """BATCH.py:55-106 (progress times dropped: [k, f])."""
+    n = x_init.shape[0]
+    x = np.copy(x_init)
+    g = np.zeros(n)
+    delta_x, delta_g = np.zeros(n), np.zeros(n)
+    g_new, x_new = np.zeros(n), np.zeros(n)
+    f_old = np.inf
+    i = 1
+    f = obj(x, g)
+    progress = [f]
+    while True:
+        flag, stop = batch_stopping(i, max_iter, f, f_old, opt_tol, prog_tol, f_min)
+        if flag:
+            break
+        if i == 1:
+            np.add(x, -g, x_new)
+        else:
+            t = delta_x.T.dot(delta_g) / delta_g.T.dot(delta_g)
+            np.add(x, -t * g, x_new)
+        proj(x_new)
+        f_new = obj(x_new, g_new)
+        f_new = line_search(x, f, g, x_new, f_new, g_new, i)
+        f_old, f = f, f_new
+        np.add(x_new, -x, delta_x)
+        np.add(g_new, -g, delta_g)
+        np.copyto(x, x_new)
+        np.copyto(g, g_new)
+        i += 1
+        progress.append(f)
+    return {'f': f, 'x': x, 'stop': stop, 'iterations': i, 'progress': np.array(progress)}
+
+
+def batch_solve_md(obj, block_starts, step_size, x_init, f_min=None, opt_tol=1e-6,
+                   max_iter=1000, prog_tol=0.0):
+    """BATCH.py:217-250 with normalization (algorithm_utils.py:175-179)."""
+    n = x_init.shape[0]
+    starts = np.asarray(block_starts)
+    ends = np.append(starts[1:], [n])
+    x = np.copy(x_init)
+    g, g_new, x_new = np.zeros(n), np.zeros(n), np.zeros(n)
+    f_old = np.inf
+    i = 1
+    f = obj(x, g)
+    progress = [f]
+    while True:
+        flag, stop = batch_stopping(i, max_iter, f, f_old, opt_tol, prog_tol, f_min)
+        if flag:
+            break
+        t = step_size(i)
+        np.copyto(x_new, x * np.exp(-t * g))
+        for s_, e_ in zip(starts, ends):
+            np.copyto(x_new[s_:e_], x_new[s_:e_] / np.sum(x_new[s_:e_]))
+        f_new = obj(x_new, g_new)
+        f_old, f = f, f_new
+        np.copyto(x, x_new)
+        np.copyto(g, g_new)
+        i += 1
+        progress.append(f)
+    return {'f': f, 'x': x, 'stop': stop, 'iterations': i, 'progress': np.array(progress)}
 
 
 def dore_solve(x0, linop, linop_T, target, record_every=5, proj=None, log=None,

@@ -332,12 +332,73 @@ def gen_solver_traces():
     np.savez_compressed(os.path.join(OUT, 'solvers.npz'), **out)
 
 
+def gen_batch_traces():
+    """x-space batch solvers (python/BATCH.py) over get_solver_parts
+    (python/algorithm_utils.py:182-271): sparse least squares with the block
+    simplex / l1-ball projection, and the dense 2-D QP of test_BATCH.py."""
+    from algorithm_utils import get_solver_parts
+    import BATCH as batch
+    from bsls_utils import generate_small_qp
+    out = {}
+    cases = [('s', SEED + 11, 3000, 150, 300, 16, 0.02, False),
+             ('c', SEED + 12, 1500, 60, 200, 8, 0.0, False),
+             ('l', SEED + 13, 2000, 100, 250, 8, 0.05, True)]
+    for tag, seed, n, p, m, pc, noise, lasso in cases:
+        A, b, xs, sizes = sparse_problem(seed, n, p, m, per_col=pc, noise=noise)
+        starts = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+        x_init = np.repeat(1.0 / sizes, sizes)
+        if lasso:
+            x_init = 0.5 * x_init
+        step_size, proj, line_search, obj = get_solver_parts((A, b), starts, 1.0,
+                                                            is_sparse=True, lasso=lasso)
+        for k in (2, 3, 6, 15, 40, 2000):
+            sol = batch.solve_BB(obj, proj, line_search, x_init.copy(), max_iter=k)
+            out['%s_bb%d_x' % (tag, k)] = sol['x']
+            out['%s_bb%d_f' % (tag, k)] = np.array(sol['f'])
+            out['%s_bb%d_it' % (tag, k)] = np.array(sol['iterations'])
+            out['%s_bb%d_stop' % (tag, k)] = np.array(sol['stop'])
+            out['%s_bb%d_prog' % (tag, k)] = np.array([q[1] for q in sol['progress']])
+        if not lasso:
+            # mirror descent over the same parts (BATCH.py:217-250); min_eig
+            # sized so that t g stays O(1) (A's entries are the flows, ~500)
+            md_step = get_solver_parts((A, b), starts, 1e8, is_sparse=True)[0]
+            for k in (2, 10, 50):
+                sol = batch.solve_MD(obj, starts, md_step, x_init.copy(), max_iter=k)
+                out['%s_md%d_x' % (tag, k)] = sol['x']
+                out['%s_md%d_prog' % (tag, k)] = np.array([q[1] for q in sol['progress']])
+        out['%s_A_data' % tag], out['%s_A_indices' % tag] = A.data, A.indices
+        out['%s_A_indptr' % tag], out['%s_A_shape' % tag] = A.indptr, np.array(A.shape)
+        out['%s_b' % tag], out['%s_starts' % tag] = b, starts
+        out['%s_x_init' % tag] = x_init
+    # dense 2-D QP of tests/fast/test_BATCH.py:24-40 (seeded like its setUp)
+    np.random.seed(SEED)
+    Q, c, x_true, f_min, min_eig = generate_small_qp()
+    step_size, proj, line_search, obj = get_solver_parts((Q, c), np.array([0]), min_eig)
+    for name, fn in (('gd', lambda: batch.solve(obj, proj, step_size, np.array([.5, .5]))),
+                     ('gdls', lambda: batch.solve(obj, proj, step_size, np.array([.5, .5]),
+                                                  line_search)),
+                     ('bb', lambda: batch.solve_BB(obj, proj, line_search, np.array([.5, .5]))),
+                     ('lbfgs', lambda: batch.solve_LBFGS(obj, proj, line_search,
+                                                        np.array([.5, .5])))):
+        sol = fn()
+        out['qp_%s_x' % name] = sol['x']
+        out['qp_%s_it' % name] = np.array(sol['iterations'])
+        out['qp_%s_stop' % name] = np.array(sol['stop'])
+    out['qp_Q'], out['qp_c'], out['qp_x_true'] = Q, c, x_true
+    out['qp_f_min'], out['qp_min_eig'] = np.array(f_min), np.array(min_eig)
+    np.savez_compressed(os.path.join(OUT, 'batch.npz'), **out)
+
+
 def main():
     prepare()
+    if len(sys.argv) > 1 and sys.argv[1] == 'batch':
+        gen_batch_traces()
+        return
     gen_projection_cases()
     gen_isotonic_cases()
     gen_xz_quad()
     gen_solver_traces()
+    gen_batch_traces()
     for f in sorted(os.listdir(OUT)):
         if f.endswith('.npz'):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -228,3 +228,25 @@ def test_panel_rows_choice():
     assert device.panel_rows(1_000_000, 256) == 245       # C3 K2: 256 workgroups
     assert device.panel_rows(10, 256) == 10
     assert device.panel_rows(10_000_000, 256) == 255
+
+
+def test_batch_stopping_matches_oracle(orc):
+    """algorithm_utils.stopping (python/algorithm_utils.py:158-172): the last
+    true test names the reason."""
+    from algorithm_utils import stopping
+    cases = [(5, 5, 1.0, 2.0, 1e-6, 1e-12, None), (3, 5, 1.0, 1.0, 1e-6, 1e-12, None),
+             (3, 5, 1.0, 2.0, 1e-6, 1e-12, 1.0 - 1e-9), (5, 5, 1.0, 1.0, 1e-6, 1e-12, 0.5),
+             (2, 5, 1.0, np.inf, 1e-6, 1e-12, None)]
+    for c in cases:
+        assert stopping(*c) == orc.batch_stopping(*c)
+
+
+def test_batch_modules_import_without_device():
+    import BATCH
+    import algorithm_utils
+    assert BATCH.solve_BB.__code__.co_varnames[:8] == ('obj', 'proj', 'line_search', 'x_init',
+                                                      'f_min', 'opt_tol', 'max_iter',
+                                                      'prog_tol')
+    with pytest.raises(RuntimeError):
+        algorithm_utils.get_solver_parts((sps.eye(4).tocsr(), np.ones(4)), np.array([0]), 1.0,
+                                         is_sparse=True)

@@ -290,3 +290,39 @@ def test_vs_ref_quad(orc):
             fr = R.ref_line_search(orc._pd(x), f1, orc._pd(g1), orc._pd(r_x), fn, orc._pd(r_g),
                                    orc._pd(Q), orc._pd(c), n)
             assert fa == fr and exact(a_x, r_x) and exact(a_g, r_g[:n])
+
+
+# ------------------------------------------------ x-space batch solvers
+
+def _batch_problem(golden, tag):
+    d = golden('batch.npz')
+    A = sps.csr_matrix((d['%s_A_data' % tag], d['%s_A_indices' % tag], d['%s_A_indptr' % tag]),
+                       shape=tuple(d['%s_A_shape' % tag]))
+    return d, A, d['%s_b' % tag], d['%s_starts' % tag], d['%s_x_init' % tag]
+
+
+@pytest.mark.parametrize('tag,lasso', [('s', False), ('c', False), ('l', True)])
+def test_golden_batch_solve_bb(orc, golden, tag, lasso):
+    """BATCH.solve_BB over get_solver_parts(is_sparse=True) (python/BATCH.py:55-106):
+    the restatement reproduces the reference bit for bit (same SciPy SpMV, same
+    projection arithmetic, same NumPy reductions)."""
+    d, A, b, starts, x0 = _batch_problem(golden, tag)
+    obj, proj, ls = orc.sparse_parts(A, b, starts, lasso=lasso)
+    for k in (2, 3, 6, 15, 40):
+        sol = orc.batch_solve_bb(obj, proj, ls, x0.copy(), max_iter=k)
+        assert exact(sol['x'], d['%s_bb%d_x' % (tag, k)]), (tag, k)
+        assert sol['iterations'] == int(d['%s_bb%d_it' % (tag, k)])
+        assert sol['stop'] == str(d['%s_bb%d_stop' % (tag, k)])
+        assert exact(sol['progress'], d['%s_bb%d_prog' % (tag, k)])
+
+
+@pytest.mark.parametrize('tag', ['s', 'c'])
+def test_golden_batch_solve_md(orc, golden, tag):
+    """BATCH.solve_MD (python/BATCH.py:217-250), decreasing_step_size(i, 1, 1e8)."""
+    d, A, b, starts, x0 = _batch_problem(golden, tag)
+    obj, _, _ = orc.sparse_parts(A, b, starts)
+    step = lambda i: 1.0 / (1e8 * i + 1.0)
+    for k in (2, 10, 50):
+        sol = orc.batch_solve_md(obj, starts, step, x0.copy(), max_iter=k)
+        assert exact(sol['x'], d['%s_md%d_x' % (tag, k)]), (tag, k)
+        assert exact(sol['progress'], d['%s_md%d_prog' % (tag, k)])
