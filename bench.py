@@ -132,6 +132,47 @@ def bench_proj(reps=50):
             'cpu_oracle_ms_1thread': cpu_s * 1e3, 'bit_exact_vs_oracle': ok}
 
 
+def bench_xspace(sh, b, rounds=40, reps=5):
+    """x-space BB (BATCH.solve_BB over get_solver_parts(is_sparse=True),
+    SURVEY.md §8 rows a14/f2) on the same C3 matrix with the block simplex
+    projection: device rounds (csrc/xbb.hip) over the panel operator
+    (csrc/lsq.hip).  A run converges (revert of a too-small step) after ~50
+    rounds, so each rep restarts from x0 and runs `rounds` rounds with
+    prog_tol < 0.  Reports rounds/s (a round = one BB step or one backtracking
+    step, each a full objective evaluation) and accepted iterations/s."""
+    import torch
+    from algorithm_utils import get_solver_parts
+    from device import XBBEngine
+    import _native
+    sizes = sh['block_sizes']
+    starts = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+    x0 = np.repeat(1.0 / sizes, sizes)
+    _, proj, _, obj = get_solver_parts((sh['A'], b), starts, 1.0, is_sparse=True)
+    eng = XBBEngine(obj, proj)
+    x0d = torch.from_numpy(x0).cuda()
+    eng.start(x0d, max_iter=10 ** 12, prog_tol=-1.0, hist_cap=1)
+    eng.rounds(rounds)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    its = bts = 0
+    ok = True
+    for k in range(reps):
+        eng.start(x0d, max_iter=10 ** 12, prog_tol=-1.0, hist_cap=1)
+        ev[2 * k].record()
+        eng.rounds(rounds)
+        ev[2 * k + 1].record()
+        s = eng.scalars()
+        its += int(s[_native.XS_ITER])
+        bts += int(s[_native.XS_BACKTRACKS])
+        ok = ok and bool(np.isfinite(s[_native.XS_F]))
+    torch.cuda.synchronize()
+    ms = sum(ev[2 * k].elapsed_time(ev[2 * k + 1]) for k in range(reps))
+    return {'operator': 'panels' if obj.lsq is not None else 'csr',
+            'rounds': rounds * reps, 'us_per_round': ms * 1e3 / (rounds * reps),
+            'rounds_per_s': rounds * reps / (ms * 1e-3), 'iterations_per_s': its / (ms * 1e-3),
+            'backtracks': bts, 'finite': ok}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -257,6 +298,7 @@ def main():
                     'frac': kern[dom]['frac'], 'traffic': traffic}
         ib = survey_iter_bytes(m, n_g * world, eng.nz * world, nnz * world)
         proj = bench_proj() if world == 1 else None
+        xspace = bench_xspace(sh, b) if world == 1 else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cps, cit, cel = cpu_baseline_bb(sh['A'], b, sh['block_sizes'])
@@ -278,7 +320,7 @@ def main():
             'iteration_roofline': {'survey_bytes_per_iter': ib,
                                    'achieved_GB_s': ib * it_s / 1e9,
                                    'frac': ib * it_s / HBM_PEAK},
-            'kernels': kern, 'proj_simplex': proj, 'cpu_baseline': cpu,
+            'kernels': kern, 'proj_simplex': proj, 'xspace_bb': xspace, 'cpu_baseline': cpu,
             'finite': finite,
         }
         print(json.dumps(out), flush=True)

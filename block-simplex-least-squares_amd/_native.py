@@ -67,6 +67,12 @@ class CSR(ctypes.Structure):
                 ('tiles', _vp), ('ntiles', _i64), ('group', _i64)]
 
 
+class LsqOp(ctypes.Structure):
+    """Mirror of struct bsls_lsq_op (include/bsls_hip.h)."""
+    _fields_ = [('m', _i64), ('n', _i64), ('A', Panels), ('AT', Panels), ('colv', _vp),
+                ('rpart', _vp), ('xs', _vp), ('work', _vp), ('work_bytes', _sz)]
+
+
 class XBBProblem(ctypes.Structure):
     """Mirror of struct bsls_xbb_problem (include/bsls_hip.h)."""
     _fields_ = [('m', _i64), ('n', _i64), ('nblocks', _i64), ('max_block', _i64),
@@ -74,7 +80,8 @@ class XBBProblem(ctypes.Structure):
                 ('x', _vp), ('g', _vp), ('xn', _vp), ('gn', _vp), ('r', _vp), ('scal', _vp),
                 ('hist', _vp), ('hist_cap', _i64), ('proj_work', _vp), ('proj_work_bytes', _sz),
                 ('work', _vp), ('work_bytes', _sz), ('max_iter', _i64), ('opt_tol', _dbl),
-                ('prog_tol', _dbl), ('f_min', _dbl), ('has_fmin', _i64)]
+                ('prog_tol', _dbl), ('f_min', _dbl), ('has_fmin', _i64),
+                ('lsq', ctypes.POINTER(LsqOp))]
 
 
 # x-space engine scal[] slots / modes / stop reasons (include/bsls_hip.h)
@@ -96,6 +103,9 @@ _SIGS = {
     'bsls_z2x': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     'bsls_n_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _int, _vp]),
     'bsls_nt_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    'bsls_lsq_workspace_size': (_sz, [_i64, _i64]),
+    'bsls_lsq_residual': (_int, [ctypes.POINTER(LsqOp), _vp, _vp, _vp, _vp, _vp]),
+    'bsls_lsq_gradient': (_int, [ctypes.POINTER(LsqOp), _vp, _vp, _vp]),
     'bsls_xbb_workspace_size': (_sz, [_i64, _i64, _i64, _i64]),
     'bsls_xbb_init': (_int, [ctypes.POINTER(XBBProblem), _vp]),
     'bsls_xbb_rounds': (_int, [ctypes.POINTER(XBBProblem), _i64, _vp]),

@@ -126,16 +126,27 @@ def proj_multi_simplex(y, blocks):
 
 class SparseLSQ:
     """sparse_least_squares_obj (algorithm_utils.py:88-94) over device CSR:
-    tmp = A x - b; g = A' tmp; f = .5 tmp.tmp."""
+    tmp = A x - b; g = A' tmp; f = .5 tmp.tmp.
 
-    def __init__(self, A, b, A_T=None):
-        from device import DeviceCSR
+    `panels`: also build the panel images (device.DeviceLSQ, csrc/lsq.hip) and
+    run both products on them -- the default from PANEL_MIN_NNZ nonzeros up.
+    g is bit-identical either way; tmp differs from SciPy's row order by
+    <= 1e-12 relative on the panel path (8 column-group partials)."""
+
+    PANEL_MIN_NNZ = 1 << 20
+
+    def __init__(self, A, b, A_T=None, panels=None):
+        from device import DeviceCSR, DeviceLSQ
         torch = _torch()
         A = sps.csr_matrix(A)
         self.A_host = A
         self.m, self.n = A.shape
+        AT = sps.csr_matrix(A_T) if A_T is not None else A.T.tocsr()
         self.A = DeviceCSR(A)
-        self.AT = DeviceCSR(sps.csr_matrix(A_T) if A_T is not None else A.T.tocsr())
+        self.AT = DeviceCSR(AT)
+        if panels is None:
+            panels = A.nnz >= self.PANEL_MIN_NNZ
+        self.lsq = DeviceLSQ(A, AT) if panels else None
         self.b = _dev(np.asarray(b, dtype=np.float64).ravel())
         self.neg_b = -self.b
         self.tmp = torch.empty(self.m, dtype=torch.float64, device='cuda')
@@ -144,8 +155,13 @@ class SparseLSQ:
         torch = _torch()
         gd = g if isinstance(g, torch.Tensor) else torch.empty(self.n, dtype=torch.float64,
                                                                  device='cuda')
-        _, sq = self.A.matvec(_dev(x), out=self.tmp, add=self.neg_b, want_sq=True)
-        self.AT.matvec(self.tmp, out=gd)
+        if self.lsq is not None:
+            sq = torch.zeros(1, dtype=torch.float64, device='cuda')
+            self.lsq.residual(_dev(x), self.tmp, add=self.neg_b, sq=sq)
+            self.lsq.gradient(self.tmp, gd)
+        else:
+            _, sq = self.A.matvec(_dev(x), out=self.tmp, add=self.neg_b, want_sq=True)
+            self.AT.matvec(self.tmp, out=gd)
         if g is not None and gd is not g:
             np.copyto(g, gd.cpu().numpy())      # a NumPy g is written in place, as np.copyto
         return .5 * float(sq.item())

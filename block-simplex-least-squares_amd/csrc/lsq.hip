@@ -1,0 +1,216 @@
+// lsq.hip -- the x-space least-squares operator pair on panel images:
+//   residual  r = A x + add, ||r||^2      (algorithm_utils.sparse_least_squares_obj
+//                                           :88-94's tmp = A.dot(x) - b, tmp.dot(tmp))
+//   gradient  g = A' r                     (its np.copyto(g, A_sparse_T.dot(tmp)))
+// used by the x-space BB engine (xbb.hip), the batch objective
+// (algorithm_utils.SparseLSQ) and mirror descent (mirror_descent.py:31-34).
+// The same LDS-chunked panel walk as the z-space engine's K1 / K2 (panels.hpp,
+// bb.hip), without the N / N' algebra: the residual splits the columns into
+// XCD groups with per-group partial rows summed in group order by the last
+// workgroup of each row block; the gradient sums each row of A' in CSR order
+// over all chunks (bit-identical to SciPy's csr_matvec).  For a scaled
+// incidence (values not stored) the residual first forms colv * x (the
+// products SciPy forms, one extra pass) and the gradient multiplies each
+// entry by its row's colv.
+#include "panels.hpp"
+
+namespace bsls {
+
+struct LsqWork {
+    unsigned *tk;       // ||r||^2 hand-off
+    unsigned *tkrb;     // one ticket per row block
+    double *part;       // one partial per row block
+    size_t bytes;
+};
+
+static size_t lal(size_t v) { return (v + 255) & ~(size_t)255; }
+
+static LsqWork lsq_layout(void *base, int64_t A_npanels) {
+    LsqWork w{};
+    char *p = (char *)base;
+    const int64_t rbs = (A_npanels + PANEL_WAVES - 1) / PANEL_WAVES + 1;
+    size_t off = 0;
+    w.tk = (unsigned *)(p + off);
+    off += lal(TICKET_BYTES);
+    w.tkrb = (unsigned *)(p + off);
+    off += lal((size_t)rbs * 4);
+    w.part = (double *)(p + off);
+    off += lal((size_t)rbs * 8);
+    w.bytes = off;
+    return w;
+}
+
+__global__ __launch_bounds__(256) void lsq_scale_kernel(double *__restrict__ xs,
+                                                        const double *__restrict__ colv,
+                                                        const double *__restrict__ x, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        xs[i] = colv[i] * x[i];
+}
+
+// workgroup (group g = blockIdx % ngroups, row block rb): the group's chunks of
+// panels 16 rb .. 16 rb + 15 -> rpart[g][row]; the row block's last arriver
+// sums the partials in group order (+ add) into r; with sq_out, the last row
+// block reduces ||r||^2 (fixed order).
+template <int MODE>
+__global__ __launch_bounds__(1024) void lsq_k1(bsls_panels M, int64_t m,
+                                               const double *__restrict__ x,
+                                               const double *__restrict__ add,
+                                               double *__restrict__ r, double *sq_out,
+                                               double *rpart, unsigned *tkrb, double *part,
+                                               unsigned *ticket) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ int row_last;
+    const int64_t G = M.ngroups;
+    const int64_t g = blockIdx.x % G, rb = blockIdx.x / G;
+    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int64_t panel = rb * PANEL_WAVES + wv;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    const double sc[4] = {0.0, 0.0, 0.0, 0.0};
+    panel_chunks<MODE>(M, rb, wv, M.group_chunk[g], M.group_chunk[g + 1], x, lds, s, sc);
+    if (panel < M.npanels) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = 64 * q + lane;
+            const int64_t row = panel * M.prow + i;
+            if (i < M.prow && row < m)
+                __hip_atomic_store(&rpart[g * m + row], s[q], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev =
+            __hip_atomic_fetch_add(&tkrb[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        row_last = (prev == (unsigned)G - 1);
+        if (row_last) __hip_atomic_store(&tkrb[rb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!row_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t r0 = rb * PANEL_WAVES * M.prow;
+    const int64_t r1 = (r0 + PANEL_WAVES * M.prow < m) ? r0 + PANEL_WAVES * M.prow : m;
+    double sq[1] = {0.0};
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x) {
+        double o = __hip_atomic_load(&rpart[row], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int64_t c = 1; c < G; ++c)
+            o += __hip_atomic_load(&rpart[c * m + row], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (add) o += add[row];
+        r[row] = o;
+        sq[0] += o * o;
+    }
+    if (!sq_out) return;
+    const unsigned nrb = (unsigned)((M.npanels + PANEL_WAVES - 1) / PANEL_WAVES);
+    block_sum<1>(sq, lds);
+    double tot[1];
+    if (last_of_sum<1>(sq, part, (unsigned)rb, nrb, ticket, tot, lds) && threadIdx.x == 0)
+        *sq_out = tot[0];
+}
+
+// g = A' r: one workgroup per 16 panels of A' rows, every chunk of r.
+template <int MODE>
+__global__ __launch_bounds__(1024) void lsq_k2(bsls_panels M, int64_t n,
+                                               const double *__restrict__ r,
+                                               const double *__restrict__ colv,
+                                               double *__restrict__ g) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int wv = threadIdx.x / WAVE, lane = lane_id();
+    const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
+    const int64_t i0 = panel * M.prow;
+    const bool live = panel < M.npanels;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    double sc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (MODE == 2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i = i0 + 64 * q + lane;
+            const bool ok = live && 64 * q + lane < M.prow && i < n;
+            const double v = colv[ok ? i : 0];
+            sc[q] = ok ? v : 0.0;
+        }
+    }
+    panel_chunks<MODE>(M, blockIdx.x, wv, 0, M.nchunks, r, lds, s, sc);
+    if (!live) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int pos = 64 * q + lane;
+        const int64_t i = i0 + pos;
+        if (pos < M.prow && i < n) g[i] = s[q];
+    }
+}
+
+constexpr int LSQ_LDS_MAX = 163840 - 512;
+template <typename K>
+static void lsq_allow_lds(K kernel) {
+    static bool done = false;
+    if (!done) {
+        (void)hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LSQ_LDS_MAX);
+        done = true;
+    }
+}
+
+static bool lsq_ok(const bsls_lsq_op *op) {
+    if (!op || op->m <= 0 || op->n <= 0) return false;
+    const bsls_panels &A = op->A, &T = op->AT;
+    if (A.rows != op->m || A.cols != op->n || T.rows != op->n || T.cols != op->m) return false;
+    if (T.halo != 0 || T.ngroups != 1 || A.halo != 0 || A.ngroups < 1) return false;
+    if (A.prow < 1 || A.prow > BSLS_PANEL_ROWS || T.prow < 1 || T.prow > BSLS_PANEL_ROWS)
+        return false;
+    if (!op->rpart || !op->work) return false;
+    if (op->colv ? (!op->xs || A.val || T.val) : (!A.val || !T.val)) return false;
+    return true;
+}
+
+}  // namespace bsls
+
+using namespace bsls;
+
+extern "C" size_t bsls_lsq_workspace_size(int64_t m, int64_t A_npanels) {
+    (void)m;
+    return lsq_layout(nullptr, A_npanels).bytes;
+}
+
+extern "C" int bsls_lsq_residual(const bsls_lsq_op *op, const double *d_x, const double *d_add,
+                                 double *d_r, double *d_sq_out, void *stream) {
+    if (!lsq_ok(op) || !d_x || !d_r) return BSLS_E_ARG;
+    LsqWork w = lsq_layout(op->work, op->A.npanels);
+    if (op->work_bytes < w.bytes) return BSLS_E_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t rbs = (op->A.npanels + PANEL_WAVES - 1) / PANEL_WAVES;
+    const int grid = (int)(op->A.ngroups * rbs);
+    if (op->colv) {
+        lsq_scale_kernel<<<grid_for(op->n < 262144 ? op->n : 262144, 256), 256, 0, st>>>(
+            op->xs, op->colv, d_x, op->n);
+        BSLS_LAUNCH_CHECK();
+        lsq_allow_lds(lsq_k1<0>);
+        lsq_k1<0><<<grid, 1024, panel_lds_bytes(op->A), st>>>(op->A, op->m, op->xs, d_add, d_r,
+                                                              d_sq_out, op->rpart, w.tkrb, w.part,
+                                                              w.tk);
+    } else {
+        lsq_allow_lds(lsq_k1<1>);
+        lsq_k1<1><<<grid, 1024, panel_lds_bytes(op->A), st>>>(op->A, op->m, d_x, d_add, d_r,
+                                                              d_sq_out, op->rpart, w.tkrb, w.part,
+                                                              w.tk);
+    }
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" int bsls_lsq_gradient(const bsls_lsq_op *op, const double *d_r, double *d_g,
+                                 void *stream) {
+    if (!lsq_ok(op) || !d_r || !d_g) return BSLS_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int grid = grid_for(op->AT.npanels, PANEL_WAVES);
+    if (op->colv) {
+        lsq_allow_lds(lsq_k2<2>);
+        lsq_k2<2><<<grid, 1024, panel_lds_bytes(op->AT), st>>>(op->AT, op->n, d_r, op->colv, d_g);
+    } else {
+        lsq_allow_lds(lsq_k2<1>);
+        lsq_k2<1><<<grid, 1024, panel_lds_bytes(op->AT), st>>>(op->AT, op->n, d_r, nullptr, d_g);
+    }
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}

@@ -219,7 +219,7 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
     if (!p || p->n <= 0 || p->m <= 0 || p->nblocks <= 0 || !p->x || !p->g || !p->xn || !p->gn ||
         !p->r || !p->scal || !p->neg_b || !p->starts || count < 0)
         return BSLS_E_ARG;
-    if (p->A.rows != p->m || p->AT.rows != p->n) return BSLS_E_ARG;
+    if (!p->lsq && (p->A.rows != p->m || p->AT.rows != p->n)) return BSLS_E_ARG;
     XWork w = xwork(p->work, p->A.ntiles);
     if (!p->work || p->work_bytes < w.bytes) return BSLS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
@@ -230,14 +230,21 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
         int rc = proj_launch_gated(p->ball != 0, p->xn, p->starts, p->nblocks, p->n, p->max_block,
                                    p->proj_work, p->proj_work_bytes, st, p->scal + BSLS_XS_MODE);
         if (rc != BSLS_OK) return rc;
-        rc = bsls_csr_spmv(p->m, p->A.indptr, p->A.indices, p->A.data, p->A.tiles, p->A.ntiles,
-                           p->xn, p->neg_b, 1.0, p->r, p->scal + BSLS_XS_SQ, (int)p->A.group,
-                           w.spmv, w.spmv_bytes, stream);
-        if (rc != BSLS_OK) return rc;
-        rc = bsls_csr_spmv(p->n, p->AT.indptr, p->AT.indices, p->AT.data, p->AT.tiles,
-                           p->AT.ntiles, p->r, nullptr, 1.0, p->gn, nullptr, (int)p->AT.group,
-                           nullptr, 0, stream);
-        if (rc != BSLS_OK) return rc;
+        if (p->lsq) {
+            rc = bsls_lsq_residual(p->lsq, p->xn, p->neg_b, p->r, p->scal + BSLS_XS_SQ, stream);
+            if (rc != BSLS_OK) return rc;
+            rc = bsls_lsq_gradient(p->lsq, p->r, p->gn, stream);
+            if (rc != BSLS_OK) return rc;
+        } else {
+            rc = bsls_csr_spmv(p->m, p->A.indptr, p->A.indices, p->A.data, p->A.tiles,
+                               p->A.ntiles, p->xn, p->neg_b, 1.0, p->r, p->scal + BSLS_XS_SQ,
+                               (int)p->A.group, w.spmv, w.spmv_bytes, stream);
+            if (rc != BSLS_OK) return rc;
+            rc = bsls_csr_spmv(p->n, p->AT.indptr, p->AT.indices, p->AT.data, p->AT.tiles,
+                               p->AT.ntiles, p->r, nullptr, 1.0, p->gn, nullptr, (int)p->AT.group,
+                               nullptr, 0, stream);
+            if (rc != BSLS_OK) return rc;
+        }
         xbb_finish_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal, p->hist,
                                              p->hist_cap, (double)p->max_iter, p->opt_tol,
                                              p->prog_tol, p->f_min, (int)p->has_fmin, w.part,

@@ -13,6 +13,7 @@ HBM layout of one z-space problem (python/main.py:41-79 restated for the GPU):
 All compute is in lib/libbsls_hip.so; this module only owns buffers and
 sequences calls.
 """
+import ctypes
 import time
 
 import numpy as np
@@ -269,6 +270,51 @@ def panel_rows(rows, workgroups_per_group, waves=16):
     16 panels per group (one per CU), within 64 .. BSLS_PANEL_ROWS."""
     want = -(-rows // (workgroups_per_group * waves))
     return int(min(_native.PANEL_ROWS, max(min(64, rows), want)))
+
+
+class DeviceLSQ:
+    """The x-space operator pair on panel images (csrc/lsq.hip, struct
+    bsls_lsq_op): residual r = A x + add with ||r||^2, gradient g = A' r.
+    sparse_least_squares_obj's two SciPy products (algorithm_utils.py:88-94).
+    A: 8 XCD column groups, no halo; A': one group.  A scaled incidence drops
+    the values (colv * x formed once per residual, A' entries scaled by colv
+    row by row: g stays bit-identical to SciPy's csr_matvec)."""
+
+    def __init__(self, A, AT=None, general=False):
+        torch = _torch()
+        L = _native.lib()
+        A = sps.csr_matrix(A)
+        AT = sps.csr_matrix(AT) if AT is not None else A.T.tocsr()
+        self.m, self.n = A.shape
+        colv = None if general else scaled_incidence_scale(A)
+        self.scaled = colv is not None
+        self.A_pan = DevicePanels(A, panel_rows(self.m, 32), False, 8, values=not self.scaled)
+        self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), False, 1,
+                                   values=not self.scaled)
+        dev = dict(dtype=torch.float64, device='cuda')
+        self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
+        self.xs = torch.empty(self.n, **dev) if self.scaled else None
+        self.rpart = torch.zeros(self.A_pan.img['ngroups'] * self.m, **dev)
+        self.work = torch.zeros(L.bsls_lsq_workspace_size(self.m, self.A_pan.img['npanels']),
+                                dtype=torch.uint8, device='cuda')
+        op = _native.LsqOp()
+        op.m, op.n = self.m, self.n
+        op.A, op.AT = self.A_pan.struct, self.AT_pan.struct
+        op.colv = ptr(self.colv)
+        op.rpart = self.rpart.data_ptr()
+        op.xs = ptr(self.xs)
+        op.work, op.work_bytes = self.work.data_ptr(), self.work.numel()
+        self.op = op
+
+    def residual(self, x, out, add=None, sq=None):
+        check(_native.lib().bsls_lsq_residual(self.op, ptr(x), ptr(add), ptr(out), ptr(sq),
+                                              stream_handle()), 'bsls_lsq_residual')
+        return out
+
+    def gradient(self, r, out):
+        check(_native.lib().bsls_lsq_gradient(self.op, ptr(r), ptr(out), stream_handle()),
+              'bsls_lsq_gradient')
+        return out
 
 
 class BlockLayout:
@@ -581,6 +627,8 @@ class XBBEngine:
         P.r, P.scal = self.r.data_ptr(), self.scal.data_ptr()
         P.proj_work, P.proj_work_bytes = proj.ws.data_ptr(), proj.ws.numel()
         P.work, P.work_bytes = self.work.data_ptr(), self.work.numel()
+        lsq = getattr(obj, 'lsq', None)
+        P.lsq = ctypes.pointer(lsq.op) if lsq is not None else None
         self.P = P
 
     def start(self, x_init, f_min=None, opt_tol=1e-6, max_iter=2000, prog_tol=1e-12,

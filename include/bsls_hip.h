@@ -229,6 +229,32 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  * bsls_bb_iterate runs 3, 4, 7. */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 
+/* ---- x-space least-squares operator on panel images -------------------------
+ * Replaces sparse_least_squares_obj's two SciPy products
+ * (python/algorithm_utils.py:88-94; python/mirror_descent.py:31-34):
+ *   bsls_lsq_residual   r = A x + add (add may be NULL), *sq_out = ||r||^2
+ *                       (device double, optional; fixed-order reduction)
+ *   bsls_lsq_gradient   g = A' r  (rows of A' summed in CSR order: bit-identical
+ *                       to SciPy's csr_matvec)
+ * A: panels with its columns in ngroups groups, halo 0 (as bsls_bb_problem.A);
+ * AT: A' panels, halo 0, one group.  Scaled incidence (colv != NULL): values
+ * not stored, xs (n doubles) is scratch for colv * x. */
+typedef struct bsls_lsq_op {
+    int64_t m, n;
+    bsls_panels A;
+    bsls_panels AT;
+    const double *colv;             /* n, or NULL (A.val / AT.val stored) */
+    double *rpart;                  /* A.ngroups x m partial residuals */
+    double *xs;                     /* n scratch (scaled only) */
+    void *work;                     /* bsls_lsq_workspace_size() bytes, zeroed once */
+    size_t work_bytes;
+} bsls_lsq_op;
+
+size_t bsls_lsq_workspace_size(int64_t m, int64_t A_npanels);
+int bsls_lsq_residual(const bsls_lsq_op *op, const double *d_x, const double *d_add, double *d_r,
+                      double *d_sq_out, void *stream);
+int bsls_lsq_gradient(const bsls_lsq_op *op, const double *d_r, double *d_g, void *stream);
+
 /* ---- fused x-space Barzilai-Borwein engine ----------------------------------
  * Replaces BATCH.solve_BB (python/BATCH.py:55-106) over the closures of
  * algorithm_utils.get_solver_parts(is_sparse=True) (python/algorithm_utils.py:
@@ -291,6 +317,7 @@ typedef struct bsls_xbb_problem {
     int64_t max_iter;
     double opt_tol, prog_tol, f_min;
     int64_t has_fmin;
+    const bsls_lsq_op *lsq;         /* panel operator for both products, or NULL (A / AT CSR) */
 } bsls_xbb_problem;
 
 size_t bsls_xbb_workspace_size(int64_t m, int64_t n, int64_t A_ntiles, int64_t AT_ntiles);

@@ -28,13 +28,17 @@ def _problem(golden, tag):
     return d, A, d['%s_b' % tag], d['%s_starts' % tag], d['%s_x_init' % tag]
 
 
-@pytest.mark.parametrize('fused', [True, False])
+@pytest.mark.parametrize('fused,panels', [(True, False), (False, False), (True, True)])
 @pytest.mark.parametrize('tag,lasso', [('s', False), ('c', False), ('l', True)])
-def test_solve_bb_vs_reference(cuda, golden, tag, lasso, fused):
+def test_solve_bb_vs_reference(cuda, golden, monkeypatch, tag, lasso, fused, panels):
     import BATCH
-    from algorithm_utils import get_solver_parts
+    from algorithm_utils import SparseLSQ, get_solver_parts
+    # panels: both products on the panel images (csrc/lsq.hip), forced on
+    # these small problems; otherwise the CSR kernels
+    monkeypatch.setattr(SparseLSQ, 'PANEL_MIN_NNZ', 0 if panels else 1 << 62)
     d, A, b, starts, x0 = _problem(golden, tag)
     step, proj, ls, obj = get_solver_parts((A, b), starts, 1.0, is_sparse=True, lasso=lasso)
+    assert (obj.lsq is not None) == panels
     for k in (2, 3, 6, 15, 40):
         sol = BATCH.solve_BB(obj, proj, ls, x0.copy(), max_iter=k, fused=fused)
         ref_it = int(d['%s_bb%d_it' % (tag, k)])

@@ -1,0 +1,105 @@
+"""The x-space operator pair on panel images (csrc/lsq.hip, device.DeviceLSQ):
+r = A x + add, ||r||^2 and g = A' r -- sparse_least_squares_obj's two SciPy
+products (python/algorithm_utils.py:88-94).  Needs an MI355X.
+
+Bar: g bit-identical to SciPy's csr_matvec on A' (each row summed in CSR
+order); r bit-identical to the host restatement of the panel walk
+(device.panels_matvec: 8 column-group partials summed in group order) and
+within 1e-12 relative of SciPy; ||r||^2 within 1e-12 relative.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sps
+
+from conftest import SEED
+
+pytestmark = pytest.mark.gpu
+
+
+def exact(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+def _scaled(m, n, per_col, rs):
+    """Scaled incidence: per_col distinct rows per column, value colv[j]."""
+    rows = np.concatenate([rs.choice(m, min(per_col, m), replace=False) for _ in range(n)])
+    cols = np.repeat(np.arange(n), min(per_col, m))
+    colv = np.floor(rs.rand(n) * 1000) + 1
+    return sps.csr_matrix((colv[cols], (rows, cols)), shape=(m, n))
+
+
+@pytest.mark.parametrize('m,n,per_col', [(1000, 9001, 5), (37, 300, 3), (20000, 150000, 12),
+                                         (4096, 64, 40)])
+@pytest.mark.parametrize('scaled', [True, False])
+def test_lsq_operator(cuda, m, n, per_col, scaled):
+    import torch
+    from device import DeviceLSQ, panels_matvec
+    rs = np.random.RandomState(SEED + m)
+    A = _scaled(m, n, per_col, rs)
+    if not scaled:
+        A.data = rs.randn(A.nnz)
+    # empty rows and columns
+    A = sps.csr_matrix(sps.diags((rs.rand(m) > 0.05).astype(float)) @ A @
+                       sps.diags((rs.rand(n) > 0.05).astype(float)))
+    A.eliminate_zeros()
+    AT = A.T.tocsr()
+    op = DeviceLSQ(A, AT, general=not scaled)
+    assert op.scaled == scaled
+    x = rs.randn(n)
+    add = rs.randn(m)
+    xd, ad = torch.from_numpy(x).cuda(), torch.from_numpy(add).cuda()
+    r = torch.empty(m, dtype=torch.float64, device='cuda')
+    sq = torch.zeros(1, dtype=torch.float64, device='cuda')
+    op.residual(xd, r, add=ad, sq=sq)
+    rh = r.cpu().numpy()
+    ref = A.dot(x) + add
+    np.testing.assert_allclose(rh, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+    assert abs(float(sq.item()) - ref.dot(ref)) <= 1e-12 * ref.dot(ref)
+    if m * n <= 10 ** 7:
+        if scaled:
+            colv = op.colv.cpu().numpy()
+            want, _ = panels_matvec(op.A_pan.img, colv * x)
+        else:
+            want, _ = panels_matvec(op.A_pan.img, x)
+        assert exact(rh, want + add)
+    # residual without add / without ||r||^2
+    r2 = torch.empty(m, dtype=torch.float64, device='cuda')
+    op.residual(xd, r2)
+    np.testing.assert_allclose(r2.cpu().numpy(), A.dot(x), rtol=1e-12,
+                               atol=1e-12 * np.abs(ref).max())
+    g = torch.empty(n, dtype=torch.float64, device='cuda')
+    op.gradient(r, g)
+    assert exact(g.cpu().numpy(), AT.dot(rh))
+    # repeated calls: deterministic (tickets re-armed)
+    r3 = torch.empty(m, dtype=torch.float64, device='cuda')
+    sq3 = torch.zeros(1, dtype=torch.float64, device='cuda')
+    for _ in range(3):
+        op.residual(xd, r3, add=ad, sq=sq3)
+    assert exact(r3.cpu().numpy(), rh) and float(sq3.item()) == float(sq.item())
+
+
+def test_sparse_lsq_panel_and_csr_paths_agree(cuda):
+    """SparseLSQ (the obj of get_solver_parts(is_sparse=True)) on panels and on
+    the CSR kernels: same f to 1e-12, g within 1e-12 (its input r differs by
+    the residual's group order only)."""
+    import torch
+    from algorithm_utils import SparseLSQ
+    from synthetic import make_shard, add_noise
+    sh = make_shard(60_000, 3_000, 6_000, 16, seed=5)
+    b = add_noise(sh['Ax'], 0.02, seed=5)
+    P = SparseLSQ(sh['A'], b, panels=True)
+    C = SparseLSQ(sh['A'], b, panels=False)
+    assert P.lsq is not None and P.lsq.scaled and C.lsq is None
+    x = np.random.RandomState(1).rand(sh['A'].shape[1])
+    gp = torch.empty(P.n, dtype=torch.float64, device='cuda')
+    gc = torch.empty(P.n, dtype=torch.float64, device='cuda')
+    fp, fc = P(torch.from_numpy(x).cuda(), gp), C(torch.from_numpy(x).cuda(), gc)
+    assert abs(fp - fc) <= 1e-12 * abs(fc)
+    tmp = sh['A'].dot(x) - b
+    assert abs(fp - .5 * tmp.dot(tmp)) <= 1e-12 * abs(fp)
+    gref = sh['A'].T.tocsr().dot(tmp)
+    np.testing.assert_allclose(gp.cpu().numpy(), gref, rtol=1e-10,
+                               atol=1e-12 * np.abs(gref).max())
+    np.testing.assert_allclose(gc.cpu().numpy(), gref, rtol=1e-10,
+                               atol=1e-12 * np.abs(gref).max())

@@ -352,7 +352,7 @@ static void launch(double *y, const int64_t *st, int64_t nb, int64_t n) {
             (void)hipMalloc(&g_count, 64);
             (void)hipMemset(g_count, 0, 64);
         }
-        proj_lds_kernel<false><<<grid_for(nb, WAVE), WAVE>>>(y, st, nb, n, g_list, g_count, 0);
+        proj_lds_kernel<false><<<grid_for(nb, WAVE), WAVE>>>(y, st, nb, n, g_list, g_count, 0, nullptr);
         return;
     }
     if (V >= 6 && V <= 10) proj_t<V><<<grid_for(nb, WAVE), WAVE>>>(y, st, nb, n);
