@@ -191,7 +191,10 @@ __device__ __forceinline__ void lane_block(Ptr y, int64_t s, int k) {
 // blocks out of LDS.  Without staging, every wave-instruction touched 64 cache
 // lines (one per block) -- measured 2.6x write amplification.  A wave whose
 // range exceeds PCAP doubles falls back to direct global access.
-constexpr int PCAP = 3072;
+// PCAP 2400: PBUF * 8 B = 20.2 KB per wave, so 8 waves per CU (the VGPR
+// limit too) -- 2048 resident waves; a grid beyond the resident set leaves a
+// tail of late waves (measured: 27 of 1563 waves at 3072 doubled the time).
+constexpr int PCAP = 2400;
 constexpr int PBUF = PCAP + 2 * WAVE + 2;   // + read slack, + one dummy slot per lane
 
 __device__ __forceinline__ int64_t uni64(int64_t v, int l) {
@@ -200,13 +203,84 @@ __device__ __forceinline__ int64_t uni64(int64_t v, int l) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
 }
 
+// Comparator of the generated top-16 selection networks (proj_net.hpp): max
+// to the lower index, 2-instruction asm like bitonic_flip's.
+#define PROJ_CE(i, l)                                                                \
+    do {                                                                             \
+        double hi_, lo_;                                                             \
+        asm volatile("v_max_f64 %0, %2, %3\n\tv_min_f64 %1, %2, %3"                  \
+                     : "=&v"(hi_), "=v"(lo_)                                         \
+                     : "v"(v[i]), "v"(v[l]));                                        \
+        v[i] = hi_;                                                                  \
+        v[l] = lo_;                                                                  \
+    } while (0)
+}  // namespace bsls
+#include "proj_net.hpp"
+namespace bsls {
+#undef PROJ_CE
+
+// lambda_fast over a sorted prefix only, stopping each lane once its answer
+// is settled.  The exact e_i = (i+1) u_i + 1 - S_i is non-increasing in i
+// (e_{i+1} - e_i = (i+1)(u_{i+1} - u_i) <= 0) and the reference's test at i
+// is e_i > 0 up to rounding; with every fl error of S_i, 1 - S_i and the test
+// bounded by 2^-53 (2 k^2 Mx + 3 (1 + k Mx)) <= margin = k 2^-49 (1 + 2 k Mx)
+// (Mx >= max |u|), a computed E_i < -margin makes the test false at i and at
+// every later index.  A lane is settled at that point or when i reaches k.
+struct Chain {
+    double run, D0, Drho;
+    int rho, a;
+    bool live;
+};
+
+template <int N>
+__device__ __forceinline__ Chain chain_begin(const double (&u)[N], int k) {
+    Chain c;
+    c.run = u[0];
+    c.D0 = 1. - c.run;
+    c.Drho = c.D0;
+    c.rho = 0;
+    c.a = 0;
+    c.live = k > 1;
+    return c;
+}
+
+// indices I0 .. I1 - 1 of the chain (u sorted there); the wave leaves as soon
+// as every lane is settled
+template <int I0, int I1, int N>
+__device__ __forceinline__ void chain_steps(const double (&u)[N], int k, double margin, Chain &c) {
+#pragma unroll
+    for (int i = I0; i < I1; ++i) {
+        if (((i - I0) & 3) == 0 && !__builtin_amdgcn_ballot_w64(c.live)) break;
+        c.live = c.live && (i < k);
+        c.run = c.run + u[i];
+        const double D = 1. - c.run;
+        const double ip1 = (double)i + 1.;
+        const double E = __builtin_fma(ip1, u[i], D);
+        const double T = ip1 * __builtin_fma(__builtin_fabs(u[i]), 0x1p-51, 0x1p-1070);
+        const bool ok = c.live && (E > T);
+        c.a |= (c.live && (E > 0.0) && !(E > T)) ? 1 : 0;
+        c.rho = ok ? i : c.rho;
+        c.Drho = ok ? D : c.Drho;
+        c.live = c.live && !(E < -margin);
+        asm volatile("" : "+v"(c.Drho), "+v"(c.rho), "+v"(c.a), "+v"(c.run));
+    }
+}
+
+__device__ __forceinline__ double chain_lambda(const Chain &c) {
+    return c.rho == 0 ? c.D0 : c.Drho / ((double)c.rho + 1.);
+}
+
 // One lane, one block of k <= KB entries at buf[off ..): straight-line code.
 // Reads are unconditional (slack after the range), writes of j >= k go to the
 // lane's dummy slot, so no per-entry branches or per-entry waits.
+// KB > 16: top-16 selection networks (proj_net.hpp) + the early-settling
+// chain; a wave with an unsettled lane sorts fully (the networks only
+// permute, the -inf padding stays put).
 template <int N, int KB, bool BALL>
 __device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int lane) {
     double v[N];
     double acc = 0.0;
+    uint32_t hx = 0;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         double t = -INFINITY;
@@ -217,16 +291,50 @@ __device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int 
             t = (t < 0.0) ? 0.0 : t;
             acc += (j < k) ? t : 0.0;
         }
+        if (KB > 16 && j < KB) {
+            const uint32_t h = (uint32_t)((uint64_t)__double_as_longlong(t) >> 32) & 0x7fffffffu;
+            hx = (j < k && h > hx) ? h : hx;
+        }
         v[j] = (j < k) ? t : -INFINITY;
     }
     const bool need = BALL ? (acc > 1.0) : true;
     double lam = 0.0;
     if (!BALL || __builtin_amdgcn_ballot_w64(need)) {
-        bitonic_flip<N, KB>(v);
-        bool amb;
-        lam = lambda_fast<N, KB>(v, k, amb);
-        if (__builtin_amdgcn_ballot_w64(amb)) {
-            if (amb) lam = lambda_sorted<N, KB>(v, k);
+        bool full = true;
+        if constexpr (KB > 16) {
+            // level 1: the 16 largest, sorted, and the chain over them;
+            // level 2 (KB > 32): the next 16 of the rest, chain continued;
+            // a wave with a lane still open after that sorts fully
+            Top16<KB>::template run<0>(v);
+            const double Mx =
+                __longlong_as_double((long long)(((uint64_t)hx << 32) | 0xffffffffull));
+            const double kk = (double)k;
+            const double margin = kk * 0x1p-49 * (1. + 2. * kk * Mx);
+            Chain c = chain_begin(v, k);
+            chain_steps<1, 16>(v, k, margin, c);
+            int depth = 16;
+            if constexpr (KB > 32) {
+                if (__builtin_amdgcn_ballot_w64(c.live && k > 16)) {
+                    Top16<KB - 16>::template run<16>(v);
+                    chain_steps<16, 32>(v, k, margin, c);
+                    depth = 32;
+                }
+            }
+            full = __builtin_amdgcn_ballot_w64(c.live && k > depth) != 0;
+            if (!full) {
+                lam = chain_lambda(c);
+                if (__builtin_amdgcn_ballot_w64(c.a != 0)) {
+                    if (c.a != 0) lam = lambda_sorted<N, (KB > 32 ? 32 : 16)>(v, k < depth ? k : depth);
+                }
+            }
+        }
+        if (full) {
+            bitonic_flip<N, KB>(v);
+            bool amb;
+            lam = lambda_fast<N, KB>(v, k, amb);
+            if (__builtin_amdgcn_ballot_w64(amb)) {
+                if (amb) lam = lambda_sorted<N, KB>(v, k);
+            }
         }
     }
     asm volatile("" ::: "memory");   // keep the o[] loads after the sort (VGPRs)
@@ -320,19 +428,33 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
     else if (kmax <= 56) lane_block_lds<64, 56, BALL>(buf, off, k, lane);
     else lane_block_lds<64, 64, BALL>(buf, off, k, lane);
     __syncthreads();
-    constexpr int SB = 16;   // LDS reads in flight per lane before the stores
-    for (int c0 = 0; c0 < tot; c0 += SB * WAVE) {
-        double t[SB];
+    // out: 16-B write-through (sc1) stores of the aligned pairs -- the bytes
+    // leave L2 while other waves still compute, instead of as dirty lines at
+    // the kernel's end (measured -2.8 us at C2) -- and the unaligned head /
+    // odd tail by lane 0
+    double *dst = y + s0 + sh;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(dst, 0, npair * 16, 0x00020000);
+    constexpr int SB = 8;   // LDS reads in flight per lane before the stores
+    for (int c0 = 0; c0 < npair; c0 += SB * WAVE) {
+        double2 t[SB];
 #pragma unroll
         for (int q = 0; q < SB; ++q) {
-            const int i = c0 + q * WAVE + lane;
-            t[q] = buf[sh + (i < tot ? i : 0)];
+            const int p = c0 + q * WAVE + lane;
+            t[q] = *(const double2 *)&buf[2 * sh + 2 * (p < npair ? p : 0)];
         }
 #pragma unroll
         for (int q = 0; q < SB; ++q) {
-            const int i = c0 + q * WAVE + lane;
-            if (i < tot) y[s0 + i] = t[q];
+            const int p = c0 + q * WAVE + lane;
+            if (p < npair)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(HIP_vector_type<unsigned, 4>::Native_vec_, t[q]), rs,
+                    16 * p, 0, 16);
         }
+    }
+    if (lane == 0) {
+        if (sh) y[s0] = buf[1];
+        if ((tot - sh) & 1) y[s0 + tot - 1] = buf[sh + tot - 1];
     }
 }
 
