@@ -36,6 +36,7 @@ int proj_launch_gated(bool ball, double *y, const int64_t *starts, int64_t nb, i
 
 constexpr int XT = 256;
 constexpr int XGRID = 1024;   // finish: partials per launch (one slot per workgroup)
+constexpr int XU = 4;         // finish: 16-B pairs per thread and step
 
 static size_t xalign(size_t v) { return (v + 255) & ~(size_t)255; }
 
@@ -111,8 +112,40 @@ __global__ __launch_bounds__(XT) void xbb_finish_kernel(
     // gd = g.(x_new - x), dx.dg, dg.dg, ||dx||_inf
     double v[4] = {0.0, 0.0, 0.0, 0.0};
     if (mode != BSLS_XM_INIT) {
-        const int64_t stride = (int64_t)gridDim.x * XT;
-        for (int64_t i = (int64_t)blockIdx.x * XT + threadIdx.x; i < n; i += stride) {
+        // XU pairs per thread and step, 16-B loads, all issued before the math
+        // (the vectors are 16-B aligned device allocations); odd tail by
+        // thread 0 of workgroup 0
+        const int64_t n2 = n >> 1;
+        const int64_t stride = (int64_t)gridDim.x * XT * XU;
+        for (int64_t p0 = (int64_t)blockIdx.x * XT * XU + threadIdx.x; p0 < n2; p0 += stride) {
+            double2 gv[XU], xv[XU], xnv[XU], gnv[XU];
+#pragma unroll
+            for (int u = 0; u < XU; ++u) {
+                const int64_t p = p0 + (int64_t)u * XT;
+                const int64_t q = p < n2 ? p : 0;
+                gv[u] = ((const double2 *)g)[q];
+                xv[u] = ((const double2 *)x)[q];
+                xnv[u] = ((const double2 *)xn)[q];
+                gnv[u] = ((const double2 *)gn)[q];
+            }
+#pragma unroll
+            for (int u = 0; u < XU; ++u) {
+                if (p0 + (int64_t)u * XT < n2) {
+                    const double dx0 = xnv[u].x - xv[u].x, dx1 = xnv[u].y - xv[u].y;
+                    const double dg0 = gnv[u].x - gv[u].x, dg1 = gnv[u].y - gv[u].y;
+                    v[0] += gv[u].x * dx0;
+                    v[0] += gv[u].y * dx1;
+                    v[1] += dx0 * dg0;
+                    v[1] += dx1 * dg1;
+                    v[2] += dg0 * dg0;
+                    v[2] += dg1 * dg1;
+                    v[3] = nan_max(v[3], fabs(dx0));
+                    v[3] = nan_max(v[3], fabs(dx1));
+                }
+            }
+        }
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const int64_t i = n - 1;
             const double gv = g[i];
             const double dx = xn[i] - x[i];
             const double dg = gn[i] - gv;
@@ -224,6 +257,8 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
     if (!p->work || p->work_bytes < w.bytes) return BSLS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
     const int gs = xgrid(p->n);
+    const int64_t fw = ((p->n >> 1) + XT * XU - 1) / (XT * XU);
+    const int gf = (int)(fw < 1 ? 1 : (fw > XGRID ? XGRID : fw));
     for (int64_t c = 0; c < count; ++c) {
         xbb_step_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal);
         BSLS_LAUNCH_CHECK();
@@ -245,7 +280,7 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
                                nullptr, 0, stream);
             if (rc != BSLS_OK) return rc;
         }
-        xbb_finish_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal, p->hist,
+        xbb_finish_kernel<<<gf, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal, p->hist,
                                              p->hist_cap, (double)p->max_iter, p->opt_tol,
                                              p->prog_tol, p->f_min, (int)p->has_fmin, w.part,
                                              w.ticket);

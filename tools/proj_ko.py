@@ -18,7 +18,10 @@ def main():
              12: 'conflict-free + no fallback', 16: 'no output pass',
              23: 'only load loop', 32: 'no HBM staging', 36: 'no staging, no fallback',
              55: 'no staging, only load loop', 64: 'x4 plain stores', 128: 'x4 sc1 stores',
-             87: 'x4 plain, only load loop', 151: 'x4 sc1, only load loop'}
+             87: 'x4 plain, only load loop', 151: 'x4 sc1, only load loop',
+             384: 'x4 sc1 + nt loads', 407: 'x4 sc1 + nt, only load loop',
+             512: 'empty (metadata only)', 2048: 'empty kernel (1563 WGs)', 4096: 'empty 1 WG (20KB LDS)', 8192: 'empty 391 WGs x256 (80KB)',
+             12288: 'empty 1563 WGs no LDS', 16384: 'empty 1563 WGs 20KB', 1536: 'streaming copy x4 sc1'}
     for kind in ('unif',):
         y_h, st_h = proj_input(kind=kind)
         y0 = torch.from_numpy(y_h).cuda()
