@@ -199,6 +199,34 @@ def bench_xspace(sh, b, rounds=40, reps=5):
             'backtracks': bts, 'finite': ok}
 
 
+def bench_md(sh, b, iters=30):
+    """Mirror descent (mirror_descent.least_squares, SURVEY.md §8 row a12;
+    BASELINE config C4) on the same C3 problem: r = A x - b and A' r on the
+    panel operator, the exp / block-normalise / ||dx||_inf step with the
+    device-side stopping test (tolerance < 0: never stops), `iters` iterations
+    between two events, inputs resident.  A and b scaled by 1/100: the step
+    t_k = sqrt(2 ln k_b)/(sqrt(k) Lf) scales as 1/s and g as s^2, so on the
+    unscaled problem exp(-t g) overflows in the first iteration (in the
+    reference as here: NaN); the cost per iteration does not depend on s."""
+    import torch
+    from mirror_descent import MirrorDescent
+    md = MirrorDescent(sh['A'] * 0.01, b * 0.01, sh['block_sizes'])
+    md.start()
+    md.iterate(1, 5, -1.0)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    md.iterate(6, iters, -1.0)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    x = md.x.cpu().numpy()
+    return {'operator': 'panels' if md.lsq is not None else 'csr', 'scale': 0.01,
+            'iterations': iters,
+            'us_per_iter': ms * 1e3 / iters, 'iterations_per_s': iters / (ms * 1e-3),
+            'finite': bool(np.all(np.isfinite(x)))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -325,6 +353,7 @@ def main():
         ib = survey_iter_bytes(m, n_g * world, eng.nz * world, nnz * world)
         proj = bench_proj() if world == 1 else None
         xspace = bench_xspace(sh, b) if world == 1 else None
+        mdr = bench_md(sh, b) if world == 1 else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cps, cit, cel = cpu_baseline_bb(sh['A'], b, sh['block_sizes'])
@@ -346,7 +375,8 @@ def main():
             'iteration_roofline': {'survey_bytes_per_iter': ib,
                                    'achieved_GB_s': ib * it_s / 1e9,
                                    'frac': ib * it_s / HBM_PEAK},
-            'kernels': kern, 'proj_simplex': proj, 'xspace_bb': xspace, 'cpu_baseline': cpu,
+            'kernels': kern, 'proj_simplex': proj, 'xspace_bb': xspace, 'mirror_descent': mdr,
+            'cpu_baseline': cpu,
             'finite': finite,
         }
         print(json.dumps(out), flush=True)

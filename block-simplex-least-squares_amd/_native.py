@@ -10,7 +10,8 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'lib', 'libbsls_hip.so')
+# BSLS_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get('BSLS_LIB') or os.path.join(HERE, 'lib', 'libbsls_hip.so')
 CSRC = os.path.join(HERE, 'csrc')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'bsls_hip.h')
 
@@ -120,6 +121,8 @@ _SIGS = {
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
+    'bsls_md_update_gated': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _dbl, _i64, _vp, _vp, _sz,
+                                    _vp]),
     'bsls_md_update': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _vp, _vp, _sz, _vp]),
     'bsls_md_workspace_size': (_sz, [_i64]),
     'bsls_version': (ctypes.c_char_p, []),

@@ -159,14 +159,20 @@ __global__ __launch_bounds__(256) void line_search_kernel(const double *x, doubl
 // up = g * t, t = sqrt(2 ln k_b) / scale (scale = sqrt(k) Lf from the host),
 // x <- x * exp(-up), then each block divided by its sum; per-block
 // max|x_new - x_old| into part[], reduced by the last workgroup into *dxinf.
+// With `state` (gated form): nothing happens once state[0] != 0; the launch
+// that sees ||x_new - x_old||_inf < tol sets state[0] = 1 and state[2] = iter
+// (the reference's break), state[1] = the norm every launch.
 __global__ __launch_bounds__(256) void md_kernel(double *__restrict__ x,
                                                  const double *__restrict__ g,
                                                  const int64_t *__restrict__ starts,
                                                  int64_t nb, int64_t n, double scale,
                                                  double *__restrict__ dxinf,
                                                  double *__restrict__ part,
-                                                 unsigned *__restrict__ ticket) {
+                                                 unsigned *__restrict__ ticket,
+                                                 double *__restrict__ state, double tol,
+                                                 int64_t iter) {
     __shared__ double red[4];
+    if (state && state[0] != 0.0) return;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double dmax = 0.0;
     if (b < nb) {
@@ -211,7 +217,14 @@ __global__ __launch_bounds__(256) void md_kernel(double *__restrict__ x,
             const double v = __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             m = v > m ? v : m;
         }
-        *dxinf = m;
+        if (dxinf) *dxinf = m;
+        if (state) {
+            state[1] = m;
+            if (m < tol) {                       // mirror_descent.py:50-51
+                state[0] = 1.0;
+                state[2] = (double)iter;
+            }
+        }
         *ticket = 0u;
     }
 }
@@ -313,7 +326,21 @@ extern "C" int bsls_md_update(double *d_x, const double *d_g, const int64_t *d_s
     unsigned *ticket = (unsigned *)d_work;
     double *part = (double *)((char *)d_work + TICKET_BYTES);
     md_kernel<<<grid_for(nblocks, 256), 256, 0, (hipStream_t)stream>>>(
-        d_x, d_g, d_starts, nblocks, n, step_scale, d_dxinf, part, ticket);
+        d_x, d_g, d_starts, nblocks, n, step_scale, d_dxinf, part, ticket, nullptr, 0.0, 0);
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" int bsls_md_update_gated(double *d_x, const double *d_g, const int64_t *d_starts,
+                                    int64_t nblocks, int64_t n, double step_scale, double tol,
+                                    int64_t iter, double *d_state, void *d_work,
+                                    size_t work_bytes, void *stream) {
+    if (nblocks <= 0 || n <= 0 || !d_x || !d_g || !d_starts || !d_state) return BSLS_E_ARG;
+    if (!d_work || work_bytes < bsls_md_workspace_size(nblocks)) return BSLS_E_WORKSPACE;
+    unsigned *ticket = (unsigned *)d_work;
+    double *part = (double *)((char *)d_work + TICKET_BYTES);
+    md_kernel<<<grid_for(nblocks, 256), 256, 0, (hipStream_t)stream>>>(
+        d_x, d_g, d_starts, nblocks, n, step_scale, nullptr, part, ticket, d_state, tol, iter);
     BSLS_LAUNCH_CHECK();
     return BSLS_OK;
 }

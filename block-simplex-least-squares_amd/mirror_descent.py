@@ -3,9 +3,9 @@ python/mirror_descent.py:7-53), on MI355X.
 
 least_squares(A, b, blocks, iters=1000, tolerance=1e-9) -> x (NumPy), with
 `blocks` the list of block sizes.  Per iteration: r = A x - b and g = A' r
-(CSR SpMV kernels, explicit A'), then one fused kernel does
-x <- x * exp(-t_k g), t_k = sqrt(2 ln k_b) / (sqrt(k) Lf), the per-block
-normalisation and ||x_new - x||_inf.  Lf = sigma_max(A) from ARPACK (svds)
+(panel operator csrc/lsq.hip for large A, CSR SpMV kernels otherwise), then
+one fused kernel does x <- x * exp(-t_k g), t_k = sqrt(2 ln k_b) / (sqrt(k) Lf),
+the per-block normalisation, ||x_new - x||_inf and the stopping test.  Lf = sigma_max(A) from ARPACK (svds)
 driving device matvecs.  The reference's ragged np.array at :10-11 (which
 NumPy >= 1.24 rejects) is not reproduced: blocks of any sizes work.
 """
@@ -17,41 +17,90 @@ import _native
 from _native import check, ptr, stream_handle
 
 
-def least_squares(A, b, blocks, iters=1000, tolerance=1e-9, return_iters=False):
-    import torch
-    from device import DeviceCSR
-    L = _native.lib()
-    A = sps.csr_matrix(A)
-    sizes = np.asarray(blocks, dtype=np.int64)
-    n = int(sizes.sum())
-    if A.shape[1] != n:
-        raise ValueError('blocks cover %d entries, A has %d columns' % (n, A.shape[1]))
-    Ad, ATd = DeviceCSR(A), DeviceCSR(A.T.tocsr())
-    starts = torch.from_numpy(np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)).cuda()
-    x = torch.from_numpy(np.repeat(1.0 / sizes.astype(float), sizes)).cuda()
-    bd = torch.from_numpy(np.asarray(b, dtype=np.float64).ravel()).cuda()
+class MirrorDescent:
+    """Device state of mirror_descent.least_squares: A (panel images from 2^20
+    nonzeros up -- `panels` overrides -- else CSR), b, the block starts, x, and
+    Lf = sigma_max(A) from ARPACK driving device mat-vecs."""
 
-    def mv(v):
-        return Ad.matvec(torch.from_numpy(np.ascontiguousarray(np.real(v).ravel())).cuda()
-                         ).cpu().numpy()
+    def __init__(self, A, b, blocks, panels=None):
+        import torch
+        from device import DeviceCSR, DeviceLSQ
+        L = _native.lib()
+        A = sps.csr_matrix(A)
+        sizes = np.asarray(blocks, dtype=np.int64)
+        n = int(sizes.sum())
+        if A.shape[1] != n:
+            raise ValueError('blocks cover %d entries, A has %d columns' % (n, A.shape[1]))
+        AT = A.T.tocsr()
+        self.n, self.sizes = n, sizes
+        self.Ad, self.ATd = DeviceCSR(A), DeviceCSR(AT)
+        if panels is None:
+            panels = A.nnz >= (1 << 20)
+        self.lsq = DeviceLSQ(A, AT) if panels else None
+        self.starts = torch.from_numpy(
+            np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)).cuda()
+        bd = torch.from_numpy(np.asarray(b, dtype=np.float64).ravel()).cuda()
+        self.neg_b = -bd
+        dev = dict(dtype=torch.float64, device='cuda')
+        self.x = torch.empty(n, **dev)
+        self.r = torch.empty(A.shape[0], **dev)
+        self.g = torch.empty(n, **dev)
+        self.state = torch.zeros(3, **dev)
+        self.ws = torch.zeros(L.bsls_md_workspace_size(len(sizes)), dtype=torch.uint8,
+                              device='cuda')
 
-    def rmv(v):
-        return ATd.matvec(torch.from_numpy(np.ascontiguousarray(np.real(v).ravel())).cuda()
-                          ).cpu().numpy()
-    op = sla.LinearOperator(A.shape, matvec=mv, rmatvec=rmv, dtype=np.float64)
-    Lf = sla.svds(op, 1, return_singular_vectors=False)[0]
-    ws = torch.zeros(L.bsls_md_workspace_size(len(sizes)), dtype=torch.uint8, device='cuda')
-    dx = torch.zeros(1, dtype=torch.float64, device='cuda')
-    r = torch.empty(A.shape[0], dtype=torch.float64, device='cuda')
-    g = torch.empty(n, dtype=torch.float64, device='cuda')
+        def mv(v):
+            return self.Ad.matvec(torch.from_numpy(np.ascontiguousarray(np.real(v).ravel()))
+                                  .cuda()).cpu().numpy()
+
+        def rmv(v):
+            return self.ATd.matvec(torch.from_numpy(np.ascontiguousarray(np.real(v).ravel()))
+                                   .cuda()).cpu().numpy()
+        op = sla.LinearOperator(A.shape, matvec=mv, rmatvec=rmv, dtype=np.float64)
+        self.Lf = sla.svds(op, 1, return_singular_vectors=False)[0]
+
+    def start(self):
+        """x = 1 / block size (mirror_descent.py:9-16), stopping state cleared."""
+        import torch
+        self.x.copy_(torch.from_numpy(np.repeat(1.0 / self.sizes.astype(float), self.sizes)))
+        self.state.zero_()
+
+    def iterate(self, first, count, tolerance):
+        """Enqueue iterations first .. first + count - 1 (no host sync)."""
+        L = _native.lib()
+        for it in range(first, first + count):
+            if self.lsq is not None:
+                self.lsq.residual(self.x, self.r, add=self.neg_b)
+                self.lsq.gradient(self.r, self.g)
+            else:
+                self.Ad.matvec(self.x, out=self.r, add=self.neg_b)
+                self.ATd.matvec(self.r, out=self.g)
+            check(L.bsls_md_update_gated(ptr(self.x), ptr(self.g), ptr(self.starts),
+                                         len(self.sizes), self.n, float(np.sqrt(it) * self.Lf),
+                                         float(tolerance), it, ptr(self.state), ptr(self.ws),
+                                         self.ws.numel(), stream_handle()),
+                  'bsls_md_update_gated')
+
+
+def least_squares(A, b, blocks, iters=1000, tolerance=1e-9, return_iters=False, poll=16,
+                  panels=None):
+    """x after at most `iters` steps, stopping at the first whose
+    ||x - x_prev||_inf < tolerance (mirror_descent.py:37-51).  The stopping test
+    runs on the device (bsls_md_update_gated) and the host reads it every
+    `poll` iterations -- iterations enqueued past the stop leave x unchanged."""
+    md = MirrorDescent(A, b, blocks, panels=panels)
+    md.start()
+    poll = max(1, int(poll))
     it = 0
-    for it in range(1, iters + 1):
-        Ad.matvec(x, out=r, add=-bd)
-        ATd.matvec(r, out=g)
-        check(L.bsls_md_update(ptr(x), ptr(g), ptr(starts), len(sizes), n,
-                               float(np.sqrt(it) * Lf), ptr(dx), ptr(ws), ws.numel(),
-                               stream_handle()), 'bsls_md_update')
-        if float(dx.item()) < tolerance:
+    done = 0
+    while done < iters:
+        k = min(poll, iters - done)
+        md.iterate(done + 1, k, tolerance)
+        done += k
+        it = done
+        st = md.state.cpu().numpy()
+        if st[0] != 0.0:
+            it = int(st[2])
             break
-    out = x.cpu().numpy()
+    out = md.x.cpu().numpy()
     return (out, it) if return_iters else out

@@ -336,6 +336,16 @@ int bsls_md_update(double *d_x, const double *d_g, const int64_t *d_starts, int6
                    size_t work_bytes, void *stream);
 size_t bsls_md_workspace_size(int64_t nblocks);
 
+/* The same update with the reference's stopping test on the device, so the
+ * host need not read ||x_new - x_old||_inf every iteration
+ * (mirror_descent.py:50-51): d_state[3] = {stopped, last norm, stop
+ * iteration}, zeroed by the caller before iteration 1; once the norm of
+ * iteration `iter` is < tol, state = {1, norm, iter} and later calls leave x
+ * unchanged. */
+int bsls_md_update_gated(double *d_x, const double *d_g, const int64_t *d_starts, int64_t nblocks,
+                         int64_t n, double step_scale, double tol, int64_t iter, double *d_state,
+                         void *d_work, size_t work_bytes, void *stream);
+
 /* Replaces BATCH.solve_MD's update (python/BATCH.py:238-240) and
  * algorithm_utils.normalization (python/algorithm_utils.py:175-179):
  * d_y = d_x * exp(-t d_g) (d_y = d_x when d_g is NULL), then every block

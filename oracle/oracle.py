@@ -517,8 +517,9 @@ def dore_run(A, b, block_sizes, max_iter, record_every=100):
     return iters, states, lsv
 
 
-def md_least_squares(A, b, blocks, iters=1000, tolerance=1e-9):
-    """mirror_descent.py:7-53 (blocks = list of block sizes)."""
+def md_least_squares(A, b, blocks, iters=1000, tolerance=1e-9, return_iters=False):
+    """mirror_descent.py:7-53 (blocks = list of block sizes); return_iters: also
+    the iteration the loop ended at (test helper)."""
     n_vector = np.concatenate([[k] * k for k in blocks]).astype(float)
     x = np.divide(1.0, n_vector)
     if sps.issparse(A):
@@ -544,7 +545,7 @@ def md_least_squares(A, b, blocks, iters=1000, tolerance=1e-9):
             beg += k
         if np.linalg.norm(x - x_prev, np.inf) < tolerance:
             break
-    return x
+    return (x, it) if return_iters else x
 
 
 logging.getLogger(__name__).addHandler(logging.NullHandler())

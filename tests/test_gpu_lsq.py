@@ -103,3 +103,29 @@ def test_sparse_lsq_panel_and_csr_paths_agree(cuda):
                                atol=1e-12 * np.abs(gref).max())
     np.testing.assert_allclose(gc.cpu().numpy(), gref, rtol=1e-10,
                                atol=1e-12 * np.abs(gref).max())
+
+
+@pytest.mark.parametrize('panels', [False, True])
+def test_mirror_descent_vs_reference(cuda, golden, orc, panels):
+    """mirror_descent.least_squares (python/mirror_descent.py:7-53) on the
+    reference's own runs (tests/golden/solvers.npz): iterates at 1, 5 and 40
+    iterations within 1e-10 (device exp and sequential block sums differ from
+    NumPy's in the last bits); with a tolerance, the device-side stopping test
+    ends at the oracle's iteration with the same x."""
+    import mirror_descent
+    G = golden('solvers.npz')
+    A = sps.csr_matrix((G['md_A_data'], G['md_A_indices'], G['md_A_indptr']),
+                       shape=tuple(G['md_A_shape']))
+    blocks = list(G['md_blocks'])
+    for it in (1, 5, 40):
+        x, k = mirror_descent.least_squares(A, G['md_b'], blocks, iters=it, tolerance=0.0,
+                                            return_iters=True, panels=panels, poll=7)
+        assert k == it
+        np.testing.assert_allclose(x, G['md_x_%d' % it], rtol=1e-10, atol=1e-14)
+    for tol in (1e-3, 1e-5):
+        xr, kr = orc.md_least_squares(A, G['md_b'], blocks, iters=500, tolerance=tol,
+                                      return_iters=True)
+        x, k = mirror_descent.least_squares(A, G['md_b'], blocks, iters=500, tolerance=tol,
+                                            return_iters=True, panels=panels, poll=16)
+        assert k == kr, (tol, k, kr)
+        np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-13)
