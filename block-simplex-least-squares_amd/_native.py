@@ -123,6 +123,9 @@ _SIGS = {
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
     'bsls_md_update_gated': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _dbl, _i64, _vp, _vp, _sz,
                                     _vp]),
+    'bsls_md_pack_workspace_size': (_sz, [_i64]),
+    'bsls_md_update_packs': (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _i64, _vp, _vp,
+                                    _sz, _vp]),
     'bsls_md_update': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _vp, _vp, _sz, _vp]),
     'bsls_md_workspace_size': (_sz, [_i64]),
     'bsls_version': (ctypes.c_char_p, []),

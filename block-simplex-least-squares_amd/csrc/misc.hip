@@ -229,6 +229,92 @@ __global__ __launch_bounds__(256) void md_kernel(double *__restrict__ x,
     }
 }
 
+// The same update with one wave per PACK of whole blocks (<= 64 entries, one
+// lane per entry; host-planned, like K3's packs): coalesced loads and stores,
+// one exp per entry, the block sums by a segmented shuffle scan (a fixed tree
+// order instead of left to right -- mirror descent is not bit-pinned: np.exp
+// and np.sum differ from any device order anyway).  A block longer than 64
+// entries is a pack of its own, summed by the whole wave.  Gated form only.
+__device__ __forceinline__ double md_shfl(double v, int src) { return __shfl(v, src, WAVE); }
+constexpr int MD_PACK_WAVES = 16;   // packs per 1024-thread workgroup
+// max over the wave, NaN-propagating (the reference's inf-norm is NaN then)
+__device__ __forceinline__ double wave_nan_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+
+__global__ __launch_bounds__(1024) void md_pack_kernel(double *__restrict__ x,
+                                                      const double *__restrict__ g,
+                                                      const int64_t *__restrict__ pk_x0,
+                                                      const int64_t *__restrict__ pk_mask,
+                                                      const int32_t *__restrict__ pk_len,
+                                                      int64_t npacks, double scale,
+                                                      double *__restrict__ part,
+                                                      unsigned *__restrict__ ticket,
+                                                      double *__restrict__ state, double tol,
+                                                      int64_t iter) {
+    __shared__ double red[MD_PACK_WAVES];
+    if (state[0] != 0.0) return;
+    const int l = threadIdx.x % WAVE, wv = threadIdx.x / WAVE;
+    const int64_t pk = (int64_t)blockIdx.x * MD_PACK_WAVES + wv;
+    double dmax = 0.0;
+    if (pk < npacks) {
+        const int64_t x0 = pk_x0[pk];
+        const int L = pk_len[pk];
+        if (L <= WAVE) {
+            const uint64_t B = (uint64_t)pk_mask[pk];
+            const bool act = l < L;
+            const uint64_t le = (l >= 63) ? ~0ull : ((2ull << l) - 1ull);
+            const uint64_t below = B & le;                        // block starts at or before l
+            const int st = 63 - __clzll((long long)below);        // this entry's block start
+            const uint64_t above = B & ~le;
+            const int en = (above ? (__ffsll((long long)above) - 1) : L) - 1;   // its last entry
+            const double xo = act ? x[x0 + l] : 0.0;
+            const double gv = act ? g[x0 + l] : 0.0;
+            const double t = sqrt(2.0 * log((double)(en - st + 1))) / scale;
+            const double v = act ? xo * exp(-(gv * t)) : 0.0;
+            // segmented inclusive scan (segments = blocks)
+            double acc = v;
+#pragma unroll
+            for (int off = 1; off < WAVE; off <<= 1) {
+                const double y = md_shfl(acc, l >= off ? l - off : l);
+                if (l - off >= st) acc += y;
+            }
+            const double tot = md_shfl(acc, en < 0 ? 0 : en);
+            if (act) {
+                const double xn = v / tot;
+                const double d = fabs(xn - xo);
+                dmax = d;
+                x[x0 + l] = xn;
+            }
+        } else {
+            // one block of L > 64 entries: strided partial sums, then the wave's
+            const double t = sqrt(2.0 * log((double)L)) / scale;
+            double acc = 0.0;
+            for (int i = l; i < L; i += WAVE) acc += x[x0 + i] * exp(-(g[x0 + i] * t));
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, WAVE);
+            for (int i = l; i < L; i += WAVE) {
+                const double xo = x[x0 + i];
+                const double xn = (xo * exp(-(g[x0 + i] * t))) / acc;
+                const double d = fabs(xn - xo);
+                dmax = (d > dmax || d != d) ? d : dmax;
+                x[x0 + i] = xn;
+            }
+        }
+    }
+    double v1[1] = {dmax}, tot[1];
+    block_reduce<1, 1u>(v1, red);
+    if (last_block_reduce<1, 1u>(v1, part, ticket, tot, red) && threadIdx.x == 0) {
+        state[1] = tot[0];
+        if (tot[0] < tol) {                      // mirror_descent.py:50-51
+            state[0] = 1.0;
+            state[2] = (double)iter;
+        }
+    }
+}
+
 // BATCH.solve_MD's update (python/BATCH.py:238-240) and
 // algorithm_utils.normalization (python/algorithm_utils.py:175-179):
 // y = x * exp((-t) * g) elementwise (y = x when g == NULL), then every block
@@ -341,6 +427,29 @@ extern "C" int bsls_md_update_gated(double *d_x, const double *d_g, const int64_
     double *part = (double *)((char *)d_work + TICKET_BYTES);
     md_kernel<<<grid_for(nblocks, 256), 256, 0, (hipStream_t)stream>>>(
         d_x, d_g, d_starts, nblocks, n, step_scale, nullptr, part, ticket, d_state, tol, iter);
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" size_t bsls_md_pack_workspace_size(int64_t npacks) {
+    const int64_t grid = (npacks + MD_PACK_WAVES - 1) / MD_PACK_WAVES;
+    return (size_t)(TICKET_BYTES + ((grid * 8 + 15) & ~(int64_t)15));
+}
+
+extern "C" int bsls_md_update_packs(double *d_x, const double *d_g, const int64_t *d_pk_x0,
+                                    const int64_t *d_pk_mask, const int32_t *d_pk_len,
+                                    int64_t npacks, double step_scale, double tol, int64_t iter,
+                                    double *d_state, void *d_work, size_t work_bytes,
+                                    void *stream) {
+    if (npacks <= 0 || !d_x || !d_g || !d_pk_x0 || !d_pk_mask || !d_pk_len || !d_state)
+        return BSLS_E_ARG;
+    if (!d_work || work_bytes < bsls_md_pack_workspace_size(npacks)) return BSLS_E_WORKSPACE;
+    unsigned *ticket = (unsigned *)d_work;
+    double *part = (double *)((char *)d_work + TICKET_BYTES);
+    md_pack_kernel<<<(int)((npacks + MD_PACK_WAVES - 1) / MD_PACK_WAVES), 64 * MD_PACK_WAVES, 0,
+                     (hipStream_t)stream>>>(
+        d_x, d_g, d_pk_x0, d_pk_mask, d_pk_len, npacks, step_scale, part, ticket, d_state, tol,
+        iter);
     BSLS_LAUNCH_CHECK();
     return BSLS_OK;
 }

@@ -4,8 +4,9 @@ python/mirror_descent.py:7-53), on MI355X.
 least_squares(A, b, blocks, iters=1000, tolerance=1e-9) -> x (NumPy), with
 `blocks` the list of block sizes.  Per iteration: r = A x - b and g = A' r
 (panel operator csrc/lsq.hip for large A, CSR SpMV kernels otherwise), then
-one fused kernel does x <- x * exp(-t_k g), t_k = sqrt(2 ln k_b) / (sqrt(k) Lf),
-the per-block normalisation, ||x_new - x||_inf and the stopping test.  Lf = sigma_max(A) from ARPACK (svds)
+one fused kernel (one wave per pack of whole blocks, bsls_md_update_packs)
+does x <- x * exp(-t_k g), t_k = sqrt(2 ln k_b) / (sqrt(k) Lf), the per-block
+normalisation, ||x_new - x||_inf and the stopping test.  Lf = sigma_max(A) from ARPACK (svds)
 driving device matvecs.  The reference's ragged np.array at :10-11 (which
 NumPy >= 1.24 rejects) is not reproduced: blocks of any sizes work.
 """
@@ -15,6 +16,31 @@ import scipy.sparse.linalg as sla
 
 import _native
 from _native import check, ptr, stream_handle
+
+
+def pack_blocks(sizes):
+    """Packs of consecutive whole blocks with <= 64 entries for one wave (one
+    entry per lane), or a single longer block: (first entry, block-start mask,
+    length) per pack (bsls_md_update_packs)."""
+    sizes = np.asarray(sizes, dtype=np.int64)
+    starts = np.concatenate(([0], np.cumsum(sizes)[:-1]))
+    x0, mask, ln = [], [], []
+    b, p = 0, sizes.size
+    while b < p:
+        if sizes[b] > 64:
+            x0.append(starts[b]); mask.append(1); ln.append(int(sizes[b]))
+            b += 1
+            continue
+        tot, m = 0, 0
+        while b < p and sizes[b] <= 64 and tot + sizes[b] <= 64:
+            if tot == 0:
+                x0.append(starts[b])
+            m |= 1 << tot
+            tot += int(sizes[b])
+            b += 1
+        mask.append(m); ln.append(tot)
+    return (np.array(x0, dtype=np.int64), np.array(mask, dtype=np.uint64).view(np.int64),
+            np.array(ln, dtype=np.int32))
 
 
 class MirrorDescent:
@@ -46,7 +72,10 @@ class MirrorDescent:
         self.r = torch.empty(A.shape[0], **dev)
         self.g = torch.empty(n, **dev)
         self.state = torch.zeros(3, **dev)
-        self.ws = torch.zeros(L.bsls_md_workspace_size(len(sizes)), dtype=torch.uint8,
+        x0, mask, ln = pack_blocks(sizes)
+        self.pk = [torch.from_numpy(a).cuda() for a in (x0, mask, ln)]
+        self.npacks = int(x0.size)
+        self.ws = torch.zeros(L.bsls_md_pack_workspace_size(self.npacks), dtype=torch.uint8,
                               device='cuda')
 
         def mv(v):
@@ -75,11 +104,11 @@ class MirrorDescent:
             else:
                 self.Ad.matvec(self.x, out=self.r, add=self.neg_b)
                 self.ATd.matvec(self.r, out=self.g)
-            check(L.bsls_md_update_gated(ptr(self.x), ptr(self.g), ptr(self.starts),
-                                         len(self.sizes), self.n, float(np.sqrt(it) * self.Lf),
-                                         float(tolerance), it, ptr(self.state), ptr(self.ws),
-                                         self.ws.numel(), stream_handle()),
-                  'bsls_md_update_gated')
+            check(L.bsls_md_update_packs(ptr(self.x), ptr(self.g), ptr(self.pk[0]),
+                                         ptr(self.pk[1]), ptr(self.pk[2]), self.npacks,
+                                         float(np.sqrt(it) * self.Lf), float(tolerance), it,
+                                         ptr(self.state), ptr(self.ws), self.ws.numel(),
+                                         stream_handle()), 'bsls_md_update_packs')
 
 
 def least_squares(A, b, blocks, iters=1000, tolerance=1e-9, return_iters=False, poll=16,

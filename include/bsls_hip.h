@@ -346,6 +346,17 @@ int bsls_md_update_gated(double *d_x, const double *d_g, const int64_t *d_starts
                          int64_t n, double step_scale, double tol, int64_t iter, double *d_state,
                          void *d_work, size_t work_bytes, void *stream);
 
+/* The gated update over host-planned packs of whole blocks (one wave each,
+ * <= 64 entries one per lane, or one block > 64 entries): pk_x0 first entry,
+ * pk_mask block-start bits (bit 0 set), pk_len entries.  Coalesced, one exp
+ * per entry; block sums in a fixed tree order (within 1e-15 of the
+ * left-to-right sum).  d_state as for bsls_md_update_gated. */
+size_t bsls_md_pack_workspace_size(int64_t npacks);
+int bsls_md_update_packs(double *d_x, const double *d_g, const int64_t *d_pk_x0,
+                         const int64_t *d_pk_mask, const int32_t *d_pk_len, int64_t npacks,
+                         double step_scale, double tol, int64_t iter, double *d_state,
+                         void *d_work, size_t work_bytes, void *stream);
+
 /* Replaces BATCH.solve_MD's update (python/BATCH.py:238-240) and
  * algorithm_utils.normalization (python/algorithm_utils.py:175-179):
  * d_y = d_x * exp(-t d_g) (d_y = d_x when d_g is NULL), then every block

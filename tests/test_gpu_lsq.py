@@ -129,3 +129,21 @@ def test_mirror_descent_vs_reference(cuda, golden, orc, panels):
                                             return_iters=True, panels=panels, poll=16)
         assert k == kr, (tol, k, kr)
         np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-13)
+
+
+def test_mirror_descent_ragged_blocks_vs_oracle(cuda, orc):
+    """Ragged blocks, including blocks of 1 and blocks longer than a wave
+    (packs of their own): the device iterates follow the oracle's restatement
+    of mirror_descent.py within 1e-10."""
+    import mirror_descent
+    rs = np.random.RandomState(SEED)
+    sizes = np.concatenate([[1, 1, 65, 200, 64, 63, 2], rs.randint(1, 40, 300)])
+    n = int(sizes.sum())
+    m = 400
+    A = sps.random(m, n, density=8.0 / m, random_state=rs, format='csr')
+    A.data = rs.rand(A.nnz)
+    b = A.dot(np.repeat(1.0 / sizes, sizes)) * (1 + 0.05 * rs.randn(m))
+    for it in (1, 7, 30):
+        x = mirror_descent.least_squares(A, b, list(sizes), iters=it, tolerance=0.0, poll=5)
+        xr = orc.md_least_squares(A, b, list(sizes), iters=it, tolerance=0.0)
+        np.testing.assert_allclose(x, xr, rtol=1e-10, atol=1e-14)

@@ -250,3 +250,20 @@ def test_batch_modules_import_without_device():
     with pytest.raises(RuntimeError):
         algorithm_utils.get_solver_parts((sps.eye(4).tocsr(), np.ones(4)), np.array([0]), 1.0,
                                          is_sparse=True)
+
+
+def test_md_pack_blocks():
+    """mirror_descent.pack_blocks: whole blocks, <= 64 entries per pack, longer
+    blocks alone, masks of block starts."""
+    from mirror_descent import pack_blocks
+    sizes = [20, 30, 20, 70, 3, 64, 1, 1]
+    x0, mask, ln = pack_blocks(sizes)
+    assert list(x0) == [0, 50, 70, 140, 143, 207]
+    assert list(mask.view(np.uint64)) == [1 + (1 << 20), 1, 1, 1, 1, 3]
+    assert list(ln) == [50, 20, 70, 3, 64, 2]
+    rs = np.random.RandomState(0)
+    sizes = rs.randint(1, 90, 2000)
+    x0, mask, ln = pack_blocks(sizes)
+    assert ln.sum() == sizes.sum() and np.all(np.diff(x0) == ln[:-1])
+    nblk = sum(bin(int(v)).count('1') for v in mask.view(np.uint64))
+    assert nblk == sizes.size
