@@ -337,6 +337,17 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
     if (L <= WAVE) {
         const uint64_t B = (uint64_t)P.pk_mask[pk];
         const bool act = l < L;
+        const bool bstart = (B >> l) & 1ull;
+        const int64_t blk = b0 + __popcll(B & mask_le(l)) - 1;
+        const int64_t xi = z0 + l + blk;                // x index of this z entry
+        const bool bend = (l == L - 1) || (l < 63 && ((B >> (l + 1)) & 1ull));
+        // the column scales of this lane's x entries, loaded before the PAVA so
+        // their round trip overlaps it (x_put's products, same arithmetic)
+        double cv = 1.0, cv2 = 1.0;
+        if (P.colv) {
+            cv = act ? P.colv[xi] : 1.0;
+            cv2 = (act && bend) ? P.colv[xi + 1] : 1.0;
+        }
         double y = act ? zc[z0 + l] - t * g[z0 + l] : 0.0;  // x_next = x - t g (BB.py:29)
         const int wv = threadIdx.x / WAVE;
         pava_v1_wave_c(y, L, B, pv_y[wv], pv_p[wv]);
@@ -344,12 +355,9 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
         const double vprev = shfl_d(v, l > 0 ? l - 1 : 0);
         if (act) {
             zn[z0 + l] = v;
-            const bool bstart = (B >> l) & 1ull;
-            const int64_t blk = b0 + __popcll(B & mask_le(l)) - 1;
-            const int64_t xi = z0 + l + blk;            // x index of this z entry
-            x_put(P, xi, v - (bstart ? 0.0 : vprev));
-            const bool bend = (l == L - 1) || (l < 63 && ((B >> (l + 1)) & 1ull));
-            if (bend) x_put(P, xi + 1, 0.0 - v);        // (N z)_last = -z_last
+            const double d = v - (bstart ? 0.0 : vprev);
+            P.x[xi] = P.colv ? cv * d : d;
+            if (bend) P.x[xi + 1] = P.colv ? cv2 * (0.0 - v) : (0.0 - v);   // (N z)_last = -z_last
         }
     } else if (l == 0) {
         // one block longer than a wave: serial PAVA in global memory

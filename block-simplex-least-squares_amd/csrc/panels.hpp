@@ -221,6 +221,18 @@ struct SegBody {
                                          const double (&sc)[4]) const {
         const uint16_t *ent = M.ent + e0;
         const double *val = M.val + e0;
+        // diagonals DBK .. 2 DBK - 1 of every slice deeper than DBK, issued
+        // before any of the walk so their round trips overlap each other and
+        // the shallow part of the walk (a deep slice in ~30 % of the waves of a
+        // chunk made those waves the stragglers at the next barrier)
+        u32x4 ext[4];
+        if (DBK == 8) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (D[q] > DBK)
+                    ext[q] = ent8(ent, base[q] + (DBK < cnt[q] ? (uint32_t)DBK : 0u));
+            }
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if (D[q] == 0) continue;
@@ -253,7 +265,9 @@ struct SegBody {
                 if (DBK == 8) {
                     // one 16-B load per 8 diagonals; a lane whose row has ended
                     // re-reads its first entries (any in-chunk offset will do)
-                    const u32x4 w = ent8(ent, base[q] + (k0 < cnt[q] ? (uint32_t)k0 : 0u));
+                    const u32x4 w = (k0 == DBK)
+                                        ? ext[q]
+                                        : ent8(ent, base[q] + (k0 < cnt[q] ? (uint32_t)k0 : 0u));
 #pragma unroll
                     for (int k = 0; k < DBK; ++k)
                         cc[k] = (int)((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xFFFFu));
