@@ -1,0 +1,113 @@
+"""Parity at BASELINE.json's full single-GPU size (C3: 1M routes, 50k blocks,
+100k links, 16M nonzeros), the configuration bench.py measures.  Needs an
+MI355X.
+
+* K2 (g = N'A'r) bit-identical to SciPy on the whole problem;
+* K1 (r = A x + target) within 1e-12 relative of SciPy;
+* K3 (PAVA + clip + N z) bit-identical to the oracle on all 950k z entries;
+* BB iterates after 1 and 3 iterations within 1e-6 relative of the oracle's
+  restatement of BB.py over SciPy (python/BB.py:7-45, main.py:41-79);
+* the x-space operator (SparseLSQ on the panel images) against SciPy.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+@pytest.fixture(scope='module')
+def c3(cuda):
+    from synthetic import make_shard, add_noise, CONFIGS, SEED
+    from device import BBEngine
+    c = CONFIGS['C3']
+    sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+    b = add_noise(sh['Ax'], 0.02, seed=SEED)
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 3, 'opt_tol': 1e-30},
+                   AT=sh['AT'])
+    return sh, b, eng
+
+
+def test_c3_k2_bit_exact(c3, orc):
+    import torch
+    sh, b, eng = c3
+    r = np.random.RandomState(5).randn(eng.m)
+    eng.r.copy_(torch.from_numpy(r))
+    eng.stage(3, 0)
+    got = eng.g[0][:eng.nz].cpu().numpy()
+    N = orc.block_sizes_to_N(sh['block_sizes'])
+    want = N.T.tocsr().dot(sh['AT'].dot(r))
+    assert np.array_equal(got.view(np.int64), want.view(np.int64))
+
+
+def test_c3_k1_residual(c3):
+    import torch
+    sh, b, eng = c3
+    x = np.random.RandomState(6).rand(eng.n)
+    eng.x.copy_(torch.from_numpy(eng.colv.cpu().numpy() * x))
+    eng.stage(7, 0)
+    got = eng.r.cpu().numpy()
+    want = sh['A'].dot(x) + eng.target.cpu().numpy()
+    assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
+
+
+def test_c3_bb_iterates_vs_oracle(c3, orc):
+    sh, b, eng = c3
+    ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], 3, record_every=1)
+    rec = {}
+
+    def log(i, s, dt):
+        rec[i] = s
+        return 0.0
+    eng.solve(log=log, record_every=1, poll=1)
+    for i in (1, 3):
+        assert rel_err(rec[i], ref[i]) < 1e-6, (i, rel_err(rec[i], ref[i]))
+
+
+def test_c3_k3_pava_bit_exact(c3, orc):
+    """Stage 4 on the full z layout: z_new = clip01(PAVA_v1(z - t g))."""
+    import torch
+    import _native
+    sh, b, eng = c3
+    rs = np.random.RandomState(8)
+    nz = eng.nz
+    zc = rs.rand(nz)
+    g = rs.randn(nz)
+    eng.z[0][:nz].copy_(torch.from_numpy(zc))
+    eng.g[1][:nz].copy_(torch.from_numpy(g))
+    # t = dz.dg / dg.dg = 0.25 through the scalar block K3 reads
+    s = eng.scal.cpu().numpy()
+    s[_native.S_STOP] = 0.0
+    s[_native.S_SUMDG] = 1.0
+    s[_native.S_DZDG] = 0.25
+    s[_native.S_DGDG] = 1.0
+    eng.scal.copy_(torch.from_numpy(s))
+    eng.stage(4, 1)          # iteration 1 reads z[0], g[1], writes z[1]
+    got = eng.z[1][:nz].cpu().numpy()
+    y = zc - 0.25 * g
+    zs = eng.layout.zstarts_h
+    orc.isotonic_regression_multi_c(y, zs)
+    want = np.maximum(np.minimum(y, 1.0), 0.0)
+    assert np.array_equal(got.view(np.int64), want.view(np.int64))
+
+
+def test_c3_xspace_operator(c3):
+    """SparseLSQ (the x-space obj) on the C3 panels: f within 1e-12, g within
+    1e-10 of SciPy (its input residual differs by the group order only)."""
+    import torch
+    from algorithm_utils import SparseLSQ
+    sh, b, eng = c3
+    P = SparseLSQ(sh['A'], b, A_T=sh['AT'])
+    assert P.lsq is not None and P.lsq.scaled
+    x = np.random.RandomState(9).rand(sh['A'].shape[1])
+    g = torch.empty(P.n, dtype=torch.float64, device='cuda')
+    f = P(torch.from_numpy(x).cuda(), g)
+    tmp = sh['A'].dot(x) - b
+    assert abs(f - .5 * tmp.dot(tmp)) <= 1e-12 * abs(f)
+    gref = sh['AT'].dot(tmp)
+    np.testing.assert_allclose(g.cpu().numpy(), gref, rtol=1e-10,
+                               atol=1e-12 * np.abs(gref).max())
