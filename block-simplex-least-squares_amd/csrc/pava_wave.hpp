@@ -144,8 +144,9 @@ __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, dou
         const double pr = Y * (double)W;
         double num = 0.0 + pr;
         int den = W;
-        const int maxd = wave_max(inpool ? depth : 0);
-        for (int k = 1; k <= maxd; ++k) {
+        // k = 1 .. the deepest pooled member (a ballot per step instead of a
+        // six-round shuffle max up front: 2-4 steps are typical)
+        for (int k = 1; __ballot(inpool && depth >= k); ++k) {
             const double np = dpp_shr1_d(num);
             const int dp = dpp_shr1_i(den);
             if (inpool && depth == k) {
