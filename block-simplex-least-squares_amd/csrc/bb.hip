@@ -301,10 +301,13 @@ __device__ __forceinline__ int64_t xend(const bsls_bb_problem &P, int64_t b) {
 // pack of whole z-blocks (<= 64 entries, one lane each): the PAVA passes run
 // wave-parallel (pava_wave.hpp, bit-identical to the serial reference); a
 // block longer than 64 entries gets a pack of its own and the serial PAVA.
-__device__ __forceinline__ bool bb_step_t(const bsls_bb_problem &P, int64_t iter, double &t) {
+// sc = scal[STOP], scal[SUMDG], scal[DZDG], scal[DGDG], loaded by the caller
+// together with its other first loads (one round trip, not three)
+__device__ __forceinline__ bool bb_step_t(const bsls_bb_problem &P, int64_t iter,
+                                          const double (&sc)[4], double &t) {
     double *s = P.scal;
-    if (s[BSLS_S_STOP] != 0.0) return false;
-    if (P.early_exit && s[BSLS_S_SUMDG] == 0.0) {  // BB.py:22
+    if (sc[0] != 0.0) return false;
+    if (P.early_exit && sc[1] == 0.0) {  // BB.py:22
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             s[BSLS_S_STOP] = (double)BSLS_STOP_NOCHANGE;
             s[BSLS_S_ITER] = (double)iter;
@@ -312,7 +315,7 @@ __device__ __forceinline__ bool bb_step_t(const bsls_bb_problem &P, int64_t iter
         }
         return false;
     }
-    t = s[BSLS_S_DZDG] / s[BSLS_S_DGDG];
+    t = sc[2] / sc[3];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         s[BSLS_S_T] = t;
         if (fabs(t) <= 1e-10 || fabs(t) > 1e10) s[BSLS_S_WARN] += 1.0;
@@ -320,62 +323,110 @@ __device__ __forceinline__ bool bb_step_t(const bsls_bb_problem &P, int64_t iter
     return true;
 }
 
+// 8-B write-through (sc1) store through a buffer resource: the line leaves L2
+// at once instead of as a dirty line at the kernel's end (as proj.hip's
+// store-out).  Lanes whose offset is past `bytes` are dropped by the hardware.
+__device__ __forceinline__ void wt_store_f64(const __amdgpu_buffer_rsrc_t &rs, int off,
+                                             double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(
+        __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, v), rs, off, 0, 16);
+}
+
+#ifndef BSLS_K3_PPW
+#define BSLS_K3_PPW 1
+#endif
+constexpr int K3_PPW = BSLS_K3_PPW;   // packs per wave
+
+// Each wave takes K3_PPW packs (w, w + W, ...; W = waves in the grid) and
+// issues every load of all of them -- metadata, then z, g and the column
+// scales -- before the first PAVA, so the round trips of the second pack
+// overlap the first one's passes and the grid is resident in one round.
 __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
                                              const double *__restrict__ zc,
                                              const double *__restrict__ g,
                                              double *__restrict__ zn,
                                              int32_t *__restrict__ wsc) {
-    double t;
-    if (!bb_step_t(P, iter, t)) return;
-    const int64_t pk = (int64_t)blockIdx.x * 4 + threadIdx.x / WAVE;
-    if (pk >= P.npacks) return;
+    const double sc[4] = {P.scal[BSLS_S_STOP], P.scal[BSLS_S_SUMDG], P.scal[BSLS_S_DZDG],
+                          P.scal[BSLS_S_DGDG]};
     const int l = lane_id();
-    const int64_t z0 = P.pk_z0[pk], b0 = P.pk_b0[pk];
-    const int L = P.pk_len[pk];
+    const int wv = threadIdx.x / WAVE;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int64_t w0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);   // wave-uniform
     __shared__ double pv_y[4][64];
     __shared__ int pv_p[4][64];
-    if (L <= WAVE) {
-        const uint64_t B = (uint64_t)P.pk_mask[pk];
-        const bool act = l < L;
-        const bool bstart = (B >> l) & 1ull;
-        const int64_t blk = b0 + __popcll(B & mask_le(l)) - 1;
-        const int64_t xi = z0 + l + blk;                // x index of this z entry
-        const bool bend = (l == L - 1) || (l < 63 && ((B >> (l + 1)) & 1ull));
-        // the column scales of this lane's x entries, loaded before the PAVA so
-        // their round trip overlaps it (x_put's products, same arithmetic)
-        double cv = 1.0, cv2 = 1.0;
+    int64_t z0[K3_PPW], b0[K3_PPW];
+    int L[K3_PPW];
+    uint64_t B[K3_PPW];
+#pragma unroll
+    for (int q = 0; q < K3_PPW; ++q) {
+        // unconditional loads at a clamped index (straight-line, one round trip)
+        const int64_t pk = w0 + q * nw;
+        const int64_t pc = pk < P.npacks ? pk : P.npacks - 1;
+        z0[q] = P.pk_z0[pc];
+        b0[q] = P.pk_b0[pc];
+        L[q] = pk < P.npacks ? P.pk_len[pc] : 0;
+        B[q] = (uint64_t)P.pk_mask[pc];
+    }
+    double zv[K3_PPW], gv[K3_PPW], cv[K3_PPW], cv2[K3_PPW];
+#pragma unroll
+    for (int q = 0; q < K3_PPW; ++q) {
+        const bool act = l < L[q] && L[q] <= WAVE;
+        const bool bend = (l == L[q] - 1) || (l < 63 && ((B[q] >> (l + 1)) & 1ull));
+        const int64_t xi = z0[q] + l + b0[q] + __popcll(B[q] & mask_le(l)) - 1;
+        cv[q] = cv2[q] = 1.0;
         if (P.colv) {
-            cv = act ? P.colv[xi] : 1.0;
-            cv2 = (act && bend) ? P.colv[xi + 1] : 1.0;
+            // the column scales of this lane's x entries, loaded before the
+            // PAVA so their round trip overlaps it (x_put's products)
+            cv[q] = act ? P.colv[xi] : 1.0;
+            cv2[q] = (act && bend) ? P.colv[xi + 1] : 1.0;
         }
-        double y = act ? zc[z0 + l] - t * g[z0 + l] : 0.0;  // x_next = x - t g (BB.py:29)
-        const int wv = threadIdx.x / WAVE;
-        pava_v1_wave_c(y, L, B, pv_y[wv], pv_p[wv]);
-        const double v = clip01(y);
-        const double vprev = shfl_d(v, l > 0 ? l - 1 : 0);
-        if (act) {
-            zn[z0 + l] = v;
-            const double d = v - (bstart ? 0.0 : vprev);
-            P.x[xi] = P.colv ? cv * d : d;
-            if (bend) P.x[xi + 1] = P.colv ? cv2 * (0.0 - v) : (0.0 - v);   // (N z)_last = -z_last
+        zv[q] = act ? zc[z0[q] + l] : 0.0;
+        gv[q] = act ? g[z0[q] + l] : 0.0;
+    }
+    double t;
+    if (!bb_step_t(P, iter, sc, t)) return;
+#pragma unroll
+    for (int q = 0; q < K3_PPW; ++q) {
+        if (L[q] == 0) break;
+        if (L[q] <= WAVE) {
+            const bool act = l < L[q];
+            const bool bstart = (B[q] >> l) & 1ull;
+            const int bl = __popcll(B[q] & mask_le(l)) - 1;   // block within the pack
+            const bool bend = (l == L[q] - 1) || (l < 63 && ((B[q] >> (l + 1)) & 1ull));
+            double yq = act ? zv[q] - t * gv[q] : 0.0;  // x_next = x - t g (BB.py:29)
+            if (BSLS_K3_KO != 1) pava_v1_wave_c(yq, L[q], B[q], pv_y[wv], pv_p[wv]);
+            const double v = clip01(yq);
+            const double vprev = shfl_d(v, l > 0 ? l - 1 : 0);
+            const int nb = __popcll(B[q]);
+            const __amdgpu_buffer_rsrc_t rz =
+                __builtin_amdgcn_make_buffer_rsrc(zn + z0[q], 0, L[q] * 8, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+                P.x + z0[q] + b0[q], 0, (L[q] + nb) * 8, 0x00020000);
+            if (act) {
+                wt_store_f64(rz, l * 8, v);
+                const double d = v - (bstart ? 0.0 : vprev);
+                const int xo = (l + bl) * 8;
+                wt_store_f64(rx, xo, P.colv ? cv[q] * d : d);
+                if (bend) wt_store_f64(rx, xo + 8, P.colv ? cv2[q] * (0.0 - v) : (0.0 - v));
+            }
+        } else if (l == 0) {
+            // one block longer than a wave: serial PAVA in global memory
+            const int64_t xs = P.xstarts[b0[q]];
+            for (int64_t j = z0[q]; j < z0[q] + L[q]; ++j) {
+                zn[j] = zc[j] - t * g[j];
+                wsc[j] = 1;
+            }
+            pava_v1(zn, wsc, z0[q], z0[q] + L[q], 1);
+            double prev = 0.0;
+            int64_t xo = xs;
+            for (int64_t j = z0[q]; j < z0[q] + L[q]; ++j) {
+                const double v = clip01(zn[j]);
+                zn[j] = v;
+                x_put(P, xo++, v - prev);
+                prev = v;
+            }
+            x_put(P, xo, 0.0 - prev);
         }
-    } else if (l == 0) {
-        // one block longer than a wave: serial PAVA in global memory
-        const int64_t xs = P.xstarts[b0];
-        for (int64_t j = z0; j < z0 + L; ++j) {
-            zn[j] = zc[j] - t * g[j];
-            wsc[j] = 1;
-        }
-        pava_v1(zn, wsc, z0, z0 + L, 1);
-        double prev = 0.0;
-        int64_t xo = xs;
-        for (int64_t j = z0; j < z0 + L; ++j) {
-            const double v = clip01(zn[j]);
-            zn[j] = v;
-            x_put(P, xo++, v - prev);
-            prev = v;
-        }
-        x_put(P, xo, 0.0 - prev);
     }
 }
 
@@ -444,7 +495,7 @@ static void launch_k2(const bsls_bb_problem &P, const double *zc, const double *
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
                       double *zn, const BBWork &w, hipStream_t st) {
-    bb_k3<<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.wsc);
+    bb_k3<<<grid_for(P.npacks, 4 * K3_PPW), 256, 0, st>>>(P, iter, zc, g, zn, w.wsc);
 }
 
 static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t halo,

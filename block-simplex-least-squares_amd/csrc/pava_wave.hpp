@@ -17,6 +17,12 @@
 #pragma once
 #include "bsls_common.hpp"
 
+// BSLS_K3_KO (timing knock-outs, never in the product build): 1 = no PAVA in
+// K3, 2 = one pass, 3 = two passes.
+#ifndef BSLS_K3_KO
+#define BSLS_K3_KO 0
+#endif
+
 namespace bsls {
 
 // bits [0, l); l may be 64 (a 64-bit shift by 64 is undefined, and wraps on the GPU)
@@ -125,7 +131,8 @@ __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, dou
     double Y = y;
     int W = 1, BS = (int)((B >> t) & 1ull), O = t;
     int nh = L;
-    for (int pass = 0; pass <= L; ++pass) {
+    const int maxpass = BSLS_K3_KO >= 2 ? BSLS_K3_KO - 2 : L;
+    for (int pass = 0; pass <= maxpass; ++pass) {
         const bool act = t < nh;
         const double yp = dpp_shr1_d(Y);
         const bool cs = act && (BS || !(Y <= yp));     // lane 0 is always a block start
