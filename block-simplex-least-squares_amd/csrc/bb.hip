@@ -354,6 +354,7 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
     const int64_t w0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);   // wave-uniform
     __shared__ double pv_y[4][64];
     __shared__ int pv_p[4][64];
+    __shared__ int pv_c[4][65];
     int64_t z0[K3_PPW], b0[K3_PPW];
     int L[K3_PPW];
     uint64_t B[K3_PPW];
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
             const int bl = __popcll(B[q] & mask_le(l)) - 1;   // block within the pack
             const bool bend = (l == L[q] - 1) || (l < 63 && ((B[q] >> (l + 1)) & 1ull));
             double yq = act ? zv[q] - t * gv[q] : 0.0;  // x_next = x - t g (BB.py:29)
-            if (BSLS_K3_KO != 1) pava_v1_wave_c(yq, L[q], B[q], pv_y[wv], pv_p[wv]);
+            if (BSLS_K3_KO != 1) pava_v1_wave_c(yq, L[q], B[q], pv_y[wv], pv_p[wv], pv_c[wv]);
             const double v = clip01(yq);
             const double vprev = shfl_d(v, l > 0 ? l - 1 : 0);
             const int nb = __popcll(B[q]);

@@ -123,10 +123,12 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// y: this lane's element (lanes < L); B: block starts (bit 0 set).  ys / ps:
-// this wave's 64 doubles / 64 ints of LDS.  On return y = the expanded fit.
+// y: this lane's element (lanes < L); B: block starts (bit 0 set).  ys / ps /
+// cst: this wave's 64 doubles / 64 ints / 65 ints of LDS.  On return y = the
+// expanded fit.  (The pass is VALU-bound: chain bounds come from a chain-start
+// table in LDS, not from 64-bit mask searches.)
 __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, double *ys,
-                                               int *ps) {
+                                               int *ps, int *cst) {
     const int t = lane_id();
     double Y = y;
     int W = 1, BS = (int)((B >> t) & 1ull), O = t;
@@ -137,16 +139,20 @@ __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, dou
         const double yp = dpp_shr1_d(Y);
         const bool cs = act && (BS || !(Y <= yp));     // lane 0 is always a block start
         const uint64_t CS = __ballot(cs);
-        const uint64_t above = CS & ~mask_le(t);
-        const int nxt = above ? lo_bit(above) : nh;    // next chain start
-        const int last = (nxt > 0 ? nxt : 1) - 1;      // this chain's last run
+        // chain c of this lane (lanes >= nh: the last chain, unused); the
+        // table holds every chain's first run, then nh
+        const int c = mbcnt64(CS) - (cs ? 0 : 1);
+        if (cs) cst[c] = t;
+        if (t == 0) cst[__popcll(CS)] = nh;
+        const int mycs = cst[c], nxt = cst[c + 1];
+        const int last = nxt - 1;                      // this chain's last run
+        const double yfirst = shfl_d(Y, mycs);
         const double ylast = shfl_d(Y, last);
-        const bool pool = cs && (Y != ylast);
-        const uint64_t POOL = __ballot(pool);
-        if (!POOL) break;
-        const uint64_t csle = CS & mask_le(t);
-        const int mycs = csle ? hi_bit(csle) : 0;
-        const bool inpool = act && ((POOL >> mycs) & 1ull);
+        // the chain pools iff its first and last values differ (the reference's
+        // y[i] != y[j]); every member sees both
+        const bool inpool = act && (yfirst != ylast);
+        const bool pool = cs && inpool;
+        if (!__ballot(pool)) break;
         const int depth = t - mycs;
         const double pr = Y * (double)W;
         double num = 0.0 + pr;
@@ -156,10 +162,9 @@ __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, dou
         for (int k = 1; __ballot(inpool && depth >= k); ++k) {
             const double np = dpp_shr1_d(num);
             const int dp = dpp_shr1_i(den);
-            if (inpool && depth == k) {
-                num = np + pr;
-                den = dp + W;
-            }
+            const bool upd = inpool && depth == k;
+            num = upd ? np + pr : num;
+            den = upd ? dp + W : den;
         }
         const double tn = shfl_d(num, last);
         const int td = shfl_i(den, last);
