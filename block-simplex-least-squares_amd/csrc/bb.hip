@@ -16,10 +16,10 @@
 //       range.  N is never materialised.
 //   K1  r = A (N z) + target, target = A x0 - b, exactly the reference's
 //       A.dot(N.dot(z)) + target.  A in panel format with its column chunks
-//       split into 8 groups, group = blockIdx % 8 (one XCD: the group's slice
-//       of x stays in that XCD's L2 while its 32 workgroups stage it chunk by
-//       chunk into LDS) and publishes one partial per (row, group); the last
-//       of a row block's 8 workgroups sums them in group order, adds target,
+//       split into G groups (device.k1_plan: C3 10), group = blockIdx % G;
+//       each workgroup stages its group's slice of x chunk by chunk into LDS
+//       and publishes one partial per (row, group); the last of a row
+//       block's G workgroups sums them in group order, adds target,
 //       ||r||^2 (next gradient's residual AND f(z)); the last row block runs
 //       the stopping test.
 //   For a scaled incidence A (bsls_utils.py:494) the values are not stored:

@@ -16,6 +16,8 @@ sequences calls.
 import ctypes
 import time
 
+import os
+
 import numpy as np
 import scipy.sparse as sps
 
@@ -272,11 +274,29 @@ def panel_rows(rows, workgroups_per_group, waves=16):
     return int(min(_native.PANEL_ROWS, max(min(64, rows), want)))
 
 
+def k1_plan(m, cus=256, max_groups=10):
+    """(rows per panel, column groups) of the A image (K1, lsq_k1): as many
+    column groups as keep the launch (groups x row blocks of 16 panels) within
+    one workgroup per CU with panels as tall as they go (<= BSLS_PANEL_ROWS),
+    i.e. full 64-row slices and fewer chunks per workgroup.  C3 (m = 100k):
+    10 groups x 25 row blocks of 250-row panels, K1 42.8 us against 45.8 us
+    for 8 x 32 of 196 rows (whose fourth slice held 4 rows).
+    BSLS_K1_PLAN="groups,wg" overrides it (A/B timing of plans)."""
+    plan = os.environ.get('BSLS_K1_PLAN')
+    if plan:
+        groups, wg = (int(v) for v in plan.split(','))
+        return panel_rows(m, wg), groups
+    rbs_min = -(-m // (16 * _native.PANEL_ROWS))
+    groups = max(1, min(max_groups, cus // max(1, rbs_min)))
+    rbs = max(rbs_min, cus // groups)
+    return panel_rows(m, rbs), groups
+
+
 class DeviceLSQ:
     """The x-space operator pair on panel images (csrc/lsq.hip, struct
     bsls_lsq_op): residual r = A x + add with ||r||^2, gradient g = A' r.
     sparse_least_squares_obj's two SciPy products (algorithm_utils.py:88-94).
-    A: 8 XCD column groups, no halo; A': one group.  A scaled incidence drops
+    A: column groups (k1_plan), no halo; A': one group.  A scaled incidence drops
     the values (colv * x formed once per residual, A' entries scaled by colv
     row by row: g stays bit-identical to SciPy's csr_matvec)."""
 
@@ -288,7 +308,8 @@ class DeviceLSQ:
         self.m, self.n = A.shape
         colv = None if general else scaled_incidence_scale(A)
         self.scaled = colv is not None
-        self.A_pan = DevicePanels(A, panel_rows(self.m, 32), False, 8, values=not self.scaled)
+        prow, groups = k1_plan(self.m)
+        self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
         self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), False, 1,
                                    values=not self.scaled)
         dev = dict(dtype=torch.float64, device='cuda')
@@ -394,11 +415,12 @@ class BBEngine:
         self.A = A_dev or DeviceCSR(A)
         self.AT = AT_dev or DeviceCSR(AT)
         self.m, self.n, self.nz = A.shape[0], lay.n, lay.nz
-        # the fused kernels' panel images: A with its column chunks in 8 XCD
+        # the fused kernels' panel images: A with its column chunks in k1_plan's
         # groups (K1), A' with halo rows (K2); values dropped for a scaled incidence
         colv = None if general else scaled_incidence_scale(A)
         self.scaled = colv is not None
-        self.A_pan = DevicePanels(A, panel_rows(self.m, 32), False, 8, values=not self.scaled)
+        prow, groups = k1_plan(self.m)
+        self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
         self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), True, 1,
                                    values=not self.scaled)
         opts = options or {}

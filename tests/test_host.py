@@ -230,6 +230,21 @@ def test_panel_rows_choice():
     assert device.panel_rows(10_000_000, 256) == 255
 
 
+def test_k1_plan_fits_one_round(monkeypatch):
+    """The A-image plan: C3 gets 10 column groups x 25 row blocks of 250-row
+    panels; every m stays within one workgroup per CU (256) and <= 255 rows."""
+    import device
+    monkeypatch.delenv('BSLS_K1_PLAN', raising=False)
+    assert device.k1_plan(100_000) == (250, 10)
+    for m in (1, 100, 5_000, 100_000, 200_000, 1_000_000, 4_000_000):
+        prow, groups = device.k1_plan(m)
+        assert 1 <= prow <= 255 and 1 <= groups <= 10
+        rbs = -(-(-(-m // prow)) // 16)
+        assert groups * rbs <= 256 or groups == 1, (m, prow, groups, rbs)
+    monkeypatch.setenv('BSLS_K1_PLAN', '8,32')
+    assert device.k1_plan(100_000) == (196, 8)
+
+
 def test_batch_stopping_matches_oracle(orc):
     """algorithm_utils.stopping (python/algorithm_utils.py:158-172): the last
     true test names the reason."""
