@@ -12,8 +12,9 @@
 //       stays in the wave; fused: dg, the four BB sums, the store of g.
 //   K3  t from the sums; per z-block PAVA (v1 pooling order, bit-identical to
 //       isotonic_regression.h:13-58) + clip to [0,1] + the vector N z (per-block
-//       differences, last entry -z_last), one lane per block over an LDS-staged
-//       range.  N is never materialised.
+//       differences, last entry -z_last), one wave per pack of whole blocks
+//       (<= 64 entries, one lane per entry, pava_wave.hpp).  N is never
+//       materialised.
 //   K1  r = A (N z) + target, target = A x0 - b, exactly the reference's
 //       A.dot(N.dot(z)) + target.  A in panel format with its column chunks
 //       split into G groups (device.k1_plan: C3 10), group = blockIdx % G;
@@ -199,8 +200,11 @@ __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t it
 // K2: g = N'(A' r); with ITER also dg = g - g_prev and the BB sums.  The
 // workgroup's 16 panels (x-rows) are summed over every chunk of r; then lane
 // position p of a panel has w_i in acc[p] and w_{i+1} in acc[p + 1] (the halo
-// row), so N'w = w_i - w_{i+1} needs no exchange.  The epilogue operands are
-// loaded before the chunk loop so their latency overlaps it.
+// row), so N'w = w_i - w_{i+1} needs no exchange.  The column scales are
+// loaded before the chunk loop; the epilogue's z indices and operands after
+// it (the walk holds 122 of the 128 VGPRs; loading the indices early measured
+// no faster).  The ITER epilogue costs ~8 us: 22.8 MB of g_prev / z / z_prev
+// reads that no walk overlaps.
 template <int MODE, bool ITER>
 __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *__restrict__ zc,
                                               const double *__restrict__ zp,

@@ -152,10 +152,16 @@ def test_k3_wave_pava_bit_exact(cuda, orc):
     A = sps.random(m, n, density=0.02, random_state=rs, format='csr')
     eng = BBEngine(A, rs.randn(m), sizes, options={'max_iter': 10, 'opt_tol': 1e-30})
     nz = eng.nz
-    for trial in range(3):
+    for trial in range(5):
         zc = np.cumsum(rs.rand(nz)) * 0.01 if trial == 0 else rs.randn(nz)
         g = rs.randn(nz) * (0.5 if trial < 2 else 50.0)
-        t = [1.0, 0.37, 3.0][trial]
+        if trial >= 3:
+            # ties: runs of equal values (equal-valued chains must not pool,
+            # and pooled runs meet equal neighbours), and signed zeros
+            zc = np.round(rs.randn(nz), 0 if trial == 3 else 1)
+            zc[rs.rand(nz) < 0.1] = -0.0
+            g = np.zeros(nz)
+        t = [1.0, 0.37, 3.0, 1.0, 1.0][trial]
         eng.z[0][:nz].copy_(torch.from_numpy(zc))
         eng.g[1][:nz].copy_(torch.from_numpy(g))
         sc = np.zeros(_native.S_COUNT)
