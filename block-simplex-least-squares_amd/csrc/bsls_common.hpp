@@ -259,11 +259,12 @@ __device__ bool last_block_reduce(const double (&mine)[NV], double *partials, un
     return true;
 }
 
-// numpy.minimum(v, 1.) then numpy.maximum(., 0.) (python/main.py:65):
-// NaN propagates, -0.0 is kept.
+// numpy.minimum(v, 1.) then numpy.maximum(., 0.) (python/main.py:65) as
+// numpy 2.x computes them: NaN propagates, and on a tie maximum returns its
+// second operand, so maximum(-0.0, 0.) is +0.0 (a -0.0 input leaves as +0.0).
 __device__ __forceinline__ double clip01(double v) {
     double a = (v > 1.0) ? 1.0 : v;
-    return (a < 0.0) ? 0.0 : a;
+    return (a > 0.0 || a != a) ? a : 0.0;
 }
 
 // std::max(v, 0.) as in proj_simplex.h:33.

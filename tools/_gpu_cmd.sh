@@ -1,3 +1,3 @@
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_bb.py tests/test_gpu_fullsize.py > gpurun_out/tests.log 2>&1 || exit 1
-timeout -k 10 200 python3 tools/stage_time.py --iters 100 > gpurun_out/ko.log 2>&1 && timeout -k 10 200 python3 tools/stage_time.py --iters 100 >> gpurun_out/ko.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_bb.py -k "k3 or deterministic" > gpurun_out/tests.log 2>&1 || exit 1
+timeout -k 10 200 python3 tools/iso_time.py > gpurun_out/iso.log 2>&1
