@@ -40,6 +40,7 @@ struct BBWork {
     unsigned *tk1, *tk2, *tkf, *tkrb;
     double *p1, *p2, *pf;
     int32_t *wsc;
+    double *dz;   // z - z_prev, written by K3 (and the prologue) for the next K2
     size_t bytes;
 };
 
@@ -64,6 +65,8 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     off += al16((size_t)((m + 255) / 256 + 1) * 8);
     w.wsc = (int32_t *)(p + off);
     off += al16((size_t)(nz > 0 ? nz : 1) * 4);
+    w.dz = (double *)(p + off);
+    off += al16((size_t)(nz > 0 ? nz : 1) * 8);
     w.bytes = off;
     return w;
 }
@@ -203,11 +206,11 @@ __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t it
 // row), so N'w = w_i - w_{i+1} needs no exchange.  The column scales are
 // loaded before the chunk loop; the epilogue's z indices and operands after
 // it (the walk holds 122 of the 128 VGPRs; loading the indices early measured
-// no faster).  The ITER epilogue costs ~8 us: 22.8 MB of g_prev / z / z_prev
-// reads that no walk overlaps.
+// no faster).  The ITER epilogue reads g_prev and dz = z - z_prev (K3 wrote
+// dz from the z's it holds, bit-identical to the subtraction here): 15.2 MB
+// that no walk overlaps, where z and z_prev were 22.8 MB.
 template <int MODE, bool ITER>
-__global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *__restrict__ zc,
-                                              const double *__restrict__ zp,
+__global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *__restrict__ dzv,
                                               const double *__restrict__ gp,
                                               double *__restrict__ gout, double *part,
                                               unsigned *ticket) {
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
     double sums[4] = {0.0, 0.0, 0.0, 0.0};
     // epilogue operands: unconditional loads at clamped indices, all in flight
     int32_t j[4];
-    double gpj[4], zcj[4], zpj[4];
+    double gpj[4], dzj[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int pos = 64 * q + lane;
@@ -258,8 +261,7 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
         for (int q = 0; q < 4; ++q) {
             const int32_t jc = j[q] >= 0 ? j[q] : 0;
             gpj[q] = gp[jc];
-            zcj[q] = zc[jc];
-            zpj[q] = zp[jc];
+            dzj[q] = dzv[jc];
         }
     }
 #pragma unroll
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
             gout[j[q]] = g;
             if (ITER) {
                 const double dg = g - gpj[q];
-                const double dz = zcj[q] - zpj[q];
+                const double dz = dzj[q];
                 sums[0] += dg;
                 sums[1] += dz * dg;
                 sums[2] += dg * dg;
@@ -349,6 +351,7 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
                                              const double *__restrict__ zc,
                                              const double *__restrict__ g,
                                              double *__restrict__ zn,
+                                             double *__restrict__ dzo,
                                              int32_t *__restrict__ wsc) {
     const double sc[4] = {P.scal[BSLS_S_STOP], P.scal[BSLS_S_SUMDG], P.scal[BSLS_S_DZDG],
                           P.scal[BSLS_S_DGDG]};
@@ -405,10 +408,13 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
             const int nb = __popcll(B[q]);
             const __amdgpu_buffer_rsrc_t rz =
                 __builtin_amdgcn_make_buffer_rsrc(zn + z0[q], 0, L[q] * 8, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rd =
+                __builtin_amdgcn_make_buffer_rsrc(dzo + z0[q], 0, L[q] * 8, 0x00020000);
             const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
                 P.x + z0[q] + b0[q], 0, (L[q] + nb) * 8, 0x00020000);
             if (act) {
                 wt_store_f64(rz, l * 8, v);
+                wt_store_f64(rd, l * 8, v - zv[q]);   // next K2's z - z_prev
                 const double d = v - (bstart ? 0.0 : vprev);
                 const int xo = (l + bl) * 8;
                 wt_store_f64(rx, xo, P.colv ? cv[q] * d : d);
@@ -427,6 +433,7 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
             for (int64_t j = z0[q]; j < z0[q] + L[q]; ++j) {
                 const double v = clip01(zn[j]);
                 zn[j] = v;
+                dzo[j] = v - zc[j];
                 x_put(P, xo++, v - prev);
                 prev = v;
             }
@@ -437,9 +444,14 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
 
 // Prologue helpers (BB.py:14-15: x_prev = x + 1); bb_z2x writes N z.
 __global__ __launch_bounds__(256) void bb_plus_one(const double *__restrict__ a,
-                                                   double *__restrict__ o, int64_t nz) {
+                                                   double *__restrict__ o,
+                                                   double *__restrict__ dz, int64_t nz) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nz) o[i] = a[i] + 1;
+    if (i < nz) {
+        const double v = a[i], w = v + 1;
+        o[i] = w;
+        dz[i] = v - w;   // iteration 1's z - z_prev
+    }
 }
 
 __global__ __launch_bounds__(256) void bb_z2x(bsls_bb_problem P, const double *__restrict__ z) {
@@ -484,23 +496,23 @@ static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, h
 }
 
 template <int MODE, bool ITER>
-static void launch_k2_mode(const bsls_bb_problem &P, const double *zc, const double *zp,
-                           const double *gp, double *gout, const BBWork &w, hipStream_t st) {
+static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *gout,
+                           const BBWork &w, hipStream_t st) {
     allow_lds(bb_k2<MODE, ITER>);
     bb_k2<MODE, ITER><<<grid_for(P.AT.npanels, PANEL_WAVES), 1024, panel_lds_bytes(P.AT), st>>>(
-        P, zc, zp, gp, gout, w.p2, w.tk2);
+        P, w.dz, gp, gout, w.p2, w.tk2);
 }
 
 template <bool ITER>
-static void launch_k2(const bsls_bb_problem &P, const double *zc, const double *zp,
-                      const double *gp, double *gout, const BBWork &w, hipStream_t st) {
-    if (P.colv) launch_k2_mode<2, ITER>(P, zc, zp, gp, gout, w, st);
-    else launch_k2_mode<1, ITER>(P, zc, zp, gp, gout, w, st);
+static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
+                      const BBWork &w, hipStream_t st) {
+    if (P.colv) launch_k2_mode<2, ITER>(P, gp, gout, w, st);
+    else launch_k2_mode<1, ITER>(P, gp, gout, w, st);
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
                       double *zn, const BBWork &w, hipStream_t st) {
-    bb_k3<<<grid_for(P.npacks, 4 * K3_PPW), 256, 0, st>>>(P, iter, zc, g, zn, w.wsc);
+    bb_k3<<<grid_for(P.npacks, 4 * K3_PPW), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
 }
 
 static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t halo,
@@ -558,15 +570,15 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
             bb_r_finish<<<grid_for(P.m, 256), 256, 0, st>>>(P, iter, w.pf, w.tkf);
             break;
         case 3:  // g = N'A'r (+ sums)
-            if (iter > 0) launch_k2<true>(P, P.z[zc], P.z[zn], P.g[zc], P.g[zn], w, st);
-            else launch_k2<false>(P, nullptr, nullptr, nullptr, P.g[0], w, st);
+            if (iter > 0) launch_k2<true>(P, P.g[zc], P.g[zn], w, st);
+            else launch_k2<false>(P, nullptr, P.g[0], w, st);
             break;
         case 4:  // t, projection, x
             if (iter <= 0) return BSLS_E_ARG;
             launch_k3(P, iter, P.z[zc], P.g[zn], P.z[zn], w, st);
             break;
         case 5:  // z[1] = z[0] + 1; x = N z[1]
-            bb_plus_one<<<grid_for(P.nz > 0 ? P.nz : 1, 256), 256, 0, st>>>(P.z[0], P.z[1], P.nz);
+            bb_plus_one<<<grid_for(P.nz > 0 ? P.nz : 1, 256), 256, 0, st>>>(P.z[0], P.z[1], w.dz, P.nz);
             BSLS_LAUNCH_CHECK();
             bb_z2x<<<grid_for(P.nblocks, 256), 256, 0, st>>>(P, P.z[1]);
             break;
@@ -612,7 +624,7 @@ extern "C" int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int
     const BBWork w = bb_layout(P);
     for (int64_t i = first_iter; i < first_iter + count; ++i) {
         const int zc = (int)((i - 1) & 1), zn = (int)(i & 1);
-        launch_k2<true>(P, P.z[zc], P.z[zn], P.g[zc], P.g[zn], w, st);
+        launch_k2<true>(P, P.g[zc], P.g[zn], w, st);
         launch_k3(P, i, P.z[zc], P.g[zn], P.z[zn], w, st);
         launch_k1<true, true, true>(P, i, w, st);
         BSLS_LAUNCH_CHECK();
