@@ -199,7 +199,9 @@ typedef struct bsls_bb_problem {
     double *x;                      /* n: N z of the current iterate (x0 is in target), times colv if set */
     double *r;                      /* m: residual */
     double *scal;                   /* BSLS_S_COUNT doubles */
-    void *work;                     /* bsls_bb_workspace_size() bytes */
+    void *work;                     /* bsls_bb_workspace_size() bytes; holds dz = z - z_prev
+                                     * between iterations, so z[] must not be
+                                     * changed between prologue and iterate calls */
     int64_t max_zblock;             /* largest z-block (x-block size - 1) */
     int64_t max_iter;               /* options['max_iter'] */
     double opt_tol;                 /* options['opt_tol'] */
@@ -221,7 +223,7 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  *   2  r += target, ||r||^2, f, stopping test of iteration `iter` (iter 0: none)
  *   3  g = N'A'r -> g[iter & 1]; iter > 0 also dg and the four BB sums into
  *      scal[SUMDG..GG] (all-reduce those four afterwards)
- *   4  t from the sums, z[iter&1] = clip01(PAVA(z - t g)), x = N z
+ *   4  t from the sums, z[iter&1] = clip01(PAVA(z - t g)), x = N z, dz for stage 3
  *   5  z[1] = z[0] + 1, x = N z[1]           (prologue)
  *   6  x = N z[0]                             (prologue)
  *   7  single GCD: r = A x + target, ||r||^2, f, stopping test (= 1 then 2 fused)
