@@ -342,6 +342,9 @@ __device__ __forceinline__ void wt_store_f64(const __amdgpu_buffer_rsrc_t &rs, i
 #define BSLS_K3_PPW 1
 #endif
 constexpr int K3_PPW = BSLS_K3_PPW;   // packs per wave
+#ifndef BSLS_DZ_PLAIN
+#define BSLS_DZ_PLAIN 0   // 1: dz through an ordinary store (A/B variant)
+#endif
 
 // Each wave takes K3_PPW packs (w, w + W, ...; W = waves in the grid) and
 // issues every load of all of them -- metadata, then z, g and the column
@@ -414,7 +417,11 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
                 P.x + z0[q] + b0[q], 0, (L[q] + nb) * 8, 0x00020000);
             if (act) {
                 wt_store_f64(rz, l * 8, v);
+#if BSLS_DZ_PLAIN
+                dzo[z0[q] + l] = v - zv[q];
+#else
                 wt_store_f64(rd, l * 8, v - zv[q]);   // next K2's z - z_prev
+#endif
                 const double d = v - (bstart ? 0.0 : vprev);
                 const int xo = (l + bl) * 8;
                 wt_store_f64(rx, xo, P.colv ? cv[q] * d : d);
