@@ -49,6 +49,17 @@ class Panels(ctypes.Structure):
                 ('seg_info', _vp), ('cnt', _vp), ('ent', _vp), ('val', _vp)]
 
 
+TILE_THREADS = 1024       # BSLS_TILE_THREADS
+TILE_MAXSLOTS = 20        # BSLS_TILE_MAXSLOTS
+
+
+class Tiles(ctypes.Structure):
+    """Mirror of struct bsls_tiles (include/bsls_hip.h)."""
+    _fields_ = [('rows', _i64), ('cols', _i64), ('H', _i64), ('halo', _i64), ('nrb', _i64),
+                ('ngroups', _i64), ('order', _i64), ('nquads', _i64), ('group_col', _vp),
+                ('wave_off', _vp), ('ent', _vp), ('val', _vp)]
+
+
 class BBProblem(ctypes.Structure):
     """Mirror of struct bsls_bb_problem (include/bsls_hip.h)."""
     _fields_ = [('m', _i64), ('n', _i64), ('nz', _i64), ('nblocks', _i64),
@@ -59,7 +70,8 @@ class BBProblem(ctypes.Structure):
                 ('z', _vp * 2), ('g', _vp * 2), ('x', _vp), ('r', _vp), ('scal', _vp),
                 ('work', _vp),
                 ('max_zblock', _i64), ('max_iter', _i64), ('opt_tol', _dbl),
-                ('early_exit', _i32), ('reserved', _i32)]
+                ('early_exit', _i32), ('reserved', _i32),
+                ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz)]
 
 
 class CSR(ctypes.Structure):
@@ -128,6 +140,8 @@ _SIGS = {
                                     _sz, _vp]),
     'bsls_md_update': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _vp, _vp, _sz, _vp]),
     'bsls_md_workspace_size': (_sz, [_i64]),
+    'bsls_tiles_build': (_i64, [_i64, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp,
+                                _i64]),
     'bsls_version': (ctypes.c_char_p, []),
     'bsls_device_arch': (_int, [ctypes.c_char_p, _int]),
 }
@@ -228,5 +242,32 @@ def declared_symbols():
     """Every function name declared in include/bsls_hip.h."""
     import re
     text = open(HEADER).read()
-    return sorted(set(re.findall(r'^\s*(?:size_t|int|const char \*)\s*(bsls_\w+)\s*\(',
+    return sorted(set(re.findall(r'^\s*(?:size_t|int64_t|int|const char \*)\s*(bsls_\w+)\s*\(',
                                  text, re.M)))
+
+
+def tiles_build(M, H, halo, group_col, values=True):
+    """Host arrays of the tile image of CSR matrix M (bsls_tiles_build, host only):
+    dict(wave_off, ent, val or None, nquads)."""
+    import numpy as np
+    ip = np.ascontiguousarray(M.indptr, dtype=np.int64)
+    ix = np.ascontiguousarray(M.indices, dtype=np.int32)
+    dv = np.ascontiguousarray(M.data, dtype=np.float64) if values else None
+    gc = np.ascontiguousarray(group_col, dtype=np.int64)
+    R, C = M.shape
+    G = gc.shape[0] - 1
+    L = load()
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data) if a is not None else ctypes.c_void_p(0)
+    nq = L.bsls_tiles_build(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc), None, None,
+                            None, 0)
+    if nq < 0:
+        raise ValueError('tile image: invalid layout (H %d, halo %d, %d groups)' % (H, halo, G))
+    nrb = -(-R // int(H))
+    wo = np.zeros(nrb * G * 16 + 1, dtype=np.int64)
+    ent = np.zeros(4 * nq + 256, dtype=np.uint32)
+    val = np.zeros(4 * nq + 256, dtype=np.float64) if values else None
+    rc = L.bsls_tiles_build(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc), vp(wo),
+                            vp(ent), vp(val), nq)
+    if rc != nq:
+        raise RuntimeError('bsls_tiles_build failed (%d)' % rc)
+    return dict(wave_off=wo, ent=ent, val=val, nquads=int(nq), nrb=nrb)

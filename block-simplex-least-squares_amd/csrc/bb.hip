@@ -26,18 +26,22 @@
 //   For a scaled incidence A (bsls_utils.py:494) the values are not stored:
 //   K3 writes colv * (N z) (the same products SciPy forms), K2 multiplies by
 //   the row's colv.
+// Sparse row blocks (C5: 1M links, ~0.3 entries per row per panel chunk) take
+// the streamed-tile format instead of the panels for K1 and/or K2 (tiles.hpp;
+// bb_k1t / bb_k2t, chosen per matrix by the host: P.At / P.ATt).
 // Every cross-workgroup sum is reduced in a fixed order by the last-arriving
 // workgroup (bsls_common.hpp last_block_sum), so runs are bit-reproducible.
 // Scalars live in device memory (scal[]); the host only polls them.
 #include "pava.hpp"
 #include "pava_wave.hpp"
 #include "panels.hpp"
+#include "tiles.hpp"
 
 namespace bsls {
 
 
 struct BBWork {
-    unsigned *tk1, *tk2, *tkf, *tkrb;
+    unsigned *tk1, *tk2, *tkf, *tkrb, *tk2rb;
     double *p1, *p2, *pf;
     int32_t *wsc;
     double *dz;   // z - z_prev, written by K3 (and the prologue) for the next K2
@@ -57,6 +61,8 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     off += al16(3 * TICKET_BYTES);
     w.tkrb = (unsigned *)(p + off);              // K1: one ticket per row block
     off += al16((size_t)(m / 16 + 2) * 4);
+    w.tk2rb = (unsigned *)(p + off);             // K2 tiles: one ticket per row block (H >= 64)
+    off += al16((size_t)(n / 64 + 2) * 4);
     w.p1 = (double *)(p + off);
     off += al16((size_t)((m + 255) / 256 + 1) * 8);
     w.p2 = (double *)(p + off);
@@ -98,6 +104,62 @@ __device__ __forceinline__ void bb_record_f(const bsls_bb_problem &P, int64_t it
         s[BSLS_S_ZBUF] = (double)(iter & 1);
         bb_stop_check(P, iter, fx);
     }
+}
+
+// K1's finish for row block rb (rows [r0, r1)), run by one workgroup: r =
+// the G partials of each row summed in group order (from rpart, or from LDS
+// `local` when the block had one group) + target; its share of ||r||^2 goes
+// to the last row block, which records f and runs the stopping test.
+template <bool ADD, bool REDUCE>
+__device__ __forceinline__ void k1_finish(const bsls_bb_problem &P, int64_t iter, bool iterating,
+                                          int64_t rb, unsigned nrb, int64_t r0, int64_t r1,
+                                          int64_t G, const double *local, double *part,
+                                          unsigned *ticket, double *red) {
+    double sq[1] = {0.0};
+    if (local) {
+        for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x) {
+            double o = local[row - r0];
+            if (ADD) o += P.target[row];
+            P.r[row] = o;
+            sq[0] += o * o;
+        }
+    } else {
+        // up to RPT rows per thread, every partial load of them in flight at once
+        constexpr int RPT = 4;
+        for (int64_t row0 = r0 + threadIdx.x; row0 < r1; row0 += RPT * blockDim.x) {
+            double v[RPT][8];
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int64_t row = row0 + (int64_t)u * blockDim.x;
+                const int64_t rr = row < r1 ? row : r0;
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    v[u][c] = (c < G) ? __hip_atomic_load(&P.rpart[c * P.m + rr], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int64_t row = row0 + (int64_t)u * blockDim.x;
+                if (row >= r1) continue;
+                double o = v[u][0];
+#pragma unroll
+                for (int c = 1; c < 8; ++c)
+                    if (c < G) o += v[u][c];
+                for (int64_t c = 8; c < G; ++c)
+                    o += __hip_atomic_load(&P.rpart[c * P.m + row], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (ADD) o += P.target[row];
+                P.r[row] = o;
+                sq[0] += o * o;
+            }
+        }
+    }
+    if (!REDUCE) return;
+    block_sum<1>(sq, red);
+    double tot[1];
+    if (last_of_sum<1>(sq, part, (unsigned)rb, nrb, ticket, tot, red) && threadIdx.x == 0)
+        bb_record_f(P, iter, tot[0], iterating);
 }
 
 // K1: workgroup (group g = blockIdx % ngroups, panels 16 rb .. 16 rb + 15)
@@ -143,43 +205,145 @@ __global__ __launch_bounds__(1024) void bb_k1(bsls_bb_problem P, int64_t iter, u
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int64_t r0 = rb * PANEL_WAVES * M.prow;
     const int64_t r1 = (r0 + PANEL_WAVES * M.prow < P.m) ? r0 + PANEL_WAVES * M.prow : P.m;
-    double sq[1] = {0.0};
-    // up to RPT rows per thread, every partial load of them in flight at once
-    constexpr int RPT = 4;
-    for (int64_t row0 = r0 + threadIdx.x; row0 < r1; row0 += RPT * blockDim.x) {
-        double v[RPT][8];
-#pragma unroll
-        for (int u = 0; u < RPT; ++u) {
-            const int64_t row = row0 + (int64_t)u * blockDim.x;
-            const int64_t rr = row < r1 ? row : r0;
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                v[u][c] = (c < G) ? __hip_atomic_load(&P.rpart[c * P.m + rr], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0.0;
+    const unsigned nrb = (unsigned)((M.npanels + PANEL_WAVES - 1) / PANEL_WAVES);
+    k1_finish<ADD, REDUCE>(P, iter, ITER, rb, nrb, r0, r1, G, nullptr, part, ticket, lds);
+}
+
+// K1 on a tile image (tiles.hpp): workgroup (rb, g) sums its rows over group
+// g's columns of x in LDS; with one group it finishes the block itself,
+// otherwise it publishes its partials (rpart, sc1) and the last of the block's
+// G workgroups finishes (group order) -- as bb_k1.
+template <int MODE, bool ITER, bool ADD, bool REDUCE>
+__global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, unsigned *tkrb,
+                                               double *part, unsigned *ticket) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ double red[16];
+    __shared__ int row_last;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    const bsls_tiles &T = P.At;
+    int64_t rb, g;
+    tile_map(T, blockIdx.x, rb, g);
+    const int HR = (int)tile_lds_doubles(T, false);
+    for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;
+    __syncthreads();
+    tile_walk<MODE>(T, rb, g, P.x, lds, nullptr);
+    __syncthreads();
+    const int64_t G = T.ngroups;
+    const int64_t r0 = rb * T.H, r1 = (r0 + T.H < P.m) ? r0 + T.H : P.m;
+    if (G == 1) {
+        k1_finish<ADD, REDUCE>(P, iter, ITER, rb, (unsigned)T.nrb, r0, r1, 1, lds, part, ticket,
+                               red);
+        return;
+    }
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+        __hip_atomic_store(&P.rpart[g * P.m + row], lds[row - r0], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev =
+            __hip_atomic_fetch_add(&tkrb[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        row_last = (prev == (unsigned)G - 1);
+        if (row_last) __hip_atomic_store(&tkrb[rb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!row_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    k1_finish<ADD, REDUCE>(P, iter, ITER, rb, (unsigned)T.nrb, r0, r1, G, nullptr, part, ticket,
+                           red);
+}
+
+// K2 on a tile image: w = A'r for row block rb (+ its halo row) in LDS, summed
+// over r's column groups (one group: in CSR order, bit-identical to SciPy;
+// several: partials in wpart, summed in group order by the block's last
+// workgroup); then g = N'w, dg and the four BB sums, as bb_k2.  MODE 1: stored
+// values; MODE 2: scaled incidence (each term colv[row] * r_i, SciPy's product).
+template <int MODE, bool ITER>
+__global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
+                                               const double *__restrict__ gp,
+                                               double *__restrict__ gout, double *part,
+                                               unsigned *ticket, unsigned *tk2rb) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ double red[4 * 16];
+    __shared__ int row_last;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    const bsls_tiles &T = P.ATt;
+    int64_t rb, g;
+    tile_map(T, blockIdx.x, rb, g);
+    const int HR = (int)tile_lds_doubles(T, false);
+    double *rows = lds;
+    double *rc = lds + HR;
+    const int64_t i0 = rb * T.H;
+    const int64_t nloc = (i0 + T.H + 1 <= P.n) ? T.H + 1 : P.n - i0;   // rows incl. the halo
+    for (int i = threadIdx.x; i < HR; i += blockDim.x) {
+        rows[i] = 0.0;
+        if (MODE == 2) rc[i] = (i < nloc) ? P.colv[i0 + i] : 0.0;
+    }
+    __syncthreads();
+    tile_walk<MODE>(T, rb, g, P.r, rows, rc);
+    __syncthreads();
+    const int64_t G = T.ngroups;
+    bool fin = true;
+    if (G > 1) {
+        double *wp = P.wpart + (g * T.nrb + rb) * (T.H + 1);
+        for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x)
+            __hip_atomic_store(&wp[i], rows[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned prev =
+                __hip_atomic_fetch_add(&tk2rb[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            row_last = (prev == (unsigned)G - 1);
+            if (row_last)
+                __hip_atomic_store(&tk2rb[rb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-#pragma unroll
-        for (int u = 0; u < RPT; ++u) {
-            const int64_t row = row0 + (int64_t)u * blockDim.x;
-            if (row >= r1) continue;
-            double o = v[u][0];
-#pragma unroll
-            for (int c = 1; c < 8; ++c)
-                if (c < G) o += v[u][c];
-            for (int64_t c = 8; c < G; ++c)
-                o += __hip_atomic_load(&P.rpart[c * P.m + row], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            if (ADD) o += P.target[row];
-            P.r[row] = o;
-            sq[0] += o * o;
+        __syncthreads();
+        fin = row_last;
+        if (fin) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x) {
+                double o = 0.0;
+                for (int64_t c = 0; c < G; ++c)
+                    o += __hip_atomic_load(&P.wpart[(c * T.nrb + rb) * (T.H + 1) + i],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rows[i] = o;
+            }
+            __syncthreads();
         }
     }
-    if (!REDUCE) return;
-    const unsigned nrb = (unsigned)((M.npanels + PANEL_WAVES - 1) / PANEL_WAVES);
-    block_sum<1>(sq, lds);
-    double tot[1];
-    if (last_of_sum<1>(sq, part, (unsigned)rb, nrb, ticket, tot, lds) && threadIdx.x == 0)
-        bb_record_f(P, iter, tot[0], ITER);
+    double sums[4] = {0.0, 0.0, 0.0, 0.0};
+    if (fin) {
+        const int64_t iend = (nloc < T.H) ? nloc : T.H;
+        for (int64_t i = threadIdx.x; i < iend; i += blockDim.x) {
+            const int32_t j = P.xz[i0 + i];
+            if (j < 0) continue;   // a block's last x entry (also the matrix's last row)
+            const double gv = rows[i] - rows[i + 1];
+            gout[j] = gv;
+            if (ITER) {
+                const double dg = gv - gp[j];
+                const double dz = dzv[j];
+                sums[0] += dg;
+                sums[1] += dz * dg;
+                sums[2] += dg * dg;
+                sums[3] += gv * gv;
+            }
+        }
+    }
+    if (!ITER || !fin) return;
+    block_sum<4>(sums, red);
+    double tot[4];
+    // one slot per row block, summed in row-block order: with several groups
+    // the finishing workgroup of a block varies from run to run, so its
+    // blockIdx must not decide where the block's sums enter the reduction
+    const bool last = (G == 1) ? last_block_sum<4>(sums, part, ticket, tot, red)
+                               : last_of_sum<4>(sums, part, (unsigned)rb, (unsigned)T.nrb, ticket,
+                                                tot, red);
+    if (last && threadIdx.x == 0) {
+        P.scal[BSLS_S_SUMDG] = tot[0];
+        P.scal[BSLS_S_DZDG] = tot[1];
+        P.scal[BSLS_S_DGDG] = tot[2];
+        P.scal[BSLS_S_GG] = tot[3];
+    }
 }
 
 // Multi-GPU stage 2: r (already all-reduced) += target, ||r||^2, stop test.
@@ -496,10 +660,25 @@ static void launch_k1_mode(const bsls_bb_problem &P, int64_t iter, const BBWork 
         P, iter, w.tkrb, w.p1, w.tk1);
 }
 
+template <int MODE, bool ADD, bool REDUCE, bool ITER>
+static void launch_k1t_mode(const bsls_bb_problem &P, int64_t iter, const BBWork &w,
+                            hipStream_t st) {
+    allow_lds(bb_k1t<MODE, ITER, ADD, REDUCE>);
+    bb_k1t<MODE, ITER, ADD, REDUCE><<<(int)(P.At.nrb * P.At.ngroups), BSLS_TILE_THREADS,
+                                      tile_lds_doubles(P.At, false) * 8, st>>>(P, iter, w.tkrb,
+                                                                                w.p1, w.tk1);
+}
+
 template <bool ADD, bool REDUCE, bool ITER>
 static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, hipStream_t st) {
-    if (P.colv) launch_k1_mode<0, ADD, REDUCE, ITER>(P, iter, w, st);
-    else launch_k1_mode<1, ADD, REDUCE, ITER>(P, iter, w, st);
+    if (P.At.ent) {
+        if (P.colv) launch_k1t_mode<0, ADD, REDUCE, ITER>(P, iter, w, st);
+        else launch_k1t_mode<1, ADD, REDUCE, ITER>(P, iter, w, st);
+    } else if (P.colv) {
+        launch_k1_mode<0, ADD, REDUCE, ITER>(P, iter, w, st);
+    } else {
+        launch_k1_mode<1, ADD, REDUCE, ITER>(P, iter, w, st);
+    }
 }
 
 template <int MODE, bool ITER>
@@ -510,11 +689,26 @@ static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *g
         P, w.dz, gp, gout, w.p2, w.tk2);
 }
 
+template <int MODE, bool ITER>
+static void launch_k2t_mode(const bsls_bb_problem &P, const double *gp, double *gout,
+                            const BBWork &w, hipStream_t st) {
+    allow_lds(bb_k2t<MODE, ITER>);
+    bb_k2t<MODE, ITER><<<(int)(P.ATt.nrb * P.ATt.ngroups), BSLS_TILE_THREADS,
+                         tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(P, w.dz, gp, gout, w.p2,
+                                                                       w.tk2, w.tk2rb);
+}
+
 template <bool ITER>
 static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
                       const BBWork &w, hipStream_t st) {
-    if (P.colv) launch_k2_mode<2, ITER>(P, gp, gout, w, st);
-    else launch_k2_mode<1, ITER>(P, gp, gout, w, st);
+    if (P.ATt.ent) {
+        if (P.colv) launch_k2t_mode<2, ITER>(P, gp, gout, w, st);
+        else launch_k2t_mode<1, ITER>(P, gp, gout, w, st);
+    } else if (P.colv) {
+        launch_k2_mode<2, ITER>(P, gp, gout, w, st);
+    } else {
+        launch_k2_mode<1, ITER>(P, gp, gout, w, st);
+    }
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
@@ -536,12 +730,32 @@ static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t 
     return need_val ? M.val != nullptr : true;
 }
 
+static bool tiles_ok(const bsls_tiles &T, int64_t rows, int64_t cols, int64_t halo,
+                     bool need_val, bool colv_lds) {
+    if (T.rows != rows || T.cols != cols || T.halo != halo || T.H < 64) return false;
+    if (T.nrb != (rows + T.H - 1) / T.H || T.ngroups < 1 || T.nquads < 0) return false;
+    if (T.order != 0 && !(T.order == 1 && T.ngroups % 8 == 0)) return false;
+    if (tile_lds_doubles(T, colv_lds) * 8 > (size_t)PANEL_LDS_MAX) return false;
+    if (!T.group_col || !T.wave_off || !T.ent) return false;
+    return need_val ? T.val != nullptr : true;
+}
+
 static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
     const bool general = p->colv == nullptr;
-    if (!panels_ok(p->A, p->m, p->n, 0, general) || !panels_ok(p->AT, p->n, p->m, 1, general) ||
-        p->AT.ngroups != 1 || !p->rpart)
+    if (p->At.ent) {
+        if (!tiles_ok(p->At, p->m, p->n, 0, general, false)) return BSLS_E_ARG;
+        if (p->At.ngroups > 1 && !p->rpart) return BSLS_E_ARG;
+    } else if (!panels_ok(p->A, p->m, p->n, 0, general) || !p->rpart) {
         return BSLS_E_ARG;
+    }
+    if (p->ATt.ent) {
+        if (!tiles_ok(p->ATt, p->n, p->m, 1, general, !general)) return BSLS_E_ARG;
+        if (p->ATt.ngroups > 1 && !p->wpart) return BSLS_E_ARG;
+    } else if (!panels_ok(p->AT, p->n, p->m, 1, general) || p->AT.ngroups != 1) {
+        return BSLS_E_ARG;
+    }
+    if (p->work_bytes < bb_layout(nullptr, p->m, p->n, p->nz).bytes) return BSLS_E_WORKSPACE;
     if (!p->target || !p->xstarts || !p->zstarts || !p->xz) return BSLS_E_ARG;
     if (!p->pk_z0 || !p->pk_b0 || !p->pk_mask || !p->pk_len || p->npacks < 1) return BSLS_E_ARG;
     if (!p->z[0] || !p->z[1] || !p->g[0] || !p->g[1] || !p->x || !p->r || !p->scal || !p->work)

@@ -1,0 +1,113 @@
+// tiles.hpp -- the SpMV format for sparse row blocks: streamed tiles
+// (include/bsls_hip.h, struct bsls_tiles).
+//
+// Why a second format.  The panel image (panels.hpp) stages a 20k-column chunk
+// of the gathered vector into LDS and walks it row-per-lane with the row sums
+// in registers; that pays while a 64-row slice holds several entries per chunk
+// (config C3: ~3.2 per row).  Over C5's 1M links a row holds ~0.3 entries per
+// chunk: the per-(slice, chunk) metadata and the mostly idle lanes make the
+// panel K1 / K2 take 278 / 465 us on a 20M-entry C5 column shard.  Measured
+// on that shard (tools/tile*_ubench.hip): staged-chunk variants were bound by
+// the per-chunk round trips (a barrier per chunk, two dependent loads after
+// it); this form, with no barrier at all, ~100 us, bound by the gathers.
+//
+// Form.  Workgroup (rb, g) of 1024 threads keeps row block rb's running sums
+// in LDS (slot-major: local row lr at rows[lr], thread lr % 1024 owns it, so
+// a wave's read-modify-write touches 64 consecutive doubles: no bank
+// conflicts, no races).  Each thread walks ONE linear stream: its rows'
+// entries of column group g sorted by column -- each row summed in CSR order
+// (bit-identical to SciPy's csr_matvec when ngroups == 1), and all threads
+// sweep the columns together.  The gathered vector is read straight through
+// L1/L2 (no LDS staging): random 8-B gathers run at the L2 line rate (~0.27 T
+// per second chip-wide, the same as the round-1 gather probe); the column
+// groups keep each XCD on one slice so the slice stays in that XCD's L2
+// (order 0 with ngroups | 8, order 1 for ngroups % 8 == 0).  The streams are
+// interleaved in 16-B quads (one 1-KB load per wave per 4 entries), loaded P
+// quads ahead, gathers one quad ahead of the row updates.
+#pragma once
+#include "bsls_common.hpp"
+
+namespace bsls {
+
+constexpr int TILE_T = BSLS_TILE_THREADS;
+
+__host__ __device__ inline int64_t tile_nslots(const bsls_tiles &T) {
+    return (T.H + T.halo + TILE_T - 1) / TILE_T;
+}
+
+// dynamic LDS doubles of a tile kernel: the row sums (+ the dummy slot), and
+// with `colv` the rows' column scales (K2 on a scaled incidence)
+__host__ __device__ inline size_t tile_lds_doubles(const bsls_tiles &T, bool colv) {
+    return (size_t)(tile_nslots(T) + 1) * TILE_T * (colv ? 2 : 1);
+}
+
+__device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t &rb, int64_t &g) {
+    if (T.order == 1) {
+        const int64_t x = b & 7, i = b >> 3;
+        rb = i % T.nrb;
+        g = x + 8 * (i / T.nrb);
+    } else {
+        g = b % T.ngroups;
+        rb = b / T.ngroups;
+    }
+}
+
+typedef uint32_t tile_quad __attribute__((ext_vector_type(4)));
+
+// Walk this thread's stream of tile (rb, g) into rows[] (LDS, zeroed by the
+// caller, barrier after):
+//   MODE 0  rows[lr] += src[c]                 (pattern / scaled incidence, K1)
+//   MODE 1  rows[lr] += val * src[c]           (stored values)
+//   MODE 2  rows[lr] += rcol[lr] * src[c]      (scaled incidence, K2: rcol in LDS)
+// src is indexed by the column relative to group_col[g].
+template <int MODE, int P = 4>
+__device__ __forceinline__ void tile_walk(const bsls_tiles &T, int64_t rb, int64_t g,
+                                          const double *__restrict__ src, double *rows,
+                                          const double *rcol) {
+    const int t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t s = (rb * T.ngroups + g) * 16 + wv;
+    const int64_t q0 = T.wave_off[s], nq = (T.wave_off[s + 1] - q0) >> 6;
+    const tile_quad *Q = reinterpret_cast<const tile_quad *>(T.ent) + q0 + lane;
+    const double *V = (MODE == 1) ? T.val + 4 * (q0 + lane) : nullptr;
+    const double *xb = src + T.group_col[g];
+    tile_quad ring[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) ring[k] = (k < nq) ? Q[(int64_t)k * 64] : tile_quad{0, 0, 0, 0};
+    double v[4], vn[4], a[4], an[4];
+    auto gat = [&](const tile_quad &u, int64_t q, double (&o)[4], double (&w)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = xb[u[j] & 0xFFFFFFu];
+        if (MODE == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = V[q * 256 + j];
+        }
+    };
+    gat(ring[0], 0, v, a);
+    for (int64_t q = 0; q < nq; q += P) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const tile_quad cur = ring[k];
+            if (q + k + 1 < nq) gat(ring[(k + 1) % P], q + k + 1, vn, an);
+            ring[k] = (q + k + P < nq) ? Q[(q + k + P) * 64] : tile_quad{0, 0, 0, 0};
+            if (q + k < nq) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int lr = (int)(cur[j] >> 24) * TILE_T + t;
+                    double term;
+                    if (MODE == 0) term = v[j];
+                    else if (MODE == 1) term = a[j] * v[j];
+                    else term = rcol[lr] * v[j];
+                    rows[lr] += term;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = vn[j];
+                if (MODE == 1) a[j] = an[j];
+            }
+        }
+    }
+}
+
+}  // namespace bsls

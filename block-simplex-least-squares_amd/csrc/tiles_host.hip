@@ -1,0 +1,169 @@
+// tiles_host.hip -- host-side builder of the streamed-tile image
+// (include/bsls_hip.h, struct bsls_tiles; device side csrc/tiles.hpp).
+//
+// Pure host code (no device memory).  Two passes over the CSR rows of each row
+// block: count the entries per (group, owning thread) to size every wave's
+// stream (its longest lane, in 4-entry quads), then bucket, sort each thread's
+// entries by column and scatter them into the interleaved quads.  Row blocks
+// are independent: they are spread over host threads (a C5 image, 160M
+// entries, builds in a few seconds instead of the minutes NumPy argsorts take).
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
+
+#include "tiles.hpp"
+
+using namespace bsls;
+
+namespace {
+
+struct Plan {
+    int64_t rows, cols, H, halo, nrb, G, nslots;
+    const int64_t *indptr;
+    const int32_t *indices;
+    const int64_t *gc;
+    std::vector<int32_t> gmap;   // column -> group
+};
+
+// rows of block rb in local order: [rb H, min(rb H + H + halo, rows))
+inline int64_t block_end(const Plan &p, int64_t rb) {
+    return std::min(p.rows, rb * p.H + p.H + p.halo);
+}
+
+template <typename F>
+void parallel_blocks(int64_t nrb, F f) {
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min(nt, 16u));
+    if (nrb < 2 || nt == 1) {
+        for (int64_t rb = 0; rb < nrb; ++rb) f(rb);
+        return;
+    }
+    std::atomic<int64_t> next(0);
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < nt; ++k)
+        th.emplace_back([&]() {
+            for (int64_t rb; (rb = next.fetch_add(1)) < nrb;) f(rb);
+        });
+    for (auto &x : th) x.join();
+}
+
+// per-thread entry counts of block rb, (g, t) -> cnt[g * T + t]
+void count_block(const Plan &p, int64_t rb, std::vector<int64_t> &cnt) {
+    cnt.assign((size_t)p.G * TILE_T, 0);
+    const int64_t r0 = rb * p.H;
+    for (int64_t i = r0; i < block_end(p, rb); ++i) {
+        const int t = (int)((i - r0) % TILE_T);
+        for (int64_t k = p.indptr[i]; k < p.indptr[i + 1]; ++k)
+            cnt[(size_t)p.gmap[p.indices[k]] * TILE_T + t]++;
+    }
+}
+
+}  // namespace
+
+extern "C" int64_t bsls_tiles_build(int64_t rows, int64_t cols, const int64_t *indptr,
+                                    const int32_t *indices, const double *data, int64_t H,
+                                    int64_t halo, int64_t ngroups, const int64_t *group_col,
+                                    int64_t *wave_off_out, uint32_t *ent_out, double *val_out,
+                                    int64_t nquads_cap) {
+    if (rows < 1 || cols < 1 || !indptr || !indices || H < 64 || (halo != 0 && halo != 1) ||
+        ngroups < 1 || !group_col)
+        return BSLS_E_ARG;
+    Plan p;
+    p.rows = rows;
+    p.cols = cols;
+    p.H = H;
+    p.halo = halo;
+    p.nrb = (rows + H - 1) / H;
+    p.G = ngroups;
+    p.nslots = (H + halo + TILE_T - 1) / TILE_T;
+    p.indptr = indptr;
+    p.indices = indices;
+    p.gc = group_col;
+    if (p.nslots + 1 > BSLS_TILE_MAXSLOTS) return BSLS_E_ARG;
+    if (group_col[0] != 0 || group_col[ngroups] != cols) return BSLS_E_ARG;
+    for (int64_t g = 0; g < ngroups; ++g) {
+        const int64_t w = group_col[g + 1] - group_col[g];
+        if (w < 1 || w > (1 << 24)) return BSLS_E_ARG;   // non-empty, 24-bit offsets
+    }
+    if (indptr[0] != 0) return BSLS_E_ARG;
+    p.gmap.resize(cols);
+    for (int64_t g = 0; g < ngroups; ++g)
+        for (int64_t j = group_col[g]; j < group_col[g + 1]; ++j) p.gmap[j] = (int32_t)g;
+    for (int64_t i = 0; i < rows; ++i)
+        if (indptr[i + 1] < indptr[i]) return BSLS_E_ARG;
+    for (int64_t k = 0; k < indptr[rows]; ++k)
+        if (indices[k] < 0 || indices[k] >= cols) return BSLS_E_ARG;
+    // pass 1: quads per wave stream
+    const int64_t nwav = p.nrb * ngroups * 16;
+    std::vector<int64_t> wq(nwav, 0);
+    parallel_blocks(p.nrb, [&](int64_t rb) {
+        std::vector<int64_t> cnt;
+        count_block(p, rb, cnt);
+        for (int64_t g = 0; g < ngroups; ++g)
+            for (int w = 0; w < 16; ++w) {
+                int64_t mx = 0;
+                for (int l = 0; l < 64; ++l) mx = std::max(mx, cnt[(size_t)g * TILE_T + w * 64 + l]);
+                wq[(rb * ngroups + g) * 16 + w] = (mx + 3) / 4 * 64;
+            }
+    });
+    int64_t total = 0;
+    for (int64_t s = 0; s < nwav; ++s) total += wq[s];
+    const int64_t nquads = total;
+    if (!wave_off_out) return nquads;
+    if (!ent_out || nquads_cap < nquads || (data && !val_out)) return BSLS_E_ARG;
+    wave_off_out[0] = 0;
+    for (int64_t s = 0; s < nwav; ++s) wave_off_out[s + 1] = wave_off_out[s] + wq[s];
+    const uint32_t dummy = (uint32_t)p.nslots << 24;
+    // pass 2: bucket, sort by column, scatter into the quads
+    parallel_blocks(p.nrb, [&](int64_t rb) {
+        std::vector<int64_t> cnt;
+        count_block(p, rb, cnt);
+        const size_t nb = (size_t)ngroups * TILE_T;
+        std::vector<int64_t> off(nb + 1, 0);
+        for (size_t k = 0; k < nb; ++k) off[k + 1] = off[k] + cnt[k];
+        std::vector<uint64_t> key(off[nb]);
+        std::vector<double> val(data ? off[nb] : 0);
+        std::vector<int64_t> cur(off.begin(), off.end() - 1);
+        const int64_t r0 = rb * p.H;
+        for (int64_t i = r0; i < block_end(p, rb); ++i) {
+            const int64_t lr = i - r0;
+            const int t = (int)(lr % TILE_T);
+            const uint64_t slot = (uint64_t)(lr / TILE_T);
+            for (int64_t k = p.indptr[i]; k < p.indptr[i + 1]; ++k) {
+                const int32_t c = p.indices[k];
+                const int64_t g = p.gmap[c];
+                const int64_t pos = cur[(size_t)g * TILE_T + t]++;
+                key[pos] = ((uint64_t)(c - p.gc[g]) << 8) | slot;   // column, then slot
+                if (data) val[pos] = data[k];
+            }
+        }
+        std::vector<int64_t> perm;
+        for (int64_t g = 0; g < ngroups; ++g) {
+            for (int w = 0; w < 16; ++w) {
+                const int64_t s = (rb * ngroups + g) * 16 + w;
+                const int64_t base = wave_off_out[s];
+                for (int64_t q = base; q < wave_off_out[s + 1]; ++q)
+                    for (int j = 0; j < 4; ++j) {
+                        ent_out[4 * q + j] = dummy;
+                        if (data) val_out[4 * q + j] = 0.0;
+                    }
+                for (int l = 0; l < 64; ++l) {
+                    const size_t bk = (size_t)g * TILE_T + w * 64 + l;
+                    const int64_t a = off[bk], e = off[bk + 1];
+                    perm.resize(e - a);
+                    for (int64_t k = a; k < e; ++k) perm[k - a] = k;
+                    std::sort(perm.begin(), perm.end(),
+                              [&](int64_t x, int64_t y) { return key[x] < key[y]; });
+                    for (int64_t k = 0; k < e - a; ++k) {
+                        const int64_t q = base + (k >> 2) * 64 + l;
+                        const uint64_t kk = key[perm[k]];
+                        ent_out[4 * q + (k & 3)] = (uint32_t)((kk & 0xFF) << 24) | (uint32_t)(kk >> 8);
+                        if (data) val_out[4 * q + (k & 3)] = val[perm[k]];
+                    }
+                }
+            }
+        }
+    });
+    return nquads;
+}

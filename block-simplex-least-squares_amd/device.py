@@ -267,6 +267,123 @@ class DevicePanels:
         return sum(v.numel() * v.element_size() for v in self.t.values())
 
 
+def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=3 << 20):
+    """(H, ngroups, order) of a tile image (include/bsls_hip.h struct bsls_tiles,
+    csrc/tiles.hpp): column groups (a power of two) until one group's slice of
+    the gathered vector fits an XCD's L2 (order 1, XCD-sequential, past 8
+    groups); row blocks as tall as the LDS holds (half of it with K2's column
+    scales), at least one workgroup per CU, the grid rounded up to whole rounds
+    of `cus` workgroups.  BSLS_TILE_PLAN="H,groups" overrides it."""
+    plan = os.environ.get('BSLS_TILE_PLAN')
+    if plan:
+        H, G = (int(v) for v in plan.split(','))
+        return H, G, (1 if G > 8 else 0)
+    G = 1
+    while 8 * cols / G > l2_slice and G < 64:
+        G *= 2
+    G = max(1, min(G, cols))
+    order = 1 if G > 8 else 0
+    per = _native.TILE_MAXSLOTS // (2 if colv_lds else 1) - 1
+    hmax = per * _native.TILE_THREADS - halo
+    nrb = max(-(-rows // hmax), -(-cus // G))
+    nrb = -(-(nrb * G) // cus) * cus // G if nrb * G > cus else nrb
+    H = max(64, -(-rows // nrb))
+    return int(H), int(G), int(order)
+
+
+def spmv_format(M, fmt=None):
+    """'panels' or 'tiles' for the fused SpMV over matrix M (rows x cols):
+    tiles when a panel chunk (BSLS_PANEL_CHUNK columns) holds under one entry
+    per row on average -- the sparse row blocks of C5 (0.3), where the panel
+    walk idles (csrc/tiles.hpp); panels for C3 (3.2).  fmt / BSLS_SPMV_FORMAT
+    force one."""
+    fmt = fmt or os.environ.get('BSLS_SPMV_FORMAT') or 'auto'
+    if fmt != 'auto':
+        if fmt not in ('panels', 'tiles'):
+            raise ValueError('unknown SpMV format %r' % fmt)
+        return fmt
+    R, C = M.shape
+    lam = (M.nnz / max(R, 1)) * min(_native.PANEL_CHUNK, C) / max(C, 1)
+    return 'tiles' if lam < 1.0 else 'panels'
+
+
+def tiles_matvec(img, x, colv=None, group_sums=False):
+    """Host restatement of the tile kernels' walk (csrc/tiles.hpp) over an image
+    from _native.tiles_build: per (row block, group) each row summed entry by
+    entry in stream order, the groups then added in group order.  Returns the
+    row sums (halo rows dropped).  Test helper (NumPy, vectorised per quad)."""
+    R, H, halo, G = img['rows'], img['H'], img['halo'], img['ngroups']
+    T = _native.TILE_THREADS
+    gc = img['group_col']
+    x = np.asarray(x, dtype=np.float64)
+    nslots = -(-(H + halo) // T)
+    out = np.zeros(R)
+    parts = []
+    for g in range(G):
+        acc = np.zeros(R)
+        for rb in range(img['nrb']):
+            rows = np.zeros((nslots + 1) * T)
+            for w in range(16):
+                s = (rb * G + g) * 16 + w
+                q0, q1 = int(img['wave_off'][s]), int(img['wave_off'][s + 1])
+                lanes = w * 64 + np.arange(64)
+                for q in range(q0, q1, 64):
+                    for j in range(4):
+                        e = img['ent'][4 * (q + np.arange(64)) + j].astype(np.int64)
+                        lr = (e >> 24) * T + lanes
+                        xv = x[gc[g] + (e & 0xFFFFFF)]
+                        if img['val'] is not None:
+                            t = img['val'][4 * (q + np.arange(64)) + j] * xv
+                        elif colv is not None:
+                            rr = np.minimum(rb * H + lr, R - 1)
+                            t = np.where(lr < H + halo, colv[rr], 0.0) * xv
+                        else:
+                            t = xv
+                        rows[lr] = rows[lr] + t
+            r0 = rb * H
+            r1 = min(r0 + H, R)
+            acc[r0:r1] = rows[:r1 - r0]
+        parts.append(acc)
+    out = parts[0].copy()
+    for a in parts[1:]:
+        out = out + a
+    return (out, parts) if group_sums else out
+
+
+class DeviceTiles:
+    """A tile image on the device + the ctypes struct pointing at it."""
+
+    def __init__(self, M, halo=0, values=True, colv_lds=False, plan=None):
+        torch = _torch()
+        M = sps.csr_matrix(M)
+        M.sort_indices()
+        R, C = M.shape
+        H, G, order = plan or tile_plan(R, C, halo, colv_lds)
+        gc = np.round(np.linspace(0, C, G + 1)).astype(np.int64)
+        if np.any(np.diff(gc) < 1):
+            raise ValueError('more column groups than columns')
+        img = _native.tiles_build(M, H, halo, gc, values=values)
+        img.update(rows=R, cols=C, H=H, halo=halo, ngroups=G, order=order, group_col=gc)
+        self.img = img
+        self.nnz = int(M.nnz)
+        self.t = {'group_col': torch.from_numpy(gc).cuda(),
+                  'wave_off': torch.from_numpy(img['wave_off']).cuda(),
+                  'ent': torch.from_numpy(img['ent'].view(np.int32)).cuda()}
+        if img['val'] is not None:
+            self.t['val'] = torch.from_numpy(img['val']).cuda()
+        S = _native.Tiles()
+        S.rows, S.cols, S.H, S.halo = R, C, H, halo
+        S.nrb, S.ngroups, S.order, S.nquads = img['nrb'], G, order, img['nquads']
+        S.group_col = self.t['group_col'].data_ptr()
+        S.wave_off = self.t['wave_off'].data_ptr()
+        S.ent = self.t['ent'].data_ptr()
+        S.val = self.t['val'].data_ptr() if 'val' in self.t else None
+        self.struct = S
+
+    def bytes(self):
+        return sum(v.numel() * v.element_size() for v in self.t.values())
+
+
 def panel_rows(rows, workgroups_per_group, waves=16):
     """Rows per panel so one launch is about `workgroups_per_group` workgroups of
     16 panels per group (one per CU), within 64 .. BSLS_PANEL_ROWS."""
@@ -404,7 +521,8 @@ class BBEngine:
     """
 
     def __init__(self, A, b, block_sizes, options=None, early_exit=True, A_dev=None,
-                 AT_dev=None, AT=None, target=None, x0=None, general=False):
+                 AT_dev=None, AT=None, target=None, x0=None, general=False, fmt=None,
+                 tile_plans=(None, None)):
         torch = _torch()
         L = _native.lib()
         self.layout = lay = BlockLayout(block_sizes)
@@ -419,10 +537,20 @@ class BBEngine:
         # groups (K1), A' with halo rows (K2); values dropped for a scaled incidence
         colv = None if general else scaled_incidence_scale(A)
         self.scaled = colv is not None
-        prow, groups = k1_plan(self.m)
-        self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
-        self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), True, 1,
-                                   values=not self.scaled)
+        # per matrix: panels (dense row blocks, C3) or streamed tiles (C5)
+        self.fmt_A, self.fmt_AT = spmv_format(A, fmt), spmv_format(AT, fmt)
+        self.A_pan = self.AT_pan = self.A_til = self.AT_til = None
+        if self.fmt_A == 'panels':
+            prow, groups = k1_plan(self.m)
+            self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
+        else:
+            self.A_til = DeviceTiles(A, 0, values=not self.scaled, plan=tile_plans[0])
+        if self.fmt_AT == 'panels':
+            self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), True, 1,
+                                       values=not self.scaled)
+        else:
+            self.AT_til = DeviceTiles(AT, 1, values=not self.scaled, colv_lds=self.scaled,
+                                      plan=tile_plans[1])
         opts = options or {}
         self.options = dict(opts)
         dev = dict(dtype=torch.float64, device='cuda')
@@ -448,11 +576,25 @@ class BBEngine:
         self.scal = torch.zeros(_native.S_COUNT, **dev)
         self.work = torch.zeros(L.bsls_bb_workspace_size(self.m, self.n, self.nz),
                                 dtype=torch.uint8, device='cuda')
-        self.rpart = torch.zeros(self.A_pan.img['ngroups'] * self.m, **dev)
+        ga = (self.A_pan or self.A_til).img['ngroups']
+        self.rpart = torch.zeros(ga * self.m if ga > 1 or self.A_pan else 1, **dev)
+        self.wpart = None
+        if self.AT_til is not None and self.AT_til.img['ngroups'] > 1:
+            ti = self.AT_til.img
+            self.wpart = torch.zeros(ti['ngroups'] * ti['nrb'] * (ti['H'] + 1), **dev)
         self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
         P = BBProblem()
         P.m, P.n, P.nz, P.nblocks = self.m, lay.n, lay.nz, lay.p
-        P.A, P.AT = self.A_pan.struct, self.AT_pan.struct
+        if self.A_pan is not None:
+            P.A = self.A_pan.struct
+        else:
+            P.At = self.A_til.struct
+        if self.AT_pan is not None:
+            P.AT = self.AT_pan.struct
+        else:
+            P.ATt = self.AT_til.struct
+        P.wpart = self.wpart.data_ptr() if self.wpart is not None else None
+        P.work_bytes = self.work.numel()
         P.colv = self.colv.data_ptr() if self.scaled else None
         P.rpart = self.rpart.data_ptr()
         P.target = self.target.data_ptr()

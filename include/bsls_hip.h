@@ -174,6 +174,51 @@ typedef struct bsls_panels {
     const double *val;              /* per entry (+ slack), or NULL when scaled (see colv) */
 } bsls_panels;
 
+/* Streamed-tile image of a sparse matrix M (rows x cols): the SpMV format for
+ * sparse row blocks, where a panel chunk holds well under one entry per row
+ * (config C5: 10M routes over 1M links, ~0.3 entries per row per 20k-column
+ * chunk).  Layout and rationale: csrc/tiles.hpp; built on the host by
+ * bsls_tiles_build.  Rows are cut into row blocks of H rows (with halo = 1 a
+ * block also holds the next block's row 0 as its local row H, for K2's
+ * N'w = w_i - w_{i+1}); columns into ngroups groups [group_col[g],
+ * group_col[g+1]).  Workgroup (rb, g) of BSLS_TILE_THREADS threads keeps the
+ * block's running row sums in LDS; thread t owns the local rows lr with
+ * lr % BSLS_TILE_THREADS == t and walks one stream: its rows' entries of group
+ * g in column order (every row summed in CSR order, like SciPy's csr_matvec).
+ * Wave w of (rb, g) (s = (rb * ngroups + g) * 16 + w) owns the quads (4
+ * entries, 16 B) wave_off[s] .. wave_off[s+1] - 1; quad k of its lane l is
+ * wave_off[s] + 64 k + l.  Entry = (lr / BSLS_TILE_THREADS) << 24 |
+ * (column - group_col[g]) (uint32); a stream shorter than its wave's longest
+ * is padded with entries of the dummy slot nslots = ceil((H + halo) / 1024).
+ * val: the values in the entries' layout (8 B each), NULL for a scaled
+ * incidence.  order: workgroup b -> (rb, g): 0: g = b % ngroups, rb = b /
+ * ngroups (with ngroups | 8 every XCD reads one column slice: it stays in the
+ * XCD's L2); 1 (ngroups % 8 == 0): XCD x = b % 8 walks its groups x, x + 8, ...
+ * one after the other over all row blocks (b / 8 = j * nrb + rb, g = x + 8 j). */
+#define BSLS_TILE_THREADS 1024
+#define BSLS_TILE_MAXSLOTS 20       /* LDS: (nslots + 1) * 1024 doubles (x2 with colv) */
+typedef struct bsls_tiles {
+    int64_t rows, cols;
+    int64_t H, halo;                /* rows per block; 1: + the next block's row 0 */
+    int64_t nrb, ngroups, order;
+    int64_t nquads;                 /* ent holds 4 * nquads entries */
+    const int64_t *group_col;       /* ngroups + 1 */
+    const int64_t *wave_off;        /* nrb * ngroups * 16 + 1 (in quads) */
+    const uint32_t *ent;
+    const double *val;              /* 4 * nquads, or NULL (scaled incidence) */
+} bsls_tiles;
+
+/* Host-side builder (no device memory): the tile image of the CSR matrix
+ * (indptr: rows + 1 int64, indices int32 column-sorted within each row, data
+ * optional).  Call once with wave_off_out == NULL to get the quad count
+ * (>= 0, or BSLS_E_ARG), allocate 4 * count entries (and values), call again
+ * to fill wave_off_out (nrb * ngroups * 16 + 1), ent_out and val_out (when
+ * data != NULL).  group_col: ngroups + 1 column bounds. */
+int64_t bsls_tiles_build(int64_t rows, int64_t cols, const int64_t *indptr,
+                         const int32_t *indices, const double *data, int64_t H, int64_t halo,
+                         int64_t ngroups, const int64_t *group_col, int64_t *wave_off_out,
+                         uint32_t *ent_out, double *val_out, int64_t nquads_cap);
+
 typedef struct bsls_bb_problem {
     int64_t m, n, nz, nblocks;      /* rows, x length, z length (n - nblocks), blocks */
     bsls_panels A;                  /* K1: A, chunks grouped per XCD (ngroups partials) */
@@ -207,6 +252,14 @@ typedef struct bsls_bb_problem {
     double opt_tol;                 /* options['opt_tol'] */
     int32_t early_exit;             /* 0 disables every early exit (fixed-count timing) */
     int32_t reserved;
+    /* Tile images replacing the panels when their ent is not NULL (then A / AT
+     * are not read): At for K1 (halo 0; ngroups partials in rpart), ATt for K2
+     * (halo 1; with ngroups > 1 the partial row sums go through wpart,
+     * ngroups * nrb * (H + 1) doubles). */
+    bsls_tiles At;
+    bsls_tiles ATt;
+    double *wpart;
+    size_t work_bytes;              /* size of work; < bsls_bb_workspace_size -> BSLS_E_WORKSPACE */
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);

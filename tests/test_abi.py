@@ -68,7 +68,8 @@ def _c_layout(tmp_path, struct, fields):
 
 
 @pytest.mark.parametrize('struct,cls', [('bsls_bb_problem', 'BBProblem'), ('bsls_panels', 'Panels'),
-                                        ('bsls_xbb_problem', 'XBBProblem'), ('bsls_csr', 'CSR')])
+                                        ('bsls_xbb_problem', 'XBBProblem'), ('bsls_csr', 'CSR'),
+                                        ('bsls_tiles', 'Tiles')])
 def test_struct_layout_matches_header(native, tmp_path, struct, cls):
     C = getattr(native, cls)
     names = [f[0] for f in C._fields_]

@@ -70,15 +70,25 @@ def shard100k(orc):
     return sh, b, ref
 
 
+# SpMV formats: the panels (dense row blocks), the streamed tiles with one
+# column group, and the tiles with several (partials + last-arriver sums)
+FORMATS = {'panels': dict(fmt='panels'),
+           'tiles': dict(fmt='tiles'),
+           'tiles-groups': dict(fmt='tiles', tile_plans=((1024, 4, 0), (1536, 2, 0)))}
+
+
+@pytest.mark.parametrize('fmt', sorted(FORMATS))
 @pytest.mark.parametrize('general', [False, True])
-def test_bb_fixed_iterations_match_oracle_at_scale(cuda, shard100k, general):
+def test_bb_fixed_iterations_match_oracle_at_scale(cuda, shard100k, general, fmt):
     """A 100k-route synthetic problem, iterates at 1, 10, 50 vs the oracle, with
-    the scaled-incidence panels (no values) and with stored values."""
+    the scaled-incidence images (no values) and with stored values, on every
+    SpMV format."""
     from device import BBEngine
     sh, b, ref = shard100k
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 50, 'opt_tol': 1e-30},
-                   general=general)
+                   general=general, **FORMATS[fmt])
     assert eng.scaled == (not general)
+    assert eng.fmt_A == eng.fmt_AT == FORMATS[fmt]['fmt']
     rec = {}
 
     def log(i, s, dt):
@@ -89,32 +99,40 @@ def test_bb_fixed_iterations_match_oracle_at_scale(cuda, shard100k, general):
         assert rel_err(rec[i], ref[i]) < 1e-6, (i, rel_err(rec[i], ref[i]))
 
 
+@pytest.mark.parametrize('fmt', sorted(FORMATS))
 @pytest.mark.parametrize('general', [False, True])
-def test_k2_gradient_bit_exact_vs_scipy(cuda, shard100k, general):
-    """K2 alone (stage 3): w = A'r is summed in CSR order in LDS, so
-    g = N'(A'r) equals SciPy's N.T.dot(A.T.dot(r)) bit for bit."""
+def test_k2_gradient_bit_exact_vs_scipy(cuda, shard100k, general, fmt):
+    """K2 alone (stage 3): w = A'r is summed in CSR order (panels: in a register
+    per row; tiles: in LDS, each thread's stream in column order), so with one
+    column group g = N'(A'r) equals SciPy's N.T.dot(A.T.dot(r)) bit for bit;
+    with several groups to rounding."""
     import torch
     from device import BBEngine
     from oracle import oracle as orc
     sh, b, _ = shard100k
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 5, 'opt_tol': 1e-30},
-                   general=general)
+                   general=general, **FORMATS[fmt])
     r = np.random.RandomState(5).randn(eng.m)
     eng.r.copy_(torch.from_numpy(r))
     eng.stage(3, 0)
     got = eng.g[0][:eng.nz].cpu().numpy()
     N = orc.block_sizes_to_N(sh['block_sizes'])
     want = N.T.tocsr().dot(sh['AT'].dot(r))
-    assert np.array_equal(got, want)
+    if fmt == 'tiles-groups':
+        assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
+    else:
+        assert np.array_equal(got, want)
 
 
-def test_k1_residual_vs_scipy(cuda, shard100k):
-    """K1 alone (stage 7 at iteration 0): r = A x + target with 8 chunk-group
+@pytest.mark.parametrize('fmt', sorted(FORMATS))
+def test_k1_residual_vs_scipy(cuda, shard100k, fmt):
+    """K1 alone (stage 7 at iteration 0): r = A x + target with chunk-group
     partials; equal to SciPy to rounding (1e-12 relative)."""
     import torch
     from device import BBEngine
     sh, b, _ = shard100k
-    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 5, 'opt_tol': 1e-30})
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 5, 'opt_tol': 1e-30},
+                   **FORMATS[fmt])
     x = np.random.RandomState(6).rand(eng.n)
     xin = torch.from_numpy(eng.colv.cpu().numpy() * x if eng.scaled else x).cuda()
     eng.x.copy_(xin)
@@ -124,7 +142,8 @@ def test_k1_residual_vs_scipy(cuda, shard100k):
     assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
 
 
-def test_bb_deterministic(cuda):
+@pytest.mark.parametrize('fmt', sorted(FORMATS))
+def test_bb_deterministic(cuda, fmt):
     """Two runs, same inputs -> bit-identical iterates (fixed reduction order)."""
     from device import BBEngine
     from synthetic import make_shard, add_noise
@@ -132,7 +151,8 @@ def test_bb_deterministic(cuda):
     b = add_noise(sh['Ax'], 0.02, seed=3)
     outs = []
     for _ in range(2):
-        eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 30, 'opt_tol': 1e-30})
+        eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 30, 'opt_tol': 1e-30},
+                       **FORMATS[fmt])
         outs.append(eng.solve(poll=30).cpu().numpy().copy())
     assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64))
 

@@ -16,16 +16,27 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=50)
     ap.add_argument('--iters', type=int, default=200)
+    ap.add_argument('--shape', type=str, default='C3',
+                    help="C3, C5, or 'n,p,m' (e.g. a C5 shard: 1250000,62500,1000000)")
     args = ap.parse_args()
     import numpy as np
     import torch
     from synthetic import make_shard, add_noise, CONFIGS, SEED
     from device import BBEngine
-    c = CONFIGS['C3']
+    if args.shape in CONFIGS:
+        c = CONFIGS[args.shape]
+    else:
+        n, p, m = (int(v) for v in args.shape.split(','))
+        c = dict(n=n, p=p, m=m, per_col=16)
+    t0 = time.perf_counter()
     sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+    print('shape n %d p %d m %d nnz %d: generated in %.1f s' % (c['n'], c['p'], c['m'],
+                                                                 sh['A'].nnz, time.perf_counter() - t0),
+          flush=True)
     b = add_noise(sh['Ax'], 0.02)
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 10 ** 12, 'opt_tol': 1e-30},
                    early_exit=False, AT=sh['AT'])
+    print('engine built in %.1f s' % (time.perf_counter() - t0), flush=True)
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
     eng.prologue()
     eng.iterate(1, 20)
