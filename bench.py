@@ -1,20 +1,23 @@
 #!/usr/bin/env python
-"""Benchmark: BB solver iterations/sec on the 1M-route block-LSQ problem (C3) +
-proj_simplex HBM GB/s (C2), on MI355X.  One JSON line on rank 0.
+"""Benchmark: BB solver iterations/sec + proj_simplex HBM GB/s on MI355X.
+One JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C5|C3]
 
 A step = one full projected-BB iteration (python/BB.py:17-41 semantics, fused
 K2 -> K3 -> K1 on the device) over the whole problem, inputs resident in HBM.
-N = 1: config C3 (1M routes, 50k blocks, 100k links, 16M nnz, fp64).
-N > 1 (torchrun, one rank per GPU): weak scaling -- every rank owns a C3-sized
-column shard (1M routes, 50k blocks, 16M nnz) of an N x 1M-route problem on
-the same 100k-link network (m stays 100k: more routes over one network, so
-every rank's shard has exactly the C3 shape); per iteration one RCCL
-all-reduce of the residual r (8 m = 800 kB) and one of the four BB sums.
-value = N x (iterations/s of the whole job), i.e. 1M-route-equivalent BB
-iterations per second.  BSLS_DIST_BACKEND=gloo rehearses the N > 1 path with
-several ranks on one GPU (RCCL refuses two ranks on one device).
+
+Default workload C5 (BASELINE.json configs[4]): ONE synthetic problem of 10M
+routes / 500k blocks / 1M links / 160M nnz, the same for every N
+(synthetic.make_partitioned), column-sharded by whole blocks over the N ranks
+(one process per GPU, torchrun); strong scaling: value = iterations/s of the
+whole job, the 1-GPU run being the N = 1 point.  Per iteration one RCCL
+all-reduce of the four BB sums and one of the residual r (8 MB), the latter
+in --parts row parts pipelined behind K1 (distributed.ShardedBB).
+At N = 1 the line also carries "c3": the BASELINE metric's 1M-route problem
+(C3: 1M routes / 50k blocks / 100k links / 16M nnz) with its kernels and
+roofline, the C2 projection, the x-space BB, mirror descent and the standalone
+PAVA legs, and the CPU baselines.
 
 Early exits are disabled for timing: exactly K iterations run.
 """
@@ -49,15 +52,24 @@ def kernel_bytes(m, n, nz, p, nnz_a, nnz_at):
 
 
 def format_bytes(eng):
-    """Bytes the kernels actually stream with the panel images (the compressed
-    figure SURVEY.md §8(d) asks to state beside the general one)."""
+    """Bytes the kernels actually stream with the engine's images (the
+    compressed figure SURVEY.md §8(d) asks to state beside the general one):
+    the image, the vectors once, and the group partials (written + read)."""
     m, n, nz = eng.m, eng.n, eng.nz
     scale = 8 * n if eng.scaled else 0
-    return {
-        'K1_spmv_A': eng.A_pan.bytes() + 8 * n + 16 * m + 8 * m * (eng.A_pan.img['ngroups'] - 1) * 2,
-        'K2_spmvT_Nt_dots': eng.AT_pan.bytes() + 8 * m + 4 * n + 32 * nz + scale,
-        'K3_pava_clip_z2x': 24 * nz + 8 * n + 4 * eng.layout.p + scale,
-    }
+    if eng.A_pan is not None:
+        k1 = eng.A_pan.bytes() + 8 * n + 16 * m + 8 * m * (eng.A_pan.img['ngroups'] - 1) * 2
+    else:
+        g = eng.A_til.img['ngroups']
+        k1 = eng.A_til.bytes() + 8 * n + 16 * m + (8 * m * g * 2 if g > 1 else 0)
+    if eng.AT_pan is not None:
+        k2 = eng.AT_pan.bytes() + 8 * m + 4 * n + 24 * nz + scale
+    else:
+        ti = eng.AT_til.img
+        wp = 8 * ti['ngroups'] * ti['nrb'] * (ti['H'] + 1) * 2 if ti['ngroups'] > 1 else 0
+        k2 = eng.AT_til.bytes() + 8 * m + 4 * n + 24 * nz + scale + wp
+    return {'K1_spmv_A': k1, 'K2_spmvT_Nt_dots': k2,
+            'K3_pava_clip_z2x': 32 * nz + 8 * n + 4 * eng.layout.p + scale}
 
 
 def survey_iter_bytes(m, n, nz, nnz):
@@ -227,13 +239,204 @@ def bench_md(sh, b, iters=30):
             'finite': bool(np.all(np.isfinite(x)))}
 
 
+def bench_iso(reps=3, batch=16):
+    """Standalone PAVA (bsls_isotonic_multi, variant 1 -- the isotonic_regression
+    path of main.py's proj, isotonic_regression.h:85-92) on the C3/C4 z layout:
+    950k entries in 50k blocks, inputs like K3's (z - t g); `batch` launches
+    back to back on distinct copies between two events.  Bytes 16 n + 4 (p+1)."""
+    import torch
+    import _native
+    from _native import ptr, stream_handle, check
+    from synthetic import make_shard, CONFIGS, SEED
+    L = _native.lib()
+    c = CONFIGS['C3']
+    rs = np.random.RandomState(SEED)
+    sizes = rs.multinomial(c['n'] - c['p'], np.ones(c['p']) / c['p']) + 1
+    zs = np.concatenate(([0], np.cumsum(sizes - 1)[:-1])).astype(np.int64)
+    nz = int((sizes - 1).sum())
+    y0 = torch.from_numpy(rs.rand(nz) - 0.3 * rs.randn(nz)).cuda()
+    st = torch.from_numpy(zs).cuda()
+    mb = int(np.max(sizes))
+    ws = torch.zeros(L.bsls_isotonic_workspace_size(nz), dtype=torch.uint8, device='cuda')
+    status = torch.zeros(4, dtype=torch.int32, device='cuda')
+    ys = [y0.clone() for _ in range(batch)]
+
+    def iso(t):
+        check(L.bsls_isotonic_multi(1, ptr(t), ptr(st), zs.size, nz, None, 1, mb, ptr(ws),
+                                    ws.numel(), ptr(status), stream_handle()), 'iso')
+    for t in ys[:2]:
+        iso(t)
+    out = []
+    for _ in range(reps):
+        for t in ys:
+            t.copy_(y0)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(2e8))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for t in ys:
+            iso(t)
+        e1.record()
+        torch.cuda.synchronize()
+        out.append(e0.elapsed_time(e1) / batch * 1e3)
+    us = sorted(out)[len(out) // 2]
+    from oracle import oracle as orc
+    yc = y0.cpu().numpy().copy()
+    t0 = time.perf_counter()
+    orc.isotonic_regression_multi_c(yc, zs)
+    cpu_s = time.perf_counter() - t0
+    ok = bool(np.array_equal(yc.view(np.int64), ys[0].cpu().numpy().view(np.int64)))
+    byt = 16 * nz + 4 * (zs.size + 1)
+    return {'n': nz, 'blocks': int(zs.size), 'avg_us': us, 'alg_bytes': byt,
+            'GB_s': byt / (us * 1e-6) / 1e9, 'frac_hbm_peak': byt / (us * 1e-6) / HBM_PEAK,
+            'cpu_oracle_ms_1thread': cpu_s * 1e3, 'bit_exact_vs_oracle': ok}
+
+
+def log(msg):
+    """Progress on stderr (the GPU box kills a command silent for 3 minutes)."""
+    print('[bench %.1fs] %s' % (time.perf_counter() - T0, msg), file=sys.stderr, flush=True)
+
+
+T0 = time.perf_counter()
+
+
+def build_problem(name, world, rank, dist):
+    """The rank's column shard of workload `name` and the full b (SURVEY §8(d)
+    recipe, 2 % multiplicative noise so the exact-zero exit never fires)."""
+    import torch
+    from synthetic import make_partitioned, make_shard, add_noise, CONFIGS, SEED
+    c = CONFIGS[name]
+    if name == 'C5':
+        sh = make_partitioned(c['n'], c['p'], c['m'], c['per_col'], rank=rank, world=world)
+    else:
+        if world != 1:
+            raise SystemExit('workload %s is a single-GPU configuration' % name)
+        sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+        sh['colv'] = None
+        sh['n_total'], sh['p_total'] = c['n'], c['p']
+    Ax = torch.from_numpy(sh['Ax']).cuda()
+    if dist:
+        dist.all_reduce(Ax)
+    b = add_noise(Ax.cpu().numpy(), 0.02, seed=SEED)
+    return sh, b
+
+
+def build_engine(sh, b, world, dist, parts):
+    """(engine, run(first, count)) for one rank: the fused single-GPU loop, or
+    the column-sharded stages with the RCCL all-reduces (distributed.ShardedBB)."""
+    import torch
+    from device import BBEngine
+    opts = {'max_iter': 10 ** 12, 'opt_tol': 1e-30}
+    if world == 1:
+        eng = BBEngine(sh['A'], b, sh['block_sizes'], options=opts, early_exit=False,
+                       AT=sh['AT'], colv=sh.get('colv'))
+        eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+        eng.prologue()
+        return eng, eng.iterate
+    from distributed import ShardedBB, torch_all_reduce, torch_all_reduce_async
+    eng = BBEngine(sh['A'], None, sh['block_sizes'], options=opts, early_exit=False,
+                   AT=sh['AT'], colv=sh.get('colv'),
+                   target=torch.zeros(sh['m'], dtype=torch.float64))
+    # target = sum_g A_g x0_g - b (main.py:48 over the shards)
+    eng.x.copy_(eng.colv * eng.x0 if eng.scaled else eng.x0)
+    eng.stage(1, 0)
+    dist.all_reduce(eng.r)
+    eng.target.copy_(eng.r - torch.from_numpy(b).cuda())
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
+                    all_reduce_async=torch_all_reduce_async())
+    drv.prologue()
+    return eng, drv.iterate
+
+
+def time_run(run, steps, warmup, dist):
+    """W untimed iterations, then exactly K between barrier + synchronize on
+    both sides; max over ranks."""
+    import torch
+    run(1, warmup)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(1 + warmup, steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def kernel_table(eng, it0, reps, world, m, n, nz, p, nnz):
+    """Per-kernel HIP-event timing on the stream the kernels run on: each stage
+    launched `reps` times back to back between two events (the stages are
+    idempotent for a fixed iteration index), the stream held by a spin kernel
+    while the host enqueues, so no host gap sits inside an interval."""
+    import torch
+    kb = kernel_bytes(m, n, nz, p, nnz, nnz)
+    fb = format_bytes(eng)
+    k1 = 7 if world == 1 else 1          # sharded: the partial residual (stage 1)
+    kern = {}
+    for stg, nm in ((3, 'K2_spmvT_Nt_dots'), (4, 'K3_pava_clip_z2x'), (k1, 'K1_spmv_A')):
+        torch.cuda._sleep(int(2e8))
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(reps):
+            eng.stage(stg, it0)
+        ev[1].record()
+        torch.cuda.synchronize()
+        us = ev[0].elapsed_time(ev[1]) * 1e3 / reps
+        kern[nm] = {'avg_us': us, 'alg_bytes': kb[nm], 'GB_s': kb[nm] / (us * 1e-6) / 1e9,
+                    'frac': kb[nm] / (us * 1e-6) / HBM_PEAK, 'format_bytes': fb[nm],
+                    'format_GB_s': fb[nm] / (us * 1e-6) / 1e9}
+    kern['formats'] = {'K1': eng.fmt_A, 'K2': eng.fmt_AT}
+    return kern
+
+
+def roofline_of(kern, traffic_file=None):
+    names = [k for k in kern if k != 'formats']
+    dom = max(names, key=lambda k: kern[k]['avg_us'])
+    traffic = None
+    if traffic_file and os.path.exists(traffic_file):
+        try:
+            traffic = json.load(open(traffic_file)).get(dom, {}).get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+    return {'bound': 'hbm', 'kernel': dom, 'achieved': kern[dom]['GB_s'],
+            'peak': HBM_PEAK / 1e9, 'unit': 'GB/s', 'frac': kern[dom]['frac'],
+            'traffic': traffic, 'traffic_source': traffic_file and os.path.basename(traffic_file)}
+
+
+def host_info(threads):
+    import platform
+    model = platform.processor()
+    try:
+        for ln in open('/proc/cpuinfo'):
+            if ln.startswith('model name'):
+                model = ln.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {'nproc': os.cpu_count(), 'cpu_model': model, 'threads_used': threads,
+            'OMP_NUM_THREADS': os.environ.get('OMP_NUM_THREADS'),
+            'OPENBLAS_NUM_THREADS': os.environ.get('OPENBLAS_NUM_THREADS')}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--workload', default='C5', choices=['C5', 'C3'])
+    ap.add_argument('--parts', type=int, default=4,
+                    help='row parts of the pipelined residual all-reduce (N > 1)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--profile-iters', type=int, default=50)
+    ap.add_argument('--no-extras', action='store_true', help='skip the C3 / C2 / x-space / MD legs')
+    ap.add_argument('--profile-iters', type=int, default=20)
     args = ap.parse_args()
 
     import torch
@@ -254,131 +457,88 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from synthetic import make_shard, add_noise, SEED
-    from device import BBEngine, DeviceCSR
-    n_g, p_g, m_per, per_col = 1_000_000, 50_000, 100_000, 16
-    m = m_per   # weak scaling over routes: the network (rows) is shared, see the docstring
-    sh = make_shard(n_g, p_g, m, per_col, seed=SEED, rank=rank)
-    Ax = torch.from_numpy(sh['Ax']).cuda()
-    if dist:
-        dist.all_reduce(Ax)
-    b = add_noise(Ax.cpu().numpy(), 0.02, seed=SEED)
-    opts = {'max_iter': 10 ** 12, 'opt_tol': 1e-30}
-    if dist:
-        from distributed import ShardedBB, torch_all_reduce
-        A_dev = DeviceCSR(sh['A'])
-        x0 = torch.zeros(n_g, dtype=torch.float64, device='cuda')
-        x0[torch.from_numpy(np.cumsum(sh['block_sizes']) - 1).cuda()] = 1.0
-        part = A_dev.matvec(x0)
-        dist.all_reduce(part)
-        target = part - torch.from_numpy(b).cuda()
-        eng = BBEngine(sh['A'], None, sh['block_sizes'], options=opts, early_exit=False,
-                       A_dev=A_dev, AT=sh['AT'], target=target)
-        eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
-        drv = ShardedBB(eng, torch_all_reduce())
-        drv.prologue()
-        run = drv.iterate
-    else:
-        eng = BBEngine(sh['A'], b, sh['block_sizes'], options=opts, early_exit=False,
-                       AT=sh['AT'])
-        eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
-        eng.prologue()
-        run = eng.iterate
-    nnz = sh['A'].nnz
-    run(1, args.warmup)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(1 + args.warmup, args.steps)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    wl = args.workload
+    sh, b = build_problem(wl, world, rank, dist)
+    log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
+        % (wl, rank, world, sh['n'], sh['p'], sh['m'], sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
+    eng, run = build_engine(sh, b, world, dist, args.parts)
+    log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
+    el = time_run(run, args.steps, args.warmup, dist)
     it_s = args.steps / el
-    value = it_s * world
-    s = eng.scalars()
-    finite = bool(np.isfinite(s[4]))
+    finite = bool(np.isfinite(eng.scalars()[4]))
+    log('%d iterations in %.3f s: %.1f it/s' % (args.steps, el, it_s))
+    m, n_g, nz_g, p_g, nnz_g = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
+    kern = {}
+    if args.profile_iters > 0 and rank == 0:
+        kern = kernel_table(eng, 1 + args.warmup + args.steps, args.profile_iters, world,
+                            m, n_g, nz_g, p_g, nnz_g)
+        log('kernel table done')
+    if dist:
+        dist.barrier()
 
     out = None
     if rank == 0:
-        kb = kernel_bytes(m, n_g, eng.nz, p_g, nnz, sh['AT'].nnz)
-        fb = format_bytes(eng)
-        kern = {}
-        if world == 1 and args.profile_iters > 0:
-            # per-kernel HIP-event timing on the stream the kernels run on:
-            # each stage launched profile_iters times back to back between two
-            # events (the stages are idempotent for a fixed iteration index:
-            # same inputs, same outputs, tickets self-resetting), after the
-            # timed run.  The stream is held by a spin kernel while the host
-            # enqueues, so no host gap sits inside an interval; what remains
-            # beyond rocprofv3's kernel time is the dispatch gap, amortised.
-            names = [(3, 'K2_spmvT_Nt_dots'), (4, 'K3_pava_clip_z2x'), (7, 'K1_spmv_A')]
-            acc = {nm: [] for _, nm in names}
-            it0 = 1 + args.warmup + args.steps
-            for stg, nm in names:
-                torch.cuda._sleep(int(2e8))
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                ev[0].record()
-                for _ in range(args.profile_iters):
-                    eng.stage(stg, it0)
-                ev[1].record()
-                torch.cuda.synchronize()
-                acc[nm].append(ev[0].elapsed_time(ev[1]) * 1e3 / args.profile_iters)
-            for nm, v in acc.items():
-                us = float(np.mean(v))
-                kern[nm] = {'avg_us': us, 'alg_bytes': kb[nm],
-                            'GB_s': kb[nm] / (us * 1e-6) / 1e9,
-                            'frac': kb[nm] / (us * 1e-6) / HBM_PEAK,
-                            'format_bytes': fb[nm],
-                            'format_GB_s': fb[nm] / (us * 1e-6) / 1e9}
-        dom = max(kern, key=lambda k: kern[k]['avg_us']) if kern else None
-        traffic = None
-        tfile = os.path.join(ROOT, 'profiles', 'traffic_r01.json')
-        if dom and os.path.exists(tfile):
-            try:
-                traffic = json.load(open(tfile)).get(dom, {}).get('hbm_bytes_per_launch')
-            except Exception:
-                traffic = None
-        roof = None
-        if dom:
-            roof = {'bound': 'hbm', 'kernel': dom,
-                    'achieved': kern[dom]['GB_s'], 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
-                    'frac': kern[dom]['frac'], 'traffic': traffic}
-        ib = survey_iter_bytes(m, n_g * world, eng.nz * world, nnz * world)
-        proj = bench_proj() if world == 1 else None
-        xspace = bench_xspace(sh, b) if world == 1 else None
-        mdr = bench_md(sh, b) if world == 1 else None
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cps, cit, cel = cpu_baseline_bb(sh['A'], b, sh['block_sizes'])
-            cpu = {'value': cps, 'unit': 'BB it/s', 'cores': 1, 'kind': 'port',
-                   'sample': '%d BB iterations (%.1f s) of the same C3 problem: oracle '
-                             'restatement of BB.py over SciPy csr_matvec + C PAVA, '
-                             'OPENBLAS_NUM_THREADS=1' % (cit, cel)}
+        n_tot, p_tot = sh['n_total'], sh['p_total']
+        nnz_tot = 16 * n_tot
+        ib = survey_iter_bytes(m, n_tot, n_tot - p_tot, nnz_tot)
+        tfile = os.path.join(ROOT, 'profiles', 'traffic_r02.json')
         out = {
-            'metric': METRIC, 'value': value,
-            'unit': 'BB iterations/s (1M-route problem; N x 1M routes at N GPUs)',
+            'metric': METRIC, 'value': it_s,
+            'unit': 'BB iterations/s of the whole job (%s: %d routes / %d blocks / %d links)'
+                    % (wl, n_tot, p_tot, m),
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': 'C3: BB (z-space, PAVA projection) on 1M routes / 50k '
-                                   'blocks / %d links / %d nnz per GPU' % (m, nnz),
-                       'routes_per_gpu': n_g, 'blocks_per_gpu': p_g, 'links': m,
-                       'nnz_per_gpu': nnz, 'parallelism': 'column-shard x%d' % world},
-            'roofline': roof,
-            'iteration_roofline': {'survey_bytes_per_iter': ib,
-                                   'achieved_GB_s': ib * it_s / 1e9,
-                                   'frac': ib * it_s / HBM_PEAK},
-            'kernels': kern, 'proj_simplex': proj, 'xspace_bb': xspace, 'mirror_descent': mdr,
-            'cpu_baseline': cpu,
-            'finite': finite,
+            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
+            'config': {'workload': '%s: BB (z-space, PAVA projection) on %d routes / %d blocks / '
+                                   '%d links / %d nnz, column-sharded over %d GPU(s)'
+                                   % (wl, n_tot, p_tot, m, nnz_tot, world),
+                       'routes': n_tot, 'blocks': p_tot, 'links': m, 'nnz': nnz_tot,
+                       'routes_rank0': n_g, 'nnz_rank0': nnz_g,
+                       'parallelism': 'column-shard x%d' % world,
+                       'residual_allreduce_parts': args.parts if world > 1 else None},
+            'roofline': roofline_of(kern, tfile) if kern else None,
+            'iteration_roofline': {'survey_bytes_per_iter': ib, 'achieved_GB_s': ib * it_s / 1e9,
+                                   'frac': ib * it_s / HBM_PEAK,
+                                   'note': 'whole job over all GPUs; peak is one GPU'},
+            'kernels': kern, 'finite': finite,
         }
+    # --- N = 1 extras: the BASELINE metric's C3 problem and the other legs ---------
+    if world == 1 and not args.no_extras:
+        del eng, run
+        torch.cuda.empty_cache()
+        sh3, b3 = build_problem('C3', 1, 0, None)
+        eng3, run3 = build_engine(sh3, b3, 1, None, 1)
+        el3 = time_run(run3, max(args.steps, 50), args.warmup, None)
+        its3 = max(args.steps, 50) / el3
+        c = sh3['A']
+        kern3 = kernel_table(eng3, 1 + args.warmup + max(args.steps, 50), 50, 1,
+                             eng3.m, eng3.n, eng3.nz, eng3.layout.p, c.nnz)
+        ib3 = survey_iter_bytes(eng3.m, eng3.n, eng3.nz, c.nnz)
+        log('C3: %.1f it/s' % its3)
+        out['c3'] = {'value': its3, 'unit': 'BB iterations/s (C3: 1M routes / 50k blocks / '
+                                            '100k links / 16M nnz, 1 GPU)',
+                     'ms_per_step': el3 / max(args.steps, 50) * 1e3, 'kernels': kern3,
+                     'roofline': roofline_of(kern3, os.path.join(ROOT, 'profiles',
+                                                                 'traffic_r02.json')),
+                     'iteration_roofline': {'survey_bytes_per_iter': ib3,
+                                            'achieved_GB_s': ib3 * its3 / 1e9,
+                                            'frac': ib3 * its3 / HBM_PEAK}}
+        del eng3, run3
+        out['proj_simplex'] = bench_proj()
+        log('C2 projection done')
+        out['isotonic'] = bench_iso()
+        out['xspace_bb'] = bench_xspace(sh3, b3)
+        out['mirror_descent'] = bench_md(sh3, b3)
+        log('extras done')
+        if not args.no_cpu_baseline:
+            cps, cit, cel = cpu_baseline_bb(sh3['A'], b3, sh3['block_sizes'])
+            out['cpu_baseline'] = {
+                'value': cps, 'unit': 'BB it/s (C3)', 'cores': 1, 'kind': 'port',
+                'sample': '%d BB iterations (%.1f s) of the C3 problem: oracle restatement of '
+                          'BB.py over SciPy csr_matvec + C PAVA' % (cit, cel),
+                'host': host_info(1)}
+            log('CPU baseline done')
+    if out is not None:
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

@@ -51,6 +51,7 @@ class Panels(ctypes.Structure):
 
 TILE_THREADS = 1024       # BSLS_TILE_THREADS
 TILE_MAXSLOTS = 20        # BSLS_TILE_MAXSLOTS
+TILE_LDS_BYTES = 163840 - 512   # dynamic LDS a tile kernel may take (bb.hip PANEL_LDS_MAX)
 
 
 class Tiles(ctypes.Structure):
@@ -133,6 +134,8 @@ _SIGS = {
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
+    'bsls_bb_row_blocks': (_i64, [ctypes.POINTER(BBProblem), _vp]),
+    'bsls_bb_residual_rows': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _i64, _vp]),
     'bsls_md_update_gated': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _dbl, _i64, _vp, _vp, _sz,
                                     _vp]),
     'bsls_md_pack_workspace_size': (_sz, [_i64]),

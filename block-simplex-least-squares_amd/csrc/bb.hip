@@ -170,13 +170,13 @@ __device__ __forceinline__ void k1_finish(const bsls_bb_problem &P, int64_t iter
 // ||r||^2 to the last row block, which records f and runs the stopping test.
 template <int MODE, bool ITER, bool ADD, bool REDUCE>
 __global__ __launch_bounds__(1024) void bb_k1(bsls_bb_problem P, int64_t iter, unsigned *tkrb,
-                                              double *part, unsigned *ticket) {
+                                              double *part, unsigned *ticket, int64_t rb_base) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int row_last;
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_panels &M = P.A;
     const int64_t G = M.ngroups;
-    const int64_t g = blockIdx.x % G, rb = blockIdx.x / G;
+    const int64_t g = blockIdx.x % G, rb = rb_base + blockIdx.x / G;
     const int wv = threadIdx.x / WAVE, lane = lane_id();
     const int64_t panel = rb * PANEL_WAVES + wv;
     double s[4] = {0.0, 0.0, 0.0, 0.0};
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(1024) void bb_k1(bsls_bb_problem P, int64_t iter, u
 // G workgroups finishes (group order) -- as bb_k1.
 template <int MODE, bool ITER, bool ADD, bool REDUCE>
 __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, unsigned *tkrb,
-                                               double *part, unsigned *ticket) {
+                                               double *part, unsigned *ticket, int64_t rb_base) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ double red[16];
     __shared__ int row_last;
@@ -223,6 +223,7 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
     const bsls_tiles &T = P.At;
     int64_t rb, g;
     tile_map(T, blockIdx.x, rb, g);
+    rb += rb_base;
     const int HR = (int)tile_lds_doubles(T, false);
     for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;
     __syncthreads();
@@ -257,7 +258,10 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
 // over r's column groups (one group: in CSR order, bit-identical to SciPy;
 // several: partials in wpart, summed in group order by the block's last
 // workgroup); then g = N'w, dg and the four BB sums, as bb_k2.  MODE 1: stored
-// values; MODE 2: scaled incidence (each term colv[row] * r_i, SciPy's product).
+// values; MODE 2: scaled incidence, each term colv[row] * r_i (SciPy's
+// product; the rows' scales sit in LDS beside the sums); MODE 3: scaled
+// incidence with several groups (no bit pattern to keep): w_i = colv_i *
+// sum r, one product per row after the group sums, and the whole LDS for rows.
 template <int MODE, bool ITER>
 __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
                                                const double *__restrict__ gp,
@@ -280,7 +284,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
         if (MODE == 2) rc[i] = (i < nloc) ? P.colv[i0 + i] : 0.0;
     }
     __syncthreads();
-    tile_walk<MODE>(T, rb, g, P.r, rows, rc);
+    tile_walk<(MODE == 3 ? 0 : MODE)>(T, rb, g, P.r, rows, rc);
     __syncthreads();
     const int64_t G = T.ngroups;
     bool fin = true;
@@ -306,7 +310,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
                 for (int64_t c = 0; c < G; ++c)
                     o += __hip_atomic_load(&P.wpart[(c * T.nrb + rb) * (T.H + 1) + i],
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                rows[i] = o;
+                rows[i] = (MODE == 3) ? P.colv[i0 + i] * o : o;
             }
             __syncthreads();
         }
@@ -651,33 +655,41 @@ static void allow_lds(K kernel) {
     }
 }
 
+// K1's row blocks: panels 16 panels each, tiles H rows each
+static int64_t k1_row_blocks(const bsls_bb_problem &P) {
+    return P.At.ent ? P.At.nrb : (P.A.npanels + PANEL_WAVES - 1) / PANEL_WAVES;
+}
+
+// row blocks [rb0, rb1) of K1 (the whole matrix unless a multi-GPU driver
+// all-reduces r part by part behind it); REDUCE needs the whole matrix
 template <int MODE, bool ADD, bool REDUCE, bool ITER>
 static void launch_k1_mode(const bsls_bb_problem &P, int64_t iter, const BBWork &w,
-                           hipStream_t st) {
-    const int64_t rbs = (P.A.npanels + PANEL_WAVES - 1) / PANEL_WAVES;
+                           hipStream_t st, int64_t rb0, int64_t rb1) {
     allow_lds(bb_k1<MODE, ITER, ADD, REDUCE>);
-    bb_k1<MODE, ITER, ADD, REDUCE><<<(int)(P.A.ngroups * rbs), 1024, panel_lds_bytes(P.A), st>>>(
-        P, iter, w.tkrb, w.p1, w.tk1);
+    bb_k1<MODE, ITER, ADD, REDUCE><<<(int)(P.A.ngroups * (rb1 - rb0)), 1024, panel_lds_bytes(P.A),
+                                     st>>>(P, iter, w.tkrb, w.p1, w.tk1, rb0);
 }
 
 template <int MODE, bool ADD, bool REDUCE, bool ITER>
 static void launch_k1t_mode(const bsls_bb_problem &P, int64_t iter, const BBWork &w,
-                            hipStream_t st) {
+                            hipStream_t st, int64_t rb0, int64_t rb1) {
     allow_lds(bb_k1t<MODE, ITER, ADD, REDUCE>);
-    bb_k1t<MODE, ITER, ADD, REDUCE><<<(int)(P.At.nrb * P.At.ngroups), BSLS_TILE_THREADS,
+    bb_k1t<MODE, ITER, ADD, REDUCE><<<(int)((rb1 - rb0) * P.At.ngroups), BSLS_TILE_THREADS,
                                       tile_lds_doubles(P.At, false) * 8, st>>>(P, iter, w.tkrb,
-                                                                                w.p1, w.tk1);
+                                                                                w.p1, w.tk1, rb0);
 }
 
 template <bool ADD, bool REDUCE, bool ITER>
-static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, hipStream_t st) {
+static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, hipStream_t st,
+                      int64_t rb0 = 0, int64_t rb1 = -1) {
+    if (rb1 < 0) rb1 = k1_row_blocks(P);
     if (P.At.ent) {
-        if (P.colv) launch_k1t_mode<0, ADD, REDUCE, ITER>(P, iter, w, st);
-        else launch_k1t_mode<1, ADD, REDUCE, ITER>(P, iter, w, st);
+        if (P.colv) launch_k1t_mode<0, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1);
+        else launch_k1t_mode<1, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1);
     } else if (P.colv) {
-        launch_k1_mode<0, ADD, REDUCE, ITER>(P, iter, w, st);
+        launch_k1_mode<0, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1);
     } else {
-        launch_k1_mode<1, ADD, REDUCE, ITER>(P, iter, w, st);
+        launch_k1_mode<1, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1);
     }
 }
 
@@ -702,8 +714,9 @@ template <bool ITER>
 static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
                       const BBWork &w, hipStream_t st) {
     if (P.ATt.ent) {
-        if (P.colv) launch_k2t_mode<2, ITER>(P, gp, gout, w, st);
-        else launch_k2t_mode<1, ITER>(P, gp, gout, w, st);
+        if (!P.colv) launch_k2t_mode<1, ITER>(P, gp, gout, w, st);
+        else if (P.ATt.ngroups == 1) launch_k2t_mode<2, ITER>(P, gp, gout, w, st);
+        else launch_k2t_mode<3, ITER>(P, gp, gout, w, st);
     } else if (P.colv) {
         launch_k2_mode<2, ITER>(P, gp, gout, w, st);
     } else {
@@ -750,7 +763,8 @@ static int check_problem(const bsls_bb_problem *p) {
         return BSLS_E_ARG;
     }
     if (p->ATt.ent) {
-        if (!tiles_ok(p->ATt, p->n, p->m, 1, general, !general)) return BSLS_E_ARG;
+        if (!tiles_ok(p->ATt, p->n, p->m, 1, general, !general && p->ATt.ngroups == 1))
+            return BSLS_E_ARG;
         if (p->ATt.ngroups > 1 && !p->wpart) return BSLS_E_ARG;
     } else if (!panels_ok(p->AT, p->n, p->m, 1, general) || p->AT.ngroups != 1) {
         return BSLS_E_ARG;
@@ -813,6 +827,29 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
         default:
             return BSLS_E_ARG;
     }
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" int64_t bsls_bb_row_blocks(const bsls_bb_problem *p, int64_t *rows_per_block) {
+    const int rc = check_problem(p);
+    if (rc != BSLS_OK) return rc;
+    if (rows_per_block)
+        *rows_per_block = p->At.ent ? p->At.H : (int64_t)PANEL_WAVES * p->A.prow;
+    return k1_row_blocks(*p);
+}
+
+extern "C" int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0,
+                                     int64_t rb1, void *stream) {
+    const int rc = check_problem(p);
+    if (rc != BSLS_OK) return rc;
+    const bsls_bb_problem &P = *p;
+    if (rb0 < 0 || rb1 <= rb0 || rb1 > k1_row_blocks(P)) return BSLS_E_ARG;
+    if (P.At.ent && P.At.order != 0 && (rb0 != 0 || rb1 != P.At.nrb)) return BSLS_E_ARG;
+    const BBWork w = bb_layout(P);
+    hipStream_t st = (hipStream_t)stream;
+    if (iter > 0) launch_k1<false, false, true>(P, iter, w, st, rb0, rb1);
+    else launch_k1<false, false, false>(P, iter, w, st, rb0, rb1);
     BSLS_LAUNCH_CHECK();
     return BSLS_OK;
 }

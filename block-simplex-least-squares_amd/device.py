@@ -267,23 +267,31 @@ class DevicePanels:
         return sum(v.numel() * v.element_size() for v in self.t.values())
 
 
-def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=3 << 20):
+def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=None):
     """(H, ngroups, order) of a tile image (include/bsls_hip.h struct bsls_tiles,
     csrc/tiles.hpp): column groups (a power of two) until one group's slice of
     the gathered vector fits an XCD's L2 (order 1, XCD-sequential, past 8
-    groups); row blocks as tall as the LDS holds (half of it with K2's column
-    scales), at least one workgroup per CU, the grid rounded up to whole rounds
-    of `cus` workgroups.  BSLS_TILE_PLAN="H,groups" overrides it."""
-    plan = os.environ.get('BSLS_TILE_PLAN')
+    groups); row blocks as tall as the LDS holds (half of it when K2 keeps the
+    column scales beside the sums: scaled incidence, one group), at least one
+    workgroup per CU, the grid rounded up to whole rounds of `cus` workgroups.
+    The environment variable `env` ("H,groups") overrides it."""
+    plan = os.environ.get(env) if env else None
     if plan:
         H, G = (int(v) for v in plan.split(','))
         return H, G, (1 if G > 8 else 0)
+    if l2_slice is None:
+        # measured on the C5 shard (tools/stage_time.py): K1 fastest with
+        # 2.5-MB slices of x (4 groups: 112 us, 8: 148 us), K2 with the whole
+        # 8-MB r in one group (117 us; 2: 122, 4: 150) -- one group also keeps
+        # K2 bit-identical to SciPy
+        l2_slice = (8 << 20) if halo else (3 << 20)
     G = 1
     while 8 * cols / G > l2_slice and G < 64:
         G *= 2
     G = max(1, min(G, cols))
     order = 1 if G > 8 else 0
-    per = _native.TILE_MAXSLOTS // (2 if colv_lds else 1) - 1
+    mult = 2 if (colv_lds and G == 1) else 1
+    per = _native.TILE_LDS_BYTES // (8 * _native.TILE_THREADS * mult) - 1
     hmax = per * _native.TILE_THREADS - halo
     nrb = max(-(-rows // hmax), -(-cus // G))
     nrb = -(-(nrb * G) // cus) * cus // G if nrb * G > cus else nrb
@@ -358,7 +366,8 @@ class DeviceTiles:
         M = sps.csr_matrix(M)
         M.sort_indices()
         R, C = M.shape
-        H, G, order = plan or tile_plan(R, C, halo, colv_lds)
+        H, G, order = plan or tile_plan(R, C, halo, colv_lds,
+                                        env='BSLS_TILE_PLAN_AT' if halo else 'BSLS_TILE_PLAN_A')
         gc = np.round(np.linspace(0, C, G + 1)).astype(np.int64)
         if np.any(np.diff(gc) < 1):
             raise ValueError('more column groups than columns')
@@ -522,7 +531,7 @@ class BBEngine:
 
     def __init__(self, A, b, block_sizes, options=None, early_exit=True, A_dev=None,
                  AT_dev=None, AT=None, target=None, x0=None, general=False, fmt=None,
-                 tile_plans=(None, None)):
+                 tile_plans=(None, None), colv=None):
         torch = _torch()
         L = _native.lib()
         self.layout = lay = BlockLayout(block_sizes)
@@ -530,12 +539,18 @@ class BBEngine:
         if A.shape[1] != lay.n:
             raise ValueError('A has %d columns but the blocks cover %d' % (A.shape[1], lay.n))
         AT = sps.csr_matrix(AT) if AT is not None else A.T.tocsr()
-        self.A = A_dev or DeviceCSR(A)
-        self.AT = AT_dev or DeviceCSR(AT)
+        # the general CSR copies (closures f / nabla_f, DORE, LBFGS, LS_postprocess)
+        # are uploaded on first use: the fused loop never reads them
+        self._A_host, self._AT_host = A, AT
+        self._A_dev, self._AT_dev = A_dev, AT_dev
         self.m, self.n, self.nz = A.shape[0], lay.n, lay.nz
-        # the fused kernels' panel images: A with its column chunks in k1_plan's
-        # groups (K1), A' with halo rows (K2); values dropped for a scaled incidence
-        colv = None if general else scaled_incidence_scale(A)
+        # the fused kernels' images: A (K1), A' with halo rows (K2), each as
+        # panels or streamed tiles (spmv_format); values dropped for a scaled
+        # incidence (colv: the caller's column scales, else detected)
+        if colv is None and not general:
+            colv = scaled_incidence_scale(A)
+        elif general:
+            colv = None
         self.scaled = colv is not None
         # per matrix: panels (dense row blocks, C3) or streamed tiles (C5)
         self.fmt_A, self.fmt_AT = spmv_format(A, fmt), spmv_format(AT, fmt)
@@ -562,13 +577,13 @@ class BBEngine:
         if target is not None:
             # column-sharded: the caller formed sum_g A_g x0_g - b (distributed.py)
             self.target = torch.as_tensor(target, dtype=torch.float64).cuda().contiguous()
+            xin = None
         else:
-            # target = A x0 - b (python/main.py:48), on the device; x0 defaults
-            # to the particular solution, as BSLSMatrices.initial_solution does
+            # target = A x0 - b (python/main.py:48), formed after the images are
+            # up by the engine's own K1; x0 defaults to the particular solution,
+            # as BSLSMatrices.initial_solution does
             xin = x0 if x is None else torch.as_tensor(np.asarray(x, dtype=np.float64)).cuda()
-            b_dev = torch.as_tensor(np.asarray(b, dtype=np.float64)).cuda()
-            self.target = torch.empty(self.m, **dev)
-            self.A.matvec(xin, out=self.target, add=-b_dev)
+            self.target = -torch.as_tensor(np.asarray(b, dtype=np.float64)).cuda()
         self.z = [torch.zeros(max(self.nz, 1), **dev) for _ in range(2)]
         self.g = [torch.zeros(max(self.nz, 1), **dev) for _ in range(2)]
         self.x = torch.empty(lay.n, **dev)
@@ -618,6 +633,22 @@ class BBEngine:
         P.early_exit = 1 if early_exit else 0
         self.P = P
         self.z0 = None
+        if xin is not None:
+            self.x.copy_(self.colv * xin if self.scaled else xin)
+            self.stage(7, 0)                       # r = A x0 + (-b)
+            self.target.copy_(self.r)
+
+    @property
+    def A(self):
+        if self._A_dev is None:
+            self._A_dev = DeviceCSR(self._A_host)
+        return self._A_dev
+
+    @property
+    def AT(self):
+        if self._AT_dev is None:
+            self._AT_dev = DeviceCSR(self._AT_host)
+        return self._AT_dev
 
     # -- raw device steps ------------------------------------------------------
     def set_z0(self, z0):
@@ -639,6 +670,20 @@ class BBEngine:
         """One building block of an iteration (bsls_bb_stage, include/bsls_hip.h)."""
         check(_native.lib().bsls_bb_stage(self.P, int(k), int(it), stream_handle()),
               'bsls_bb_stage %d' % k)
+
+    def row_blocks(self):
+        """(K1 row blocks, rows per block): the granule of residual_rows."""
+        R = ctypes.c_int64(0)
+        nb = _native.lib().bsls_bb_row_blocks(self.P, ctypes.byref(R))
+        if nb < 0:
+            check(int(nb), 'bsls_bb_row_blocks')
+        return int(nb), int(R.value)
+
+    def residual_rows(self, it, rb0, rb1, stream=None):
+        """Stage 1 on K1 row blocks [rb0, rb1) (bsls_bb_residual_rows)."""
+        check(_native.lib().bsls_bb_residual_rows(self.P, int(it), int(rb0), int(rb1),
+                                                  stream_handle(stream)),
+              'bsls_bb_residual_rows')
 
     # -- closures of main.solve_in_z (python/main.py:53-65), on the device ------
     def n_apply(self, z, with_x0=False, out=None):

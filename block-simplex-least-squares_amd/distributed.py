@@ -44,30 +44,66 @@ def partition_blocks(block_sizes, col_weights, world):
     return np.array(bounds, dtype=np.int64)
 
 
+def row_parts(nblocks, parts):
+    """parts + 1 row-block bounds splitting K1's row blocks into `parts` runs."""
+    parts = max(1, min(int(parts), int(nblocks)))
+    return [int(v) for v in np.round(np.linspace(0, nblocks, parts + 1)).astype(np.int64)]
+
+
 class ShardedBB:
     """Drive one rank's stages with the all-reduces between them.
 
     `engine` exposes stage(k, it), r (m-vector), scal (BSLS_S_COUNT vector) --
-    device.BBEngine on GPUs; a numpy/torch fake in the gloo tests.
-    `all_reduce(t)` sums a tensor in place across ranks."""
+    device.BBEngine on GPUs; a numpy/torch fake in the gloo tests -- and, for
+    the overlapped residual, row_blocks() and residual_rows(it, rb0, rb1).
+    `all_reduce(t)` sums a tensor in place across ranks; `all_reduce_async(t)`
+    starts that sum and returns a handle with wait().
+
+    With parts > 1 the residual's all-reduce is pipelined behind K1 (SURVEY.md
+    §8(e)): K1 runs on row parts one after the other on the compute stream; as
+    soon as part p is enqueued its rows of r are all-reduced asynchronously
+    (RCCL on its own stream, ordered after part p only), so the exchange of
+    part p overlaps the computation of part p + 1; the compute stream waits
+    for every part before stage 2."""
 
     SUMS = slice(5, 9)   # scal[SUMDG..GG]
 
-    def __init__(self, engine, all_reduce):
+    def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None):
         self.e = engine
         self.all_reduce = all_reduce
+        self.all_reduce_async = all_reduce_async
+        self.parts = int(parts) if all_reduce_async is not None else 1
+        self._slices = None
+        if self.parts > 1:
+            nb, R = engine.row_blocks()
+            m = engine.r.shape[0]
+            b = row_parts(nb, self.parts)
+            self._slices = [(b[k], b[k + 1], b[k] * R, min(b[k + 1] * R, m))
+                            for k in range(len(b) - 1)]
+
+    def residual(self, it):
+        """r = sum over ranks of A_g x_g (before stage 2)."""
+        e = self.e
+        if not self._slices:
+            e.stage(1, it)
+            self.all_reduce(e.r)
+            return
+        works = []
+        for rb0, rb1, r0, r1 in self._slices:
+            e.residual_rows(it, rb0, rb1)
+            works.append(self.all_reduce_async(e.r[r0:r1]))
+        for w in works:
+            w.wait()
 
     def prologue(self):
         e = self.e
         e.stage(0, 0)
         e.stage(5, 0)            # z[1] = z0 + 1, x = x0 + N z[1]
-        e.stage(1, 0)
-        self.all_reduce(e.r)
+        self.residual(0)
         e.stage(2, 0)            # r(z0 + 1)
         e.stage(3, 0)            # g_prev = grad(z0 + 1) -> g[0]
         e.stage(6, 0)            # x = x0 + N z0
-        e.stage(1, 0)
-        self.all_reduce(e.r)
+        self.residual(0)
         e.stage(2, 0)            # r(z0), f(z0)
 
     def iterate(self, first, count):
@@ -76,8 +112,7 @@ class ShardedBB:
             e.stage(3, i)
             self.all_reduce(e.scal[self.SUMS])
             e.stage(4, i)
-            e.stage(1, i)
-            self.all_reduce(e.r)
+            self.residual(i)
             e.stage(2, i)
 
 
@@ -86,4 +121,12 @@ def torch_all_reduce(group=None):
 
     def f(t):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return f
+
+
+def torch_all_reduce_async(group=None):
+    import torch.distributed as dist
+
+    def f(t):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
     return f

@@ -60,6 +60,61 @@ def make_shard(n, p, m, per_col=16, seed=SEED, rank=0):
     return dict(A=A, AT=AT, block_sizes=sizes, x_true=x_split, f=f, Ax=Ax, m=m, n=n, p=p)
 
 
+def make_partitioned(n, p, m, per_col=16, rank=0, world=1, seed=SEED, gen_chunks=256,
+                     need_csr_values=False):
+    """Rank `rank`'s column shard of ONE problem that does not depend on `world`
+    (strong scaling, BASELINE config C5): block sizes multinomial(n - p, 1/p) + 1
+    from one stream; blocks split into `gen_chunks` fixed generation chunks,
+    each drawing its flows, Dirichlet splits and rows from its own stream
+    (seed, 1000 + k); the shard = the contiguous run of whole blocks that
+    distributed.partition_blocks gives this rank (balanced by nnz = per_col x
+    routes, bsls_matrices.py:109-126 keeps blocks whole).  The union of the
+    shards is the same matrix for every world size.
+
+    Returns dict(A, AT (CSR, scaled incidence: every stored entry of column j
+    is colv[j]), colv, block_sizes, x_true, Ax (= A_g x_true_g: sum over ranks
+    for b), bounds (block partition), col0 (first column), n, p, m, nnz)."""
+    from distributed import partition_blocks
+    rs = np.random.RandomState(seed)
+    sizes = rs.multinomial(n - p, np.ones(p) / p) + 1
+    bounds = partition_blocks(sizes, per_col * sizes.astype(np.float64), world)
+    b0, b1 = int(bounds[rank]), int(bounds[rank + 1])
+    cb = np.linspace(0, p, gen_chunks + 1).astype(np.int64)
+    k0 = int(np.searchsorted(cb, b0, side='right') - 1)
+    k1 = int(np.searchsorted(cb, b1, side='left'))
+    f_l, x_l, rows_l = [], [], []
+    for k in range(k0, k1):
+        c0, c1 = int(cb[k]), int(cb[k + 1])
+        sz = sizes[c0:c1]
+        nk = int(sz.sum())
+        crs = np.random.RandomState([seed, 1000 + k])
+        f = np.maximum(np.floor(crs.random_sample(c1 - c0) * 1000), 1.0)
+        e = crs.standard_exponential(nk)
+        bid = np.repeat(np.arange(c1 - c0), sz)
+        sums = np.bincount(bid, weights=e, minlength=c1 - c0)
+        rows = _distinct_rows(crs, m, nk, per_col)
+        # keep this rank's blocks of the chunk
+        lo, hi = max(b0, c0) - c0, min(b1, c1) - c0
+        xs = np.concatenate(([0], np.cumsum(sz)))
+        f_l.append(np.repeat(f[lo:hi], sz[lo:hi]))
+        x_l.append((e / sums[bid])[xs[lo]:xs[hi]])
+        rows_l.append(rows[xs[lo]:xs[hi]])
+    colv = np.concatenate(f_l)
+    x_true = np.concatenate(x_l)
+    rows = np.concatenate(rows_l)
+    ng = colv.shape[0]
+    indptr = np.arange(0, per_col * (ng + 1), per_col, dtype=np.int64)
+    vals = np.repeat(colv, per_col)
+    AT = sps.csr_matrix((vals, rows.reshape(-1).astype(np.int32), indptr), shape=(ng, m))
+    A = AT.T.tocsr()
+    A.sort_indices()
+    Ax = A.dot(x_true)
+    col0 = int(sizes[:b0].sum())
+    return dict(A=A, AT=AT, colv=colv, block_sizes=sizes[b0:b1], x_true=x_true, Ax=Ax,
+                bounds=bounds, col0=col0, n=ng, p=b1 - b0, m=m, nnz=int(A.nnz),
+                n_total=n, p_total=p)
+
+
 def add_noise(b, noise, seed=SEED):
     """b + N(0, (|b| noise)^2) elementwise (python/main.py:164-166)."""
     if not noise:

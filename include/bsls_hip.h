@@ -283,6 +283,13 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  * One iteration i >= 1 = 3, [allreduce sums], 4, 1, [allreduce r], 2; on one GCD
  * bsls_bb_iterate runs 3, 4, 7. */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
+/* Stage 1 restricted to K1's row blocks [rb0, rb1) (rows rb0 * R .. rb1 * R - 1,
+ * R = *rows_per_block from bsls_bb_row_blocks, which returns the block count):
+ * a multi-GPU driver all-reduces r part by part while the next part computes.
+ * Tile images with order 1 only take the whole range. */
+int64_t bsls_bb_row_blocks(const bsls_bb_problem *p, int64_t *rows_per_block);
+int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
+                          void *stream);
 
 /* ---- x-space least-squares operator on panel images -------------------------
  * Replaces sparse_least_squares_obj's two SciPy products

@@ -50,6 +50,15 @@ class FakeStages:
             g[self.zst[b]:self.zst[b] + k - 1] = w[xs:xs + k - 1] - w[xs + 1:xs + k]
         return g
 
+    ROWS = 97   # rows per K1 row block (residual_rows granule)
+
+    def row_blocks(self):
+        return -(-self.A.shape[0] // self.ROWS), self.ROWS
+
+    def residual_rows(self, it, rb0, rb1):
+        r0, r1 = rb0 * self.ROWS, min(rb1 * self.ROWS, self.A.shape[0])
+        self.r[r0:r1] = torch.from_numpy(self.A[r0:r1].dot(self.x))
+
     def stage(self, k, it):
         s = self.scal
         zc, zn = (it - 1) & 1, it & 1
@@ -95,7 +104,12 @@ def _problem():
     return sh, b
 
 
-def _run(rank, world, iters, out_q):
+class _Done:
+    def wait(self):
+        pass
+
+
+def _run(rank, world, iters, out_q, parts=1):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, PKG)
     from oracle import oracle as orc
@@ -103,8 +117,10 @@ def _run(rank, world, iters, out_q):
     if world > 1:
         dist.init_process_group('gloo', rank=rank, world_size=world)
         red = lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        red_async = lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
     else:
         red = lambda t: None
+        red_async = lambda t: _Done()
     sh, b = _problem()
     sizes = sh['block_sizes']
     bounds = partition_blocks(sizes, sizes * 8.0, world)
@@ -118,7 +134,7 @@ def _run(rank, world, iters, out_q):
     red(part)
     target = part.numpy() - b
     eng = FakeStages(A_g, A_g.T.tocsr(), sz_g, target, orc, iters)
-    drv = ShardedBB(eng, red)
+    drv = ShardedBB(eng, red, parts=parts, all_reduce_async=red_async)
     drv.prologue()
     traj = {}
     for i in range(1, iters + 1):
@@ -129,12 +145,12 @@ def _run(rank, world, iters, out_q):
         dist.destroy_process_group()
 
 
-def _spawn(world, iters):
+def _spawn(world, iters, parts=1):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
-    os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000))
+    os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000) + 7 * parts)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_run, args=(r, world, iters, q)) for r in range(world)]
+    procs = [ctx.Process(target=_run, args=(r, world, iters, q, parts)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
@@ -157,3 +173,49 @@ def test_two_rank_sharded_bb_matches_single_and_oracle(orc):
     for i in one:
         d = np.max(np.abs(two[i] - ref[i])) / max(1.0, np.max(np.abs(ref[i])))
         assert d < 1e-8, (i, d)
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_overlapped_residual_matches_single(orc):
+    """The residual all-reduced in 3 row parts, asynchronously, behind K1's
+    row parts (ShardedBB parts > 1): same trajectory as the single rank."""
+    iters = 12
+    one = _spawn(1, iters)
+    three = _spawn(2, iters, parts=3)
+    for i in one:
+        d = np.max(np.abs(one[i] - three[i])) / max(1.0, np.max(np.abs(one[i])))
+        assert d < 1e-10, (i, d)
+
+
+def test_row_parts():
+    sys.path.insert(0, PKG)
+    from distributed import row_parts
+    assert row_parts(10, 3) == [0, 3, 7, 10]
+    assert row_parts(2, 5) == [0, 1, 2]
+    assert row_parts(7, 1) == [0, 7]
+
+
+def test_partitioned_problem_is_world_independent():
+    """synthetic.make_partitioned (config C5's generator): the shards of every
+    world size concatenate to the same matrix, x_true and block sizes, and the
+    partial products sum to the same b."""
+    sys.path.insert(0, PKG)
+    import scipy.sparse as sps
+    from synthetic import make_partitioned
+    full = make_partitioned(60_000, 3_000, 5_000, gen_chunks=8)
+    for world in (2, 3):
+        sh = [make_partitioned(60_000, 3_000, 5_000, rank=r, world=world, gen_chunks=8)
+              for r in range(world)]
+        A = sps.hstack([q['A'] for q in sh]).tocsr()
+        A.sort_indices()
+        assert (A != full['A']).nnz == 0
+        assert np.array_equal(np.concatenate([q['x_true'] for q in sh]), full['x_true'])
+        assert np.array_equal(np.concatenate([q['block_sizes'] for q in sh]),
+                              full['block_sizes'])
+        assert [q['col0'] for q in sh] == list(np.cumsum([0] + [q['n'] for q in sh])[:-1])
+        b = sum(q['Ax'] for q in sh)
+        assert np.max(np.abs(b - full['Ax'])) <= 1e-12 * np.max(np.abs(full['Ax']))
+        # scaled incidence: every stored entry of column j is colv[j]
+        for q in sh:
+            C = q['A'].tocsc()
+            assert np.array_equal(C.data, np.repeat(q['colv'], np.diff(C.indptr)))

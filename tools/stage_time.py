@@ -18,6 +18,9 @@ def main():
     ap.add_argument('--iters', type=int, default=200)
     ap.add_argument('--shape', type=str, default='C3',
                     help="C3, C5, or 'n,p,m' (e.g. a C5 shard: 1250000,62500,1000000)")
+    ap.add_argument('--world', type=int, default=1, help='C5: time rank --rank of this many shards')
+    ap.add_argument('--rank', type=int, default=0)
+    ap.add_argument('--fmt', type=str, default=None, help='panels / tiles (default: auto)')
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -29,13 +32,25 @@ def main():
         n, p, m = (int(v) for v in args.shape.split(','))
         c = dict(n=n, p=p, m=m, per_col=16)
     t0 = time.perf_counter()
-    sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+    if args.shape == 'C5':
+        from synthetic import make_partitioned
+        sh = make_partitioned(c['n'], c['p'], c['m'], c['per_col'], rank=args.rank,
+                              world=args.world)
+        c = dict(c, n=sh['n'], p=sh['p'])
+    else:
+        sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
     print('shape n %d p %d m %d nnz %d: generated in %.1f s' % (c['n'], c['p'], c['m'],
                                                                  sh['A'].nnz, time.perf_counter() - t0),
           flush=True)
     b = add_noise(sh['Ax'], 0.02)
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 10 ** 12, 'opt_tol': 1e-30},
-                   early_exit=False, AT=sh['AT'])
+                   early_exit=False, AT=sh['AT'], colv=sh.get('colv'), fmt=args.fmt)
+    print('formats: K1 %s, K2 %s' % (eng.fmt_A, eng.fmt_AT), flush=True)
+    for nm, t in (('K1', eng.A_til), ('K2', eng.AT_til)):
+        if t is not None:
+            i = t.img
+            print('  %s tiles: H %d groups %d order %d row blocks %d, %.0f MB stream'
+                  % (nm, i['H'], i['ngroups'], i['order'], i['nrb'], t.bytes() / 1e6), flush=True)
     print('engine built in %.1f s' % (time.perf_counter() - t0), flush=True)
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
     eng.prologue()
