@@ -29,7 +29,17 @@ def _problem():
     return sh, b
 
 
-def _run(rank, world, backend, port, out_q):
+def _partitioned(rank, world):
+    """A small world-independent problem (synthetic.make_partitioned, config
+    C5's generator): rank's shard, full b."""
+    from synthetic import make_partitioned, add_noise
+    kw = dict(per_col=8, seed=33, gen_chunks=8)
+    full = make_partitioned(40_000, 2_000, 3_000, **kw)
+    sh = make_partitioned(40_000, 2_000, 3_000, rank=rank, world=world, **kw)
+    return sh, add_noise(full['Ax'], 0.02, seed=33), full
+
+
+def _run(rank, world, backend, port, out_q, fmt=None, parts=1):
     for p in (ROOT, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -39,28 +49,35 @@ def _run(rank, world, backend, port, out_q):
     import torch.distributed as dist
     torch.cuda.set_device(0)
     from device import BBEngine
-    from distributed import ShardedBB, partition_blocks, torch_all_reduce
+    from distributed import (ShardedBB, partition_blocks, torch_all_reduce,
+                             torch_all_reduce_async)
     if backend == 'nccl':
         dist.init_process_group('nccl', rank=rank, world_size=world,
                                 device_id=torch.device('cuda', 0))
     else:
         dist.init_process_group(backend, rank=rank, world_size=world)
-    sh, b = _problem()
-    sizes = sh['block_sizes']
-    bounds = partition_blocks(sizes, sizes.astype(np.float64), world)
-    xst = np.concatenate(([0], np.cumsum(sizes)))
-    c0, c1 = xst[bounds[rank]], xst[bounds[rank + 1]]
-    A_g = sh['A'][:, c0:c1].tocsr()
-    sz_g = sizes[bounds[rank]:bounds[rank + 1]]
-    x0 = np.zeros(c1 - c0)
+    if fmt:
+        sh, b, _ = _partitioned(rank, world)
+        A_g, sz_g = sh['A'], sh['block_sizes']
+        x0 = np.zeros(sh['n'])
+    else:
+        sh, b = _problem()
+        sizes = sh['block_sizes']
+        bounds = partition_blocks(sizes, sizes.astype(np.float64), world)
+        xst = np.concatenate(([0], np.cumsum(sizes)))
+        c0, c1 = xst[bounds[rank]], xst[bounds[rank + 1]]
+        A_g = sh['A'][:, c0:c1].tocsr()
+        sz_g = sizes[bounds[rank]:bounds[rank + 1]]
+        x0 = np.zeros(c1 - c0)
     x0[np.cumsum(sz_g) - 1] = 1.0
     part = torch.from_numpy(A_g.dot(x0)).cuda()
     dist.all_reduce(part)
     target = part - torch.from_numpy(b).cuda()
     eng = BBEngine(A_g, None, sz_g, options={'max_iter': 10 ** 9, 'opt_tol': 1e-30},
-                   early_exit=False, target=target)
+                   early_exit=False, target=target, fmt=fmt)
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
-    drv = ShardedBB(eng, torch_all_reduce())
+    drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
+                    all_reduce_async=torch_all_reduce_async())
     drv.prologue()
     traj = {}
     for i in range(1, ITERS + 1):
@@ -72,12 +89,13 @@ def _run(rank, world, backend, port, out_q):
     dist.destroy_process_group()
 
 
-def _spawn(world, backend):
+def _spawn(world, backend, fmt=None, parts=1):
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29700 + (os.getpid() % 500) + world
-    procs = [ctx.Process(target=_run, args=(r, world, backend, port, q)) for r in range(world)]
+    port = 29700 + (os.getpid() % 500) + world + 3 * parts
+    procs = [ctx.Process(target=_run, args=(r, world, backend, port, q, fmt, parts))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
@@ -87,8 +105,12 @@ def _spawn(world, backend):
     return {i: np.concatenate([res[r][i] for r in range(world)]) for i in CHECK}
 
 
-def _check(got, orc):
-    sh, b = _problem()
+def _check(got, orc, partitioned=False):
+    if partitioned:
+        full, b = _partitioned(0, 1)[2], _partitioned(0, 1)[1]
+        sh = dict(A=full['A'], block_sizes=full['block_sizes'])
+    else:
+        sh, b = _problem()
     ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], ITERS, record_every=1)
     for i in CHECK:
         d = np.max(np.abs(got[i] - ref[i])) / max(1.0, np.max(np.abs(ref[i])))
@@ -105,3 +127,18 @@ def test_sharded_bb_two_ranks_on_device(cuda, orc):
 @pytest.mark.timeout(400)
 def test_sharded_bb_rccl_one_rank(cuda, orc):
     _check(_spawn(1, 'nccl'), orc)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_sharded_bb_tiles_overlapped_two_ranks(cuda, orc):
+    """C5's path at small size: world-independent shards (make_partitioned), the
+    streamed-tile kernels, the residual all-reduced in 3 row parts behind K1
+    (bsls_bb_residual_rows + async all-reduce)."""
+    _check(_spawn(2, 'gloo', fmt='tiles', parts=3), orc, partitioned=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_sharded_bb_tiles_overlapped_rccl(cuda, orc):
+    _check(_spawn(1, 'nccl', fmt='tiles', parts=3), orc, partitioned=True)
