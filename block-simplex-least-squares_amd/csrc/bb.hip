@@ -222,7 +222,7 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_tiles &T = P.At;
     int64_t rb, g;
-    tile_map(T, blockIdx.x, rb, g);
+    tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, g);
     rb += rb_base;
     const int HR = (int)tile_lds_doubles(T, false);
     for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_tiles &T = P.ATt;
     int64_t rb, g;
-    tile_map(T, blockIdx.x, rb, g);
+    tile_map(T, blockIdx.x, T.nrb, rb, g);
     const int HR = (int)tile_lds_doubles(T, false);
     double *rows = lds;
     double *rc = lds + HR;
@@ -845,7 +845,6 @@ extern "C" int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int
     if (rc != BSLS_OK) return rc;
     const bsls_bb_problem &P = *p;
     if (rb0 < 0 || rb1 <= rb0 || rb1 > k1_row_blocks(P)) return BSLS_E_ARG;
-    if (P.At.ent && P.At.order != 0 && (rb0 != 0 || rb1 != P.At.nrb)) return BSLS_E_ARG;
     const BBWork w = bb_layout(P);
     hipStream_t st = (hipStream_t)stream;
     if (iter > 0) launch_k1<false, false, true>(P, iter, w, st, rb0, rb1);

@@ -41,11 +41,13 @@ __host__ __device__ inline size_t tile_lds_doubles(const bsls_tiles &T, bool col
     return (size_t)(tile_nslots(T) + 1) * TILE_T * (colv ? 2 : 1);
 }
 
-__device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t &rb, int64_t &g) {
+// workgroup b of a launch over `nrb` row blocks -> (row block, group)
+__device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t nrb, int64_t &rb,
+                                         int64_t &g) {
     if (T.order == 1) {
         const int64_t x = b & 7, i = b >> 3;
-        rb = i % T.nrb;
-        g = x + 8 * (i / T.nrb);
+        rb = i % nrb;
+        g = x + 8 * (i / nrb);
     } else {
         g = b % T.ngroups;
         rb = b / T.ngroups;

@@ -194,7 +194,8 @@ typedef struct bsls_panels {
  * incidence.  order: workgroup b -> (rb, g): 0: g = b % ngroups, rb = b /
  * ngroups (with ngroups | 8 every XCD reads one column slice: it stays in the
  * XCD's L2); 1 (ngroups % 8 == 0): XCD x = b % 8 walks its groups x, x + 8, ...
- * one after the other over all row blocks (b / 8 = j * nrb + rb, g = x + 8 j). */
+ * one after the other over the launch's row blocks (b / 8 = j * nrb' + rb, g =
+ * x + 8 j, nrb' = the row blocks of the launch). */
 #define BSLS_TILE_THREADS 1024
 #define BSLS_TILE_MAXSLOTS 20       /* LDS: (nslots + 1) * 1024 doubles (x2 with colv) */
 typedef struct bsls_tiles {
@@ -285,8 +286,7 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 /* Stage 1 restricted to K1's row blocks [rb0, rb1) (rows rb0 * R .. rb1 * R - 1,
  * R = *rows_per_block from bsls_bb_row_blocks, which returns the block count):
- * a multi-GPU driver all-reduces r part by part while the next part computes.
- * Tile images with order 1 only take the whole range. */
+ * a multi-GPU driver all-reduces r part by part while the next part computes. */
 int64_t bsls_bb_row_blocks(const bsls_bb_problem *p, int64_t *rows_per_block);
 int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
                           void *stream);
