@@ -389,16 +389,110 @@ def gen_batch_traces():
     np.savez_compressed(os.path.join(OUT, 'batch.npz'), **out)
 
 
+def gen_plugin_traces():
+    """GradientDescent dispatch (python/gradient_descent.py:47-69) over the
+    z-space closures of main.solve_in_z (python/main.py:47-65): every exit of
+    solvers.stopping reachable from BB.solve (python/solvers.py:40-63, BB.py:22)
+    with its iteration and message, and the LBFGS method (python/LBFGS.py)."""
+    import contextlib
+    import io
+    import logging
+    import numpy.linalg as la
+    import BB
+    import LBFGS
+    from bsls_utils import x2z, particular_x0, block_sizes_to_N
+    from c_extensions.c_extensions import isotonic_regression_multi_c
+    from gradient_descent import GradientDescent
+
+    def closures(A, b, sizes):
+        x0 = particular_x0(sizes)
+        N = block_sizes_to_N(sizes)
+        z0 = x2z(x0, sizes)
+        target = A.dot(x0) - b
+        AT = A.T.tocsr(); NT = N.T.tocsr()
+        f = lambda z: 0.5 * la.norm(A.dot(N.dot(z)) + target) ** 2
+        nabla_f = lambda z: NT.dot(AT.dot(A.dot(N.dot(z)) + target))
+        cum = np.concatenate(([0], np.cumsum(sizes - 1)))
+
+        def proj(x):
+            isotonic_regression_multi_c(x, cum[:-1])
+            return np.maximum(np.minimum(x, 1.), 0.)
+        return z0, f, nabla_f, proj
+
+    class Grab(logging.Handler):
+        def __init__(self):
+            logging.Handler.__init__(self, logging.WARNING)
+            self.msgs = []
+
+        def emit(self, rec):
+            self.msgs.append(rec.getMessage())
+
+    def run(tag, A, b, sizes, method, options):
+        z0, f, nabla_f, proj = closures(A, b, sizes)
+        grab = Grab()
+        logging.getLogger().addHandler(grab)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            gd = GradientDescent(z0=z0, f=f, nabla_f=nabla_f, proj=proj, method=method,
+                                 options=options)
+            iters, times, states = gd.run()
+        logging.getLogger().removeHandler(grab)
+        msgs = grab.msgs + [ln for ln in buf.getvalue().splitlines() if 'Exiting' in ln]
+        out['%s_iters' % tag] = np.array(iters)
+        out['%s_states' % tag] = np.array(states)
+        out['%s_exit' % tag] = np.array(msgs[-1] if msgs else 'max_iter')
+        out['%s_A_data' % tag], out['%s_A_indices' % tag] = A.data, A.indices
+        out['%s_A_indptr' % tag], out['%s_A_shape' % tag] = A.indptr, np.array(A.shape)
+        out['%s_b' % tag], out['%s_block_sizes' % tag] = b, np.asarray(sizes)
+
+    out = {}
+    A, b, xs, sizes = sparse_problem(SEED + 5, 1200, 40, 150, per_col=8, noise=0.0)
+    # ||g||^2 <= opt_tol (1 + |f|) with a realistic tolerance
+    run('grad8', A, b, sizes, 'BB', {'max_iter': 20000, 'verbose': 0, 'opt_tol': 1e-8})
+    # no opt_tol in options: stopping's TOLER = 1e-6 default
+    run('noopt', A, b, sizes, 'BB', {'max_iter': 20000, 'verbose': 0})
+    # max_iter
+    run('maxit', A, b, sizes, 'BB', {'max_iter': 777, 'verbose': 0, 'opt_tol': 1e-30})
+    # BB.py:22 builtin sum(delta_g) == 0: a target pushing every block to a vertex,
+    # where the projection returns the same z and the gradient repeats exactly
+    A2, _, _, sizes2 = sparse_problem(SEED + 21, 600, 40, 100, per_col=8, noise=0.0)
+    bneg = -A2.dot(np.ones(A2.shape[1])) * 1000.0
+    run('vertex', A2, bneg, sizes2, 'BB', {'max_iter': 2000, 'verbose': 0, 'opt_tol': 1e-30})
+    # LBFGS through GradientDescent (starts at z0 + 1, gradient_descent.py:49)
+    A3, b3, _, sizes3 = sparse_problem(SEED + 23, 600, 30, 80, per_col=8, noise=0.01)
+    # (5 iterations: LBFGS on this problem amplifies a 1e-15 gradient perturbation
+    #  to 4e-8 by iteration 6 and 1e-3 by 25 -- measured with the CPU restatement)
+    run('lbfgs', A3, b3, sizes3, 'LBFGS', {'max_iter': 5, 'verbose': 0, 'opt_tol': 1e-30})
+    # and its per-iteration trajectory (record_every=1)
+    z0, f, nabla_f, proj = closures(A3, b3, sizes3)
+    rec = {}
+
+    def log(i, state, dt):
+        rec[i] = np.array(state)
+        return 0.0
+    with contextlib.redirect_stdout(io.StringIO()):
+        LBFGS.solve(z0 + 1, f, nabla_f, __import__('solvers').stopping, record_every=1,
+                    proj=proj, log=log, options={'max_iter': 25, 'verbose': 0, 'opt_tol': 1e-30})
+    keep = sorted(rec)
+    out['lbfgs_trace_iters'] = np.array(keep)
+    out['lbfgs_trace_states'] = np.array([rec[i] for i in keep])
+    np.savez_compressed(os.path.join(OUT, 'plugins.npz'), **out)
+
+
 def main():
     prepare()
     if len(sys.argv) > 1 and sys.argv[1] == 'batch':
         gen_batch_traces()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == 'plugins':
+        gen_plugin_traces()
         return
     gen_projection_cases()
     gen_isotonic_cases()
     gen_xz_quad()
     gen_solver_traces()
     gen_batch_traces()
+    gen_plugin_traces()
     for f in sorted(os.listdir(OUT)):
         if f.endswith('.npz'):
             print(f, os.path.getsize(os.path.join(OUT, f)))

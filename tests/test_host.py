@@ -282,3 +282,25 @@ def test_md_pack_blocks():
     assert ln.sum() == sizes.sum() and np.all(np.diff(x0) == ln[:-1])
     nblk = sum(bin(int(v)).count('1') for v in mask.view(np.uint64))
     assert nblk == sizes.size
+
+
+def test_lbfgs_host_loop_matches_reference(orc, golden):
+    """LBFGS.py (the host loop over whatever closures it is given) over the
+    CPU restatement's closures reproduces the reference's LBFGS.solve
+    trajectory bit for bit (tests/golden/plugins.npz, 25 iterations)."""
+    import LBFGS
+    import solvers
+    G = golden('plugins.npz')
+    A = sps.csr_matrix((G['lbfgs_A_data'], G['lbfgs_A_indices'], G['lbfgs_A_indptr']),
+                       shape=tuple(G['lbfgs_A_shape']))
+    P = orc.solve_in_z_parts(A, G['lbfgs_b'], G['lbfgs_block_sizes'])
+    rec = {}
+
+    def log(i, s, dt):
+        rec[i] = np.array(s)
+        return 0.0
+    LBFGS.solve(P['z0'] + 1, P['f'], P['nabla_f'], solvers.stopping, record_every=1,
+                proj=P['proj'], log=log, options={'max_iter': 25, 'verbose': 0, 'opt_tol': 1e-30})
+    assert sorted(rec) == list(G['lbfgs_trace_iters'])
+    for k, i in enumerate(G['lbfgs_trace_iters']):
+        assert np.array_equal(rec[i], G['lbfgs_trace_states'][k]), i

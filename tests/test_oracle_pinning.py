@@ -234,6 +234,30 @@ def test_golden_main_problems_converge(orc, golden):
         assert 0.5 * np.linalg.norm(A.dot(x) - b) ** 2 < 1e-16
 
 
+@pytest.mark.parametrize('tag', ['grad8', 'noopt', 'maxit', 'vertex'])
+def test_golden_stopping_exits(orc, golden, tag):
+    """Oracle BB loop + stopping == the reference's GradientDescent('BB') runs
+    ending at each exit of solvers.stopping / BB.py:22: same logged
+    iterations (so the same exit iteration), same states bit for bit."""
+    G = golden('plugins.npz')
+    A = _csr(G, tag)
+    opts = {'grad8': {'max_iter': 20000, 'verbose': 0, 'opt_tol': 1e-8},
+            'noopt': {'max_iter': 20000, 'verbose': 0},
+            'maxit': {'max_iter': 777, 'verbose': 0, 'opt_tol': 1e-30},
+            'vertex': {'max_iter': 2000, 'verbose': 0, 'opt_tol': 1e-30}}[tag]
+    P = orc.solve_in_z_parts(A, G['%s_b' % tag], G['%s_block_sizes' % tag])
+    rec = {}
+
+    def log(i, s, dt):
+        rec[i] = np.array(s)
+        return 0.0
+    orc.bb_solve(P['z0'], P['f'], P['nabla_f'], orc.stopping, proj=P['proj'], log=log,
+                 options=opts)
+    assert sorted(rec) == list(G['%s_iters' % tag])
+    for k, it in enumerate(G['%s_iters' % tag]):
+        assert exact(rec[it], G['%s_states' % tag][k]), it
+
+
 # --------------------------------------------------------------- vs compiled reference
 
 def _ref_or_skip(orc):
