@@ -136,7 +136,7 @@ class SparseLSQ:
     PANEL_MIN_NNZ = 1 << 20
 
     def __init__(self, A, b, A_T=None, panels=None):
-        from device import DeviceCSR, DeviceLSQ
+        from device import DeviceCSR, lsq_operator
         torch = _torch()
         A = sps.csr_matrix(A)
         self.A_host = A
@@ -146,7 +146,7 @@ class SparseLSQ:
         self.AT = DeviceCSR(AT)
         if panels is None:
             panels = A.nnz >= self.PANEL_MIN_NNZ
-        self.lsq = DeviceLSQ(A, AT) if panels else None
+        self.lsq = lsq_operator(A, AT) if panels else None
         self.b = _dev(np.asarray(b, dtype=np.float64).ravel())
         self.neg_b = -self.b
         self.tmp = torch.empty(self.m, dtype=torch.float64, device='cuda')

@@ -7,7 +7,17 @@
 // block in LDS, and the range is written back coalesced.  A wave whose range
 // exceeds ISO_CAP elements runs the same code on global memory instead (run
 // lengths then live in the caller's weight array or in the workspace).
+//
+// The path main.py takes (variant 1, weight=None, update=1 -- fresh unit run
+// lengths, c_extensions.pyx:84-85) runs wave-parallel instead (iso_pack_kernel,
+// the compacted PAVA of pava_wave.hpp that K3 runs, bit-identical): a planning
+// pass maps every 32-element window to the blocks starting in it; wave q takes
+// windows 2q and 2q + 1 as one pack when their blocks span at most 64
+// elements, else each window's blocks as a pack of at most 63 elements (every
+// block but a window's last is shorter than 32, the last is taken on its own
+// when it is longer), so no host plan is needed.
 #include "pava.hpp"
+#include "pava_wave.hpp"
 
 namespace bsls {
 
@@ -63,12 +73,104 @@ __global__ __launch_bounds__(WAVE) void iso_kernel(double *__restrict__ y,
     if (!ok && status) atomicOr(status, 1);
 }
 
+constexpr int ISO_WIN = 32;   // pack window (elements)
+
+inline int64_t iso_nwin(int64_t n) { return (n + ISO_WIN - 1) / ISO_WIN; }
+
+// win_first[w] = first block starting at or after element 32 w (w = 0 .. nwin)
+__global__ __launch_bounds__(256) void iso_plan_kernel(const int64_t *__restrict__ starts,
+                                                       int64_t nb, int64_t nwin,
+                                                       int32_t *__restrict__ win_first) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nb) return;
+    const int64_t lo = (b == 0) ? 0 : (starts[b - 1] / ISO_WIN) + 1;
+    const int64_t hi = (b == nb) ? nwin : starts[b] / ISO_WIN;
+    for (int64_t w = lo; w <= hi; ++w) win_first[w] = (int32_t)b;
+}
+
+// one wave-parallel PAVA v1 (unit weights, expand) over y[s0, s0 + L), L <= 64,
+// blocks starting at the set bits of B
+__device__ __forceinline__ void iso_wave_pack(double *__restrict__ y, int64_t s0, int L,
+                                              uint64_t B, double *ys, int *ps, int *cst) {
+    const int l = lane_id();
+    double v = (l < L) ? y[s0 + l] : 0.0;
+    pava_v1_wave_c(v, L, B, ys, ps, cst);
+    if (l < L) y[s0 + l] = v;
+}
+
+// window blocks [f, e): one pack of <= 63 elements, the last block on its own
+// when it is longer than the window
+__device__ __forceinline__ void iso_window(double *__restrict__ y,
+                                           const int64_t *__restrict__ starts, int64_t nb,
+                                           int64_t n, int64_t f, int64_t e,
+                                           int32_t *__restrict__ wscratch, double *ys, int *ps,
+                                           int *cst) {
+    const int l = lane_id();
+    if (f >= e) return;
+    const int64_t s0 = starts[f], sl = starts[e - 1];
+    const int64_t el = block_end(starts, nb, e - 1, n);
+    const bool big = el - sl > ISO_WIN;          // only the window's last block can be
+    const int64_t nsm = (e - f) - (big ? 1 : 0);
+    if (nsm > 0) {
+        const int L = (int)((big ? sl : el) - s0);  // <= 63
+        ps[l] = 0;
+        if (l < nsm) ps[(int)(starts[f + l] - s0)] = 1;
+        const uint64_t B = __ballot(l < L && ps[l] != 0);
+        iso_wave_pack(y, s0, L, B, ys, ps, cst);
+    }
+    if (big) {
+        const int64_t len = el - sl;
+        if (len <= WAVE) {
+            iso_wave_pack(y, sl, (int)len, 1ull, ys, ps, cst);
+        } else if (l == 0) {
+            for (int64_t j = sl; j < el; ++j) wscratch[j] = 1;
+            pava_v1(y, wscratch, sl, el, 1);
+        }
+    }
+}
+
+// wave q: windows 2q and 2q + 1 -- as one pack when their blocks span <= 64
+// elements (the common case), else window by window
+__global__ __launch_bounds__(256) void iso_pack_kernel(double *__restrict__ y,
+                                                       const int64_t *__restrict__ starts,
+                                                       int64_t nb, int64_t n, int64_t nwin,
+                                                       const int32_t *__restrict__ win_first,
+                                                       int32_t *__restrict__ wscratch) {
+    const int l = lane_id();
+    const int wv = threadIdx.x / WAVE;
+    const int64_t q = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);
+    __shared__ double pv_y[4][64];
+    __shared__ int pv_p[4][64];
+    __shared__ int pv_c[4][65];
+    const int64_t p0 = 2 * q;
+    if (p0 >= nwin) return;
+    const int64_t f = win_first[p0];
+    const int64_t m = win_first[p0 + 1];
+    const int64_t e = win_first[p0 + 2 <= nwin ? p0 + 2 : nwin];
+    if (f >= e) return;
+    const int64_t s0 = starts[f];
+    const int64_t span = block_end(starts, nb, e - 1, n) - s0;
+    int *ps = pv_p[wv];
+    if (span <= WAVE) {
+        const int64_t nbk = e - f;               // <= 64 blocks (each >= 1 element)
+        ps[l] = 0;
+        if (l < nbk) ps[(int)(starts[f + l] - s0)] = 1;
+        const uint64_t B = __ballot(l < span && ps[l] != 0);
+        iso_wave_pack(y, s0, (int)span, B, pv_y[wv], ps, pv_c[wv]);
+    } else {
+        iso_window(y, starts, nb, n, f, m, wscratch, pv_y[wv], ps, pv_c[wv]);
+        iso_window(y, starts, nb, n, m, e, wscratch, pv_y[wv], ps, pv_c[wv]);
+    }
+}
+
 }  // namespace bsls
 
 using namespace bsls;
 
 extern "C" size_t bsls_isotonic_workspace_size(int64_t n) {
-    return (size_t)((n * 4 + 15) & ~(int64_t)15);
+    // unit run lengths (n int32) + the pack plan (nwin + 1 int32)
+    const int64_t b = n * 4 + (iso_nwin(n) + 1) * 4;
+    return (size_t)((b + 15) & ~(int64_t)15);
 }
 
 extern "C" int bsls_isotonic_multi(int variant, double *d_y, const int64_t *d_starts,
@@ -83,6 +185,16 @@ extern "C" int bsls_isotonic_multi(int variant, double *d_y, const int64_t *d_st
     hipStream_t st = (hipStream_t)stream;
     const int grid = grid_for(nblocks, WAVE);
     int32_t *ws = (int32_t *)d_work;
+    if (variant == 1 && !d_weight && expand) {
+        const int64_t nwin = iso_nwin(n);
+        int32_t *wf = ws + n;
+        iso_plan_kernel<<<grid_for(nblocks + 1, 256), 256, 0, st>>>(d_starts, nblocks, nwin, wf);
+        BSLS_LAUNCH_CHECK();
+        iso_pack_kernel<<<grid_for((nwin + 1) / 2, 4), 256, 0, st>>>(d_y, d_starts, nblocks, n, nwin, wf,
+                                                           ws);
+        BSLS_LAUNCH_CHECK();
+        return BSLS_OK;
+    }
     if (variant == 1)
         iso_kernel<1><<<grid, WAVE, 0, st>>>(d_y, d_starts, nblocks, n, d_weight, expand, ws, d_status);
     else if (variant == 2)

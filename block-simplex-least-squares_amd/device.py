@@ -99,6 +99,12 @@ def chunk_plan(ncols, ngroups, chunk=None):
     return np.array(cols, dtype=np.int64), np.array(gch, dtype=np.int64)
 
 
+class PanelOverflow(ValueError):
+    """A 64-row slice holds more entries in one chunk than the panel format's
+    16-bit running counts address (dense rows): the caller falls back to
+    another format (BBEngine: streamed tiles; DeviceLSQ users: the CSR kernels)."""
+
+
 def build_panels(M, prow, halo=False, chunk_col=None, group_chunk=None, values=True):
     """Panel image of the CSR matrix M (include/bsls_hip.h struct bsls_panels,
     csrc/panels.hpp).  Host arrays in a dict; `values=False` drops the entry
@@ -148,7 +154,7 @@ def build_panels(M, prow, halo=False, chunk_col=None, group_chunk=None, values=T
     padc = cnt_all + (cnt_all & 1)
     incl = np.cumsum(padc, axis=2)                # per slice, inclusive over lanes
     if incl[:, :, 63].max(initial=0) > 0xFFFE:
-        raise ValueError('a 64-row slice has more than 65534 entries in one chunk')
+        raise PanelOverflow('a 64-row slice has more than 65534 entries in one chunk')
     cnt = (incl | (cnt_all & 1))[live].astype(np.uint16).reshape(-1)
     cnt_off = np.concatenate(([0], np.cumsum(64 * live.sum(axis=1)))).astype(np.int64)
     ne = padc.sum(axis=(1, 2))
@@ -464,6 +470,15 @@ class DeviceLSQ:
         return out
 
 
+def lsq_operator(A, AT=None, general=False):
+    """DeviceLSQ on the panel images, or None (the caller keeps the general CSR
+    kernels) when the panel format cannot hold the matrix (dense rows)."""
+    try:
+        return DeviceLSQ(A, AT, general=general)
+    except PanelOverflow:
+        return None
+
+
 class BlockLayout:
     """Block structure of x (sizes k_b) and of z (sizes k_b - 1), on device."""
 
@@ -557,13 +572,19 @@ class BBEngine:
         self.A_pan = self.AT_pan = self.A_til = self.AT_til = None
         if self.fmt_A == 'panels':
             prow, groups = k1_plan(self.m)
-            self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
-        else:
+            try:
+                self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
+            except PanelOverflow:
+                self.fmt_A = 'tiles'      # dense rows: the tiles have no such limit
+        if self.fmt_A == 'tiles':
             self.A_til = DeviceTiles(A, 0, values=not self.scaled, plan=tile_plans[0])
         if self.fmt_AT == 'panels':
-            self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), True, 1,
-                                       values=not self.scaled)
-        else:
+            try:
+                self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), True, 1,
+                                           values=not self.scaled)
+            except PanelOverflow:
+                self.fmt_AT = 'tiles'
+        if self.fmt_AT == 'tiles':
             self.AT_til = DeviceTiles(AT, 1, values=not self.scaled, colv_lds=self.scaled,
                                       plan=tile_plans[1])
         opts = options or {}

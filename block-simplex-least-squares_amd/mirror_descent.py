@@ -50,7 +50,7 @@ class MirrorDescent:
 
     def __init__(self, A, b, blocks, panels=None):
         import torch
-        from device import DeviceCSR, DeviceLSQ
+        from device import DeviceCSR, lsq_operator
         L = _native.lib()
         A = sps.csr_matrix(A)
         sizes = np.asarray(blocks, dtype=np.int64)
@@ -62,7 +62,7 @@ class MirrorDescent:
         self.Ad, self.ATd = DeviceCSR(A), DeviceCSR(AT)
         if panels is None:
             panels = A.nnz >= (1 << 20)
-        self.lsq = DeviceLSQ(A, AT) if panels else None
+        self.lsq = lsq_operator(A, AT) if panels else None
         self.starts = torch.from_numpy(
             np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)).cuda()
         bd = torch.from_numpy(np.asarray(b, dtype=np.float64).ravel()).cuda()

@@ -198,3 +198,30 @@ def test_k3_wave_pava_bit_exact(cuda, orc):
         assert np.array_equal(got.view(np.int64), ref.view(np.int64)), trial
         xr = orc.block_sizes_to_N(sizes).dot(ref)
         assert np.array_equal(eng.x.cpu().numpy(), xr), trial
+
+
+def test_dense_row_network_falls_back_to_tiles(cuda, orc):
+    """A 100k-route network with 8 links every route crosses: the panel image
+    overflows, the engine takes the streamed tiles for A, and the iterates
+    still follow the oracle; the x-space operator falls back to the CSR kernels."""
+    from device import BBEngine
+    from algorithm_utils import SparseLSQ
+    from test_host import _dense_row_matrix
+    A = _dense_row_matrix()
+    rs = np.random.RandomState(4)
+    sizes = rs.multinomial(A.shape[1] - 5000, np.ones(5000) / 5000) + 1
+    x = np.concatenate([rs.dirichlet(np.ones(k)) for k in sizes])
+    b = A.dot(x) * (1 + 0.02 * rs.randn(A.shape[0]))
+    eng = BBEngine(A, b, sizes, options={'max_iter': 10, 'opt_tol': 1e-30})
+    assert eng.fmt_A == 'tiles'
+    rec = {}
+
+    def log(i, s, dt):
+        rec[i] = s
+        return 0.0
+    eng.solve(log=log, record_every=1, poll=1)
+    ref = orc.bb_trace(A, b, sizes, 10, record_every=1)
+    for i in (1, 5, 10):
+        assert rel_err(rec[i], ref[i]) < 1e-6, i
+    op = SparseLSQ(A, b, panels=True)
+    assert op.lsq is None

@@ -138,6 +138,41 @@ def test_isotonic_golden(cx, golden):
     assert exact(y, G['kat_single'])
 
 
+def test_isotonic_wave_path_golden(cx, golden):
+    """weight=None, update=1 (main.py's call) takes the wave-parallel pack path:
+    same bits as the reference with fresh unit weights."""
+    G = golden('isotonic.npz')
+    for ci in range(int(G['ncases'])):
+        yy = G['c%d_y' % ci].copy()
+        cx.isotonic_regression_multi_c(yy, G['c%d_blocks' % ci])
+        assert exact(yy, G['c%d_v1_u1' % ci]), ci
+
+
+@pytest.mark.parametrize('kind', ['randn', 'ties', 'decreasing'])
+def test_isotonic_wave_path_size_classes(cx, orc, kind):
+    """Pack-window edge cases: blocks of 1..130 elements incl. 31/32/33 (the
+    window), 63/64/65 (a wave), blocks[0] > 0, and long runs of 1-element
+    blocks."""
+    rs = np.random.RandomState(17)
+    sizes = np.concatenate([rs.randint(1, 40, 3000), [31, 32, 33, 63, 64, 65, 130, 1, 1, 1],
+                            np.ones(200, dtype=np.int64), rs.randint(30, 70, 300)])
+    rs.shuffle(sizes)
+    first = 7
+    starts = (first + np.concatenate(([0], np.cumsum(sizes)[:-1]))).astype(np.int64)
+    n = int(first + sizes.sum())
+    if kind == 'randn':
+        y = rs.randn(n)
+    elif kind == 'ties':
+        y = np.round(rs.randn(n), 0)
+        y[rs.rand(n) < 0.1] = -0.0
+    else:
+        y = -np.arange(n, dtype=np.float64) + 0.25 * rs.randn(n)
+    ref = y.copy(); orc.isotonic_regression_multi_c(ref, starts)
+    got = y.copy(); cx.isotonic_regression_multi_c(got, starts)
+    assert exact(got, ref)
+    assert exact(got[:first], y[:first])
+
+
 def test_isotonic_c3_full_size(cx, orc):
     """z-space PAVA at config C3 (950k entries, 50k blocks) vs the oracle."""
     import torch

@@ -304,3 +304,28 @@ def test_lbfgs_host_loop_matches_reference(orc, golden):
     assert sorted(rec) == list(G['lbfgs_trace_iters'])
     for k, i in enumerate(G['lbfgs_trace_iters']):
         assert np.array_equal(rec[i], G['lbfgs_trace_states'][k]), i
+
+
+def _dense_row_matrix(n=100_000, m=1000, dense=8, seed=3):
+    """A network with a few links every route crosses (dense rows 0..dense-1)
+    plus 16 random links per route: a 64-row slice then holds more entries per
+    chunk than the panel format addresses."""
+    rs = np.random.RandomState(seed)
+    rows = np.concatenate([np.repeat(np.arange(dense), n),
+                           rs.randint(dense, m, size=16 * n)])
+    cols = np.concatenate([np.tile(np.arange(n), dense), np.repeat(np.arange(n), 16)])
+    A = sps.csr_matrix((np.ones(rows.size), (rows, cols)), shape=(m, n))
+    A.sum_duplicates()
+    return A
+
+
+def test_panel_overflow_is_typed():
+    """build_panels refuses a dense-row slice with PanelOverflow (a ValueError),
+    which BBEngine / lsq_operator catch to fall back."""
+    import device
+    A = _dense_row_matrix()
+    prow, groups = device.k1_plan(A.shape[0])
+    with pytest.raises(device.PanelOverflow):
+        device.build_panels(A, prow, False, *device.chunk_plan(A.shape[1], groups),
+                            values=False)
+    assert issubclass(device.PanelOverflow, ValueError)
