@@ -58,7 +58,8 @@ class Tiles(ctypes.Structure):
     """Mirror of struct bsls_tiles (include/bsls_hip.h)."""
     _fields_ = [('rows', _i64), ('cols', _i64), ('H', _i64), ('halo', _i64), ('nrb', _i64),
                 ('ngroups', _i64), ('order', _i64), ('nquads', _i64), ('group_col', _vp),
-                ('wave_off', _vp), ('ent', _vp), ('val', _vp)]
+                ('wave_off', _vp), ('ent', _vp), ('val', _vp), ('layout', _i64),
+                ('base', _vp)]
 
 
 class BBProblem(ctypes.Structure):
@@ -145,6 +146,8 @@ _SIGS = {
     'bsls_md_workspace_size': (_sz, [_i64]),
     'bsls_tiles_build': (_i64, [_i64, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp,
                                 _i64]),
+    'bsls_tiles_build_dealt': (_i64, [_i64, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
+                                      _vp, _vp, _i64]),
     'bsls_version': (ctypes.c_char_p, []),
     'bsls_device_arch': (_int, [ctypes.c_char_p, _int]),
 }
@@ -274,3 +277,33 @@ def tiles_build(M, H, halo, group_col, values=True):
     if rc != nq:
         raise RuntimeError('bsls_tiles_build failed (%d)' % rc)
     return dict(wave_off=wo, ent=ent, val=val, nquads=int(nq), nrb=nrb)
+
+
+def tiles_build_dealt(M, H, halo, group_col, values=True):
+    """Host arrays of the layout-1 (dealt) tile image of CSR matrix M
+    (bsls_tiles_build_dealt, host only): dict(wave_off, ent, base, val or None,
+    nquads, nrb)."""
+    import numpy as np
+    ip = np.ascontiguousarray(M.indptr, dtype=np.int64)
+    ix = np.ascontiguousarray(M.indices, dtype=np.int32)
+    dv = np.ascontiguousarray(M.data, dtype=np.float64) if values else None
+    gc = np.ascontiguousarray(group_col, dtype=np.int64)
+    R, C = M.shape
+    G = gc.shape[0] - 1
+    L = load()
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data) if a is not None else ctypes.c_void_p(0)
+    nq = L.bsls_tiles_build_dealt(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc),
+                                  None, None, None, None, 0)
+    if nq < 0:
+        raise ValueError('dealt tile image: invalid layout (H %d, halo %d, %d groups)'
+                         % (H, halo, G))
+    nrb = -(-R // int(H))
+    wo = np.zeros(nrb * G + 1, dtype=np.int64)
+    ent = np.zeros(4 * nq + 256, dtype=np.uint32)
+    base = np.zeros(4 * nq // 64 + 64, dtype=np.int32)
+    val = np.zeros(4 * nq + 256, dtype=np.float64) if values else None
+    rc = L.bsls_tiles_build_dealt(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc),
+                                  vp(wo), vp(ent), vp(base), vp(val), nq)
+    if rc != nq:
+        raise RuntimeError('bsls_tiles_build_dealt failed (%d)' % rc)
+    return dict(wave_off=wo, ent=ent, base=base, val=val, nquads=int(nq), nrb=nrb)

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
     const int HR = (int)tile_lds_doubles(T, false);
     for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;
     __syncthreads();
-    tile_walk<MODE>(T, rb, g, P.x, lds, nullptr);
+    tile_walk_any<MODE>(T, rb, g, P.x, lds, nullptr);
     __syncthreads();
     const int64_t G = T.ngroups;
     const int64_t r0 = rb * T.H, r1 = (r0 + T.H < P.m) ? r0 + T.H : P.m;
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
         if (MODE == 2) rc[i] = (i < nloc) ? P.colv[i0 + i] : 0.0;
     }
     __syncthreads();
-    tile_walk<(MODE == 3 ? 0 : MODE)>(T, rb, g, P.r, rows, rc);
+    tile_walk_any<(MODE == 3 ? 0 : MODE)>(T, rb, g, P.r, rows, rc);
     __syncthreads();
     const int64_t G = T.ngroups;
     bool fin = true;
@@ -750,6 +750,7 @@ static bool tiles_ok(const bsls_tiles &T, int64_t rows, int64_t cols, int64_t ha
     if (T.order != 0 && !(T.order == 1 && T.ngroups % 8 == 0)) return false;
     if (tile_lds_doubles(T, colv_lds) * 8 > (size_t)PANEL_LDS_MAX) return false;
     if (!T.group_col || !T.wave_off || !T.ent) return false;
+    if (T.layout != 0 && !(T.layout == 1 && T.base && T.H + T.halo < 65536)) return false;
     return need_val ? T.val != nullptr : true;
 }
 

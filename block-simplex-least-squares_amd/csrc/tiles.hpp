@@ -38,6 +38,7 @@ __host__ __device__ inline int64_t tile_nslots(const bsls_tiles &T) {
 // dynamic LDS doubles of a tile kernel: the row sums (+ the dummy slot), and
 // with `colv` the rows' column scales (K2 on a scaled incidence)
 __host__ __device__ inline size_t tile_lds_doubles(const bsls_tiles &T, bool colv) {
+    if (T.layout == 1) return (size_t)(T.H + T.halo + 1) * (colv ? 2 : 1);
     return (size_t)(tile_nslots(T) + 1) * TILE_T * (colv ? 2 : 1);
 }
 
@@ -110,6 +111,79 @@ __device__ __forceinline__ void tile_walk(const bsls_tiles &T, int64_t rb, int64
             }
         }
     }
+}
+
+// Layout 1 (dealt, include/bsls_hip.h): wave w walks its instructions of tile
+// (rb, g) quad-step by quad-step -- one 16-B entry load (4 slots) and one
+// scalar 16-B base load per step, loaded P steps ahead, the gathers of step
+// s + 1 issued before the LDS atomic adds of step s.  MODE as tile_walk.
+template <int MODE, int P = 4>
+__device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
+                                                const double *__restrict__ src, double *rows,
+                                                const double *rcol) {
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t t = rb * T.ngroups + g;
+    const int64_t q0 = T.wave_off[t], nq = T.wave_off[t + 1] - q0;
+    const tile_quad *Q = reinterpret_cast<const tile_quad *>(T.ent) + (q0 * 16 + wv) * 64 + lane;
+    const int4 *Bq = reinterpret_cast<const int4 *>(T.base) + q0 * 16 + wv;
+    const double *V = (MODE == 1) ? T.val + 4 * ((q0 * 16 + wv) * 64 + lane) : nullptr;
+    const double *xb = src + T.group_col[g];
+    tile_quad ring[P];
+    int4 bring[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        ring[k] = (k < nq) ? Q[(int64_t)k * 1024] : tile_quad{0, 0, 0, 0};
+        bring[k] = (k < nq) ? Bq[(int64_t)k * 16] : int4{0, 0, 0, 0};
+    }
+    double v[4], vn[4], a[4], an[4];
+    auto gat = [&](const tile_quad &u, const int4 &b, int64_t q, double (&o)[4], double (&w)[4]) {
+        o[0] = xb[b.x + (u[0] & 0xFFFFu)];
+        o[1] = xb[b.y + (u[1] & 0xFFFFu)];
+        o[2] = xb[b.z + (u[2] & 0xFFFFu)];
+        o[3] = xb[b.w + (u[3] & 0xFFFFu)];
+        if (MODE == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = V[q * 4096 + j];
+        }
+    };
+    gat(ring[0], bring[0], 0, v, a);
+    for (int64_t q = 0; q < nq; q += P) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const tile_quad cur = ring[k];
+            if (q + k + 1 < nq) gat(ring[(k + 1) % P], bring[(k + 1) % P], q + k + 1, vn, an);
+            if (q + k + P < nq) {
+                ring[k] = Q[(q + k + P) * 1024];
+                bring[k] = Bq[(q + k + P) * 16];
+            }
+            if (q + k < nq) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int lr = (int)(cur[j] >> 16);
+                    double term;
+                    if (MODE == 0) term = v[j];
+                    else if (MODE == 1) term = a[j] * v[j];
+                    else term = rcol[lr] * v[j];
+                    atomicAdd(&rows[lr], term);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = vn[j];
+                if (MODE == 1) a[j] = an[j];
+            }
+        }
+    }
+}
+
+// the walk of either layout
+template <int MODE>
+__device__ __forceinline__ void tile_walk_any(const bsls_tiles &T, int64_t rb, int64_t g,
+                                              const double *__restrict__ src, double *rows,
+                                              const double *rcol) {
+    if (T.layout == 1) tile_walk_dealt<MODE>(T, rb, g, src, rows, rcol);
+    else tile_walk<MODE>(T, rb, g, src, rows, rcol);
 }
 
 }  // namespace bsls

@@ -167,3 +167,143 @@ extern "C" int64_t bsls_tiles_build(int64_t rows, int64_t cols, const int64_t *i
     });
     return nquads;
 }
+
+// ---------------------------------------------------------------------------
+// Layout 1 ("dealt", include/bsls_hip.h): per tile (rb, g) the entries sorted
+// by (column, local row), packed greedily into 64-lane instructions whose
+// columns stay within base + 65535, padded to whole quad-steps (64
+// instructions: 4 slots x 16 waves).
+
+namespace {
+
+struct DealtEnt {
+    uint64_t key;   // column offset in the group << 16 | local row
+    double v;
+};
+
+// the tile's sorted entries (values only when data != NULL)
+void dealt_collect(const Plan &p, const double *data, int64_t rb, std::vector<std::vector<DealtEnt>> &out) {
+    out.assign((size_t)p.G, {});
+    const int64_t r0 = rb * p.H;
+    for (int64_t i = r0; i < block_end(p, rb); ++i) {
+        const uint64_t lr = (uint64_t)(i - r0);
+        for (int64_t k = p.indptr[i]; k < p.indptr[i + 1]; ++k) {
+            const int32_t c = p.indices[k];
+            const int64_t g = p.gmap[c];
+            out[(size_t)g].push_back({((uint64_t)(c - p.gc[g]) << 16) | lr, data ? data[k] : 0.0});
+        }
+    }
+    for (auto &v : out)
+        std::sort(v.begin(), v.end(),
+                  [](const DealtEnt &a, const DealtEnt &b) { return a.key < b.key; });
+}
+
+// instruction starts of a sorted tile (greedy: <= 64 entries, column span <= 65535)
+void dealt_insts(const std::vector<DealtEnt> &e, std::vector<int64_t> &st) {
+    st.clear();
+    size_t i = 0;
+    while (i < e.size()) {
+        st.push_back((int64_t)i);
+        const uint64_t base = e[i].key >> 16;
+        size_t j = i + 1;
+        while (j < e.size() && j - i < 64 && (e[j].key >> 16) - base <= 65535) ++j;
+        i = j;
+    }
+    st.push_back((int64_t)e.size());
+}
+
+}  // namespace
+
+extern "C" int64_t bsls_tiles_build_dealt(int64_t rows, int64_t cols, const int64_t *indptr,
+                                          const int32_t *indices, const double *data, int64_t H,
+                                          int64_t halo, int64_t ngroups, const int64_t *group_col,
+                                          int64_t *wave_off_out, uint32_t *ent_out,
+                                          int32_t *base_out, double *val_out,
+                                          int64_t nquads_cap) {
+    if (rows < 1 || cols < 1 || !indptr || !indices || H < 64 || (halo != 0 && halo != 1) ||
+        ngroups < 1 || !group_col || H + halo + 1 > 65536)
+        return BSLS_E_ARG;
+    Plan p;
+    p.rows = rows;
+    p.cols = cols;
+    p.H = H;
+    p.halo = halo;
+    p.nrb = (rows + H - 1) / H;
+    p.G = ngroups;
+    p.nslots = 0;
+    p.indptr = indptr;
+    p.indices = indices;
+    p.gc = group_col;
+    if (group_col[0] != 0 || group_col[ngroups] != cols) return BSLS_E_ARG;
+    for (int64_t g = 0; g < ngroups; ++g) {
+        const int64_t w = group_col[g + 1] - group_col[g];
+        if (w < 1 || w > INT32_MAX) return BSLS_E_ARG;   // int32 bases
+    }
+    if (indptr[0] != 0) return BSLS_E_ARG;
+    p.gmap.resize(cols);
+    for (int64_t g = 0; g < ngroups; ++g)
+        for (int64_t j = group_col[g]; j < group_col[g + 1]; ++j) p.gmap[j] = (int32_t)g;
+    for (int64_t i = 0; i < rows; ++i)
+        if (indptr[i + 1] < indptr[i]) return BSLS_E_ARG;
+    for (int64_t k = 0; k < indptr[rows]; ++k)
+        if (indices[k] < 0 || indices[k] >= cols) return BSLS_E_ARG;
+    // pass 1: quad-steps per tile
+    const int64_t ntiles = p.nrb * ngroups;
+    std::vector<int64_t> qs(ntiles, 0);
+    parallel_blocks(p.nrb, [&](int64_t rb) {
+        std::vector<std::vector<DealtEnt>> e;
+        std::vector<int64_t> st;
+        dealt_collect(p, nullptr, rb, e);
+        for (int64_t g = 0; g < ngroups; ++g) {
+            dealt_insts(e[(size_t)g], st);
+            const int64_t ni = (int64_t)st.size() - 1;
+            qs[rb * ngroups + g] = (ni + 63) / 64;
+        }
+    });
+    int64_t total = 0;
+    for (int64_t t = 0; t < ntiles; ++t) total += qs[t];
+    const int64_t nquads = total * 1024;
+    if (!wave_off_out) return nquads;
+    if (!ent_out || !base_out || nquads_cap < nquads || (data && !val_out)) return BSLS_E_ARG;
+    wave_off_out[0] = 0;
+    for (int64_t t = 0; t < ntiles; ++t) wave_off_out[t + 1] = wave_off_out[t] + qs[t];
+    const uint32_t dummy = (uint32_t)(H + halo) << 16;
+    // pass 2: fill
+    parallel_blocks(p.nrb, [&](int64_t rb) {
+        std::vector<std::vector<DealtEnt>> e;
+        std::vector<int64_t> st;
+        dealt_collect(p, data, rb, e);
+        for (int64_t g = 0; g < ngroups; ++g) {
+            const auto &E = e[(size_t)g];
+            dealt_insts(E, st);
+            const int64_t t = rb * ngroups + g, q0 = wave_off_out[t];
+            const int64_t nslot = (wave_off_out[t + 1] - q0) * 64;   // instructions incl. padding
+            const int64_t ni = (int64_t)st.size() - 1;
+            for (int64_t k = 0; k < nslot; ++k) {
+                const int64_t w = k % 16, j = (k / 16) % 4, q = q0 + k / 64;
+                const int64_t qi = (q * 16 + w) * 64;           // uint4 index of lane 0
+                uint32_t base = 0;
+                int64_t a = 0, b = 0;
+                if (k < ni) {
+                    a = st[(size_t)k];
+                    b = st[(size_t)k + 1];
+                    base = (uint32_t)(E[(size_t)a].key >> 16);
+                }
+                base_out[(q * 16 + w) * 4 + j] = (int32_t)base;
+                for (int64_t l = 0; l < 64; ++l) {
+                    const int64_t u = 4 * (qi + l) + j;
+                    if (a + l < b) {
+                        const DealtEnt &d = E[(size_t)(a + l)];
+                        ent_out[u] = (uint32_t)(d.key & 0xFFFF) << 16 |
+                                     (uint32_t)((d.key >> 16) - base);
+                        if (data) val_out[u] = d.v;
+                    } else {
+                        ent_out[u] = dummy;
+                        if (data) val_out[u] = 0.0;
+                    }
+                }
+            }
+        }
+    });
+    return nquads;
+}

@@ -273,7 +273,7 @@ class DevicePanels:
         return sum(v.numel() * v.element_size() for v in self.t.values())
 
 
-def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=None):
+def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=None, layout=0):
     """(H, ngroups, order) of a tile image (include/bsls_hip.h struct bsls_tiles,
     csrc/tiles.hpp): column groups (a power of two) until one group's slice of
     the gathered vector fits an XCD's L2 (order 1, XCD-sequential, past 8
@@ -285,6 +285,25 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
     if plan:
         H, G = (int(v) for v in plan.split(','))
         return H, G, (1 if G > 8 else 0)
+    if layout == 1:
+        # dealt image: one workgroup per CU at most, as few column groups as
+        # fill the CUs (each extra group costs m partial sums written and read
+        # back); every workgroup sweeps its group's columns in order, so the
+        # workgroups of an XCD share the sweep front in L2 whatever the slice
+        # width.  Measured on C5 (tools/stage_time.py): K1 G = 4 x 64 row blocks
+        # 374 us (G = 8: 400, 16: 526, 32: 812; G = 2 / 1 leave CUs idle: 698 /
+        # 1303); K2 (the routes' rows: partial sums of n rows are dear) one
+        # group of 1024 row blocks 503 us (2: 611, 4: 775).
+        mult = 2 if colv_lds else 1
+        hmax = _native.TILE_LDS_BYTES // (8 * mult) - 1 - halo
+        nmin = -(-rows // hmax)
+        G = 1
+        while not halo and 2 * G * nmin <= cus and 2 * G <= cols:
+            G *= 2
+        nrb = max(nmin, cus // G)
+        nrb = -(-(nrb * G) // cus) * cus // G if nrb * G > cus else nrb
+        H = max(64, -(-rows // nrb))
+        return int(H), int(G), (1 if G > 8 and G % 8 == 0 else 0)
     if l2_slice is None:
         # measured on the C5 shard (tools/stage_time.py): K1 fastest with
         # 2.5-MB slices of x (4 groups: 112 us, 8: 148 us), K2 with the whole
@@ -297,8 +316,11 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
     G = max(1, min(G, cols))
     order = 1 if G > 8 else 0
     mult = 2 if (colv_lds and G == 1) else 1
-    per = _native.TILE_LDS_BYTES // (8 * _native.TILE_THREADS * mult) - 1
-    hmax = per * _native.TILE_THREADS - halo
+    if layout == 1:
+        hmax = _native.TILE_LDS_BYTES // (8 * mult) - 1 - halo      # rows + the dummy row
+    else:
+        per = _native.TILE_LDS_BYTES // (8 * _native.TILE_THREADS * mult) - 1
+        hmax = per * _native.TILE_THREADS - halo
     nrb = max(-(-rows // hmax), -(-cus // G))
     nrb = -(-(nrb * G) // cus) * cus // G if nrb * G > cus else nrb
     H = max(64, -(-rows // nrb))
@@ -330,6 +352,8 @@ def tiles_matvec(img, x, colv=None, group_sums=False):
     T = _native.TILE_THREADS
     gc = img['group_col']
     x = np.asarray(x, dtype=np.float64)
+    if img.get('layout', 0) == 1:
+        return _dealt_matvec(img, x, colv, group_sums)
     nslots = -(-(H + halo) // T)
     out = np.zeros(R)
     parts = []
@@ -364,21 +388,69 @@ def tiles_matvec(img, x, colv=None, group_sums=False):
     return (out, parts) if group_sums else out
 
 
+def _dealt_matvec(img, x, colv=None, group_sums=False):
+    """tiles_matvec for a layout-1 (dealt) image: every (quad-step, wave, slot,
+    lane) entry added to its row (the device adds them with LDS atomics in no
+    fixed order; the sums agree to rounding)."""
+    R, H, halo, G = img['rows'], img['H'], img['halo'], img['ngroups']
+    gc, wo = img['group_col'], img['wave_off']
+    ent = img['ent'].astype(np.int64)
+    parts = []
+    for g in range(G):
+        acc = np.zeros(R)
+        for rb in range(img['nrb']):
+            t = rb * G + g
+            q0, q1 = int(wo[t]), int(wo[t + 1])
+            if q1 == q0:
+                continue
+            rows = np.zeros(H + halo + 1)
+            lanes = np.arange(64)
+            for q in range(q0, q1):
+                for w in range(16):
+                    u = ((q * 16 + w) * 64 + lanes) * 4
+                    for j in range(4):
+                        e = ent[u + j]
+                        lr = e >> 16
+                        col = gc[g] + int(img['base'][(q * 16 + w) * 4 + j]) + (e & 0xFFFF)
+                        xv = x[np.minimum(col, x.size - 1)]
+                        if img['val'] is not None:
+                            term = img['val'][u + j] * xv
+                        elif colv is not None:
+                            rr = np.minimum(rb * H + lr, R - 1)
+                            term = np.where(lr < H + halo, colv[rr], 0.0) * xv
+                        else:
+                            term = xv
+                        np.add.at(rows, lr, term)
+            r0 = rb * H
+            r1 = min(r0 + H, R)
+            acc[r0:r1] = rows[:r1 - r0]
+        parts.append(acc)
+    out = parts[0].copy()
+    for a in parts[1:]:
+        out = out + a
+    return (out, parts) if group_sums else out
+
+
 class DeviceTiles:
     """A tile image on the device + the ctypes struct pointing at it."""
 
-    def __init__(self, M, halo=0, values=True, colv_lds=False, plan=None):
+    def __init__(self, M, halo=0, values=True, colv_lds=False, plan=None, layout=0):
         torch = _torch()
         M = sps.csr_matrix(M)
         M.sort_indices()
         R, C = M.shape
         H, G, order = plan or tile_plan(R, C, halo, colv_lds,
-                                        env='BSLS_TILE_PLAN_AT' if halo else 'BSLS_TILE_PLAN_A')
+                                        env='BSLS_TILE_PLAN_AT' if halo else 'BSLS_TILE_PLAN_A',
+                                        layout=layout)
         gc = np.round(np.linspace(0, C, G + 1)).astype(np.int64)
         if np.any(np.diff(gc) < 1):
             raise ValueError('more column groups than columns')
-        img = _native.tiles_build(M, H, halo, gc, values=values)
-        img.update(rows=R, cols=C, H=H, halo=halo, ngroups=G, order=order, group_col=gc)
+        if layout == 1:
+            img = _native.tiles_build_dealt(M, H, halo, gc, values=values)
+        else:
+            img = _native.tiles_build(M, H, halo, gc, values=values)
+        img.update(rows=R, cols=C, H=H, halo=halo, ngroups=G, order=order, group_col=gc,
+                   layout=layout)
         self.img = img
         self.nnz = int(M.nnz)
         self.t = {'group_col': torch.from_numpy(gc).cuda(),
@@ -386,7 +458,11 @@ class DeviceTiles:
                   'ent': torch.from_numpy(img['ent'].view(np.int32)).cuda()}
         if img['val'] is not None:
             self.t['val'] = torch.from_numpy(img['val']).cuda()
+        if layout == 1:
+            self.t['base'] = torch.from_numpy(img['base']).cuda()
         S = _native.Tiles()
+        S.layout = layout
+        S.base = self.t['base'].data_ptr() if layout == 1 else None
         S.rows, S.cols, S.H, S.halo = R, C, H, halo
         S.nrb, S.ngroups, S.order, S.nquads = img['nrb'], G, order, img['nquads']
         S.group_col = self.t['group_col'].data_ptr()
@@ -546,7 +622,7 @@ class BBEngine:
 
     def __init__(self, A, b, block_sizes, options=None, early_exit=True, A_dev=None,
                  AT_dev=None, AT=None, target=None, x0=None, general=False, fmt=None,
-                 tile_plans=(None, None), colv=None):
+                 tile_plans=(None, None), colv=None, deterministic=False, tile_layouts=None):
         torch = _torch()
         L = _native.lib()
         self.layout = lay = BlockLayout(block_sizes)
@@ -576,8 +652,19 @@ class BBEngine:
                 self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
             except PanelOverflow:
                 self.fmt_A = 'tiles'      # dense rows: the tiles have no such limit
+        # tile layouts (K1, K2): the dealt images (column-sorted gathers, LDS
+        # atomic sums: the same sums to rounding, not run-to-run bit-identical;
+        # C5 K1 1334 -> 374 us, K2 984 -> 503 us) unless `deterministic`, which
+        # keeps the thread streams (every row summed in CSR order: K2
+        # bit-identical to SciPy with one group).  BSLS_TILE_LAYOUT="a,at" overrides.
+        if tile_layouts is None:
+            env = os.environ.get('BSLS_TILE_LAYOUT')
+            tile_layouts = (tuple(int(v) for v in env.split(',')) if env
+                            else ((0, 0) if deterministic else (1, 1)))
+        self.tile_layouts = tile_layouts
         if self.fmt_A == 'tiles':
-            self.A_til = DeviceTiles(A, 0, values=not self.scaled, plan=tile_plans[0])
+            self.A_til = DeviceTiles(A, 0, values=not self.scaled, plan=tile_plans[0],
+                                     layout=tile_layouts[0])
         if self.fmt_AT == 'panels':
             try:
                 self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), True, 1,
@@ -586,7 +673,7 @@ class BBEngine:
                 self.fmt_AT = 'tiles'
         if self.fmt_AT == 'tiles':
             self.AT_til = DeviceTiles(AT, 1, values=not self.scaled, colv_lds=self.scaled,
-                                      plan=tile_plans[1])
+                                      plan=tile_plans[1], layout=tile_layouts[1])
         opts = options or {}
         self.options = dict(opts)
         dev = dict(dtype=torch.float64, device='cuda')

@@ -198,15 +198,31 @@ typedef struct bsls_panels {
  * x + 8 j, nrb' = the row blocks of the launch). */
 #define BSLS_TILE_THREADS 1024
 #define BSLS_TILE_MAXSLOTS 20       /* LDS: (nslots + 1) * 1024 doubles (x2 with colv) */
+/* layout 1 ("dealt"; bsls_tiles_build_dealt): the entries of tile (rb, g) are
+ * sorted by column and dealt to the workgroup in that order, so the 64 gathers
+ * of one wave-instruction fall in a narrow column range and share cache lines
+ * (column-sorted gathers ~2-3x the rate of the thread streams' scattered ones,
+ * tools/coal_ubench.hip); the running sums are then added with LDS atomics
+ * (ds_add_f64): same sums to rounding, not a fixed order.  Instruction k of a
+ * tile (k = (4 s + j) * 16 + w: quad-step s, slot j, wave w) holds up to 64
+ * entries whose columns lie in [base_k, base_k + 65535]; entry = local row << 16
+ * | (column - group_col[g] - base_k); unused lanes point at the dummy row
+ * H + halo.  Tile t = rb * ngroups + g owns quad-steps wave_off[t] ..
+ * wave_off[t+1] - 1 (wave_off: nrb * ngroups + 1 entries); quad-step q, wave
+ * w, lane l: uint4 ent[(q * 16 + w) * 64 + l] = its slots j = 0..3, bases
+ * base[(q * 16 + w) * 4 + j], values val[4 * ((q * 16 + w) * 64 + l) + j].
+ * LDS: H + halo + 1 doubles (x2 with colv).  nquads = quad-steps * 1024. */
 typedef struct bsls_tiles {
     int64_t rows, cols;
     int64_t H, halo;                /* rows per block; 1: + the next block's row 0 */
     int64_t nrb, ngroups, order;
     int64_t nquads;                 /* ent holds 4 * nquads entries */
     const int64_t *group_col;       /* ngroups + 1 */
-    const int64_t *wave_off;        /* nrb * ngroups * 16 + 1 (in quads) */
+    const int64_t *wave_off;        /* layout 0: nrb * ngroups * 16 + 1 (in quads); 1: see above */
     const uint32_t *ent;
     const double *val;              /* 4 * nquads, or NULL (scaled incidence) */
+    int64_t layout;                 /* 0: thread streams (CSR order per row), 1: dealt */
+    const int32_t *base;            /* layout 1: 4 * nquads / 64 instruction bases */
 } bsls_tiles;
 
 /* Host-side builder (no device memory): the tile image of the CSR matrix
@@ -219,6 +235,14 @@ int64_t bsls_tiles_build(int64_t rows, int64_t cols, const int64_t *indptr,
                          const int32_t *indices, const double *data, int64_t H, int64_t halo,
                          int64_t ngroups, const int64_t *group_col, int64_t *wave_off_out,
                          uint32_t *ent_out, double *val_out, int64_t nquads_cap);
+/* The same for layout 1: call with wave_off_out == NULL for the quad count
+ * (quad-steps * 1024), then to fill wave_off_out (nrb * ngroups + 1),
+ * ent_out (4 * count), base_out (4 * count / 64) and val_out. */
+int64_t bsls_tiles_build_dealt(int64_t rows, int64_t cols, const int64_t *indptr,
+                               const int32_t *indices, const double *data, int64_t H,
+                               int64_t halo, int64_t ngroups, const int64_t *group_col,
+                               int64_t *wave_off_out, uint32_t *ent_out, int32_t *base_out,
+                               double *val_out, int64_t nquads_cap);
 
 typedef struct bsls_bb_problem {
     int64_t m, n, nz, nblocks;      /* rows, x length, z length (n - nblocks), blocks */

@@ -2,7 +2,8 @@
 500k blocks / 1M links / 160M nnz, the world-independent problem
 (synthetic.make_partitioned) that bench.py shards over N GPUs.  Its sparse row
 blocks take the streamed-tile kernels (csrc/tiles.hpp):
-  * K2 (g = N'A'r, one column group) bit-identical to SciPy;
+  * K2 (g = N'A'r, one column group): on the deterministic engine (thread
+    streams) bit-identical to SciPy; on the default dealt image within 1e-12;
   * K1 (r = A x + target, column-group partials) within 1e-12;
   * K3 (PAVA v1 + clip + N z on the 9.5M-entry z layout) bit-identical to the
     oracle;
@@ -39,15 +40,35 @@ def test_c5_takes_the_tile_kernels(c5):
     assert eng.AT_til.img['ngroups'] == 1
 
 
-def test_c5_k2_bit_exact_vs_scipy(c5):
+def test_c5_k2_vs_scipy(c5):
+    """The default (dealt) K2: LDS atomic sums, equal to SciPy to rounding."""
     import torch
     sh, _, eng = c5
+    assert eng.AT_til.img['layout'] == 1
+    r = np.random.RandomState(5).randn(eng.m)
+    eng.r.copy_(torch.from_numpy(r))
+    eng.stage(3, 0)
+    got = eng.g[0][:eng.nz].cpu().numpy()
+    want = _nt(sh['block_sizes'], sh['AT'].dot(r))
+    assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
+
+
+def test_c5_k2_bit_exact_vs_scipy_deterministic(c5):
+    """deterministic=True: K2 on thread streams, every row in CSR order --
+    bit-identical to SciPy at full C5 size."""
+    import torch
+    from device import BBEngine
+    sh, b, _ = c5
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 3, 'opt_tol': 1e-30},
+                   AT=sh['AT'], colv=sh['colv'], deterministic=True)
+    assert eng.AT_til.img['layout'] == 0 and eng.AT_til.img['ngroups'] == 1
     r = np.random.RandomState(5).randn(eng.m)
     eng.r.copy_(torch.from_numpy(r))
     eng.stage(3, 0)
     got = eng.g[0][:eng.nz].cpu().numpy()
     want = _nt(sh['block_sizes'], sh['AT'].dot(r))
     assert np.array_equal(got, want)
+    del eng
 
 
 def test_c5_k1_residual_vs_scipy(c5):

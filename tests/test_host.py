@@ -329,3 +329,35 @@ def test_panel_overflow_is_typed():
         device.build_panels(A, prow, False, *device.chunk_plan(A.shape[1], groups),
                             values=False)
     assert issubclass(device.PanelOverflow, ValueError)
+
+
+@pytest.mark.parametrize('layout', [0, 1])
+@pytest.mark.parametrize('halo', [0, 1])
+@pytest.mark.parametrize('values', [True, False])
+def test_tile_images_restate_scipy(layout, halo, values):
+    """Both tile layouts (thread streams; dealt column-sorted instructions)
+    hold every entry once: the host restatement of the kernels' walk over the
+    image equals SciPy's A.dot to rounding (halo rows dropped), with several
+    column groups, a short last row block and empty rows."""
+    import _native
+    import device
+    rs = np.random.RandomState(9 + layout)
+    m, n = 5000, 3000
+    A = sps.random(m, n, density=0.004, random_state=rs, format='csr')
+    A = sps.csr_matrix(A.toarray() * (rs.rand(m, 1) > 0.05))   # some empty rows
+    A.data = rs.randn(A.nnz) if values else np.ones(A.nnz)
+    gc = np.round(np.linspace(0, n, 4)).astype(np.int64)
+    H = 1500
+    build = _native.tiles_build_dealt if layout else _native.tiles_build
+    img = build(A, H, halo, gc, values=values)
+    img.update(rows=m, cols=n, H=H, halo=halo, ngroups=3, order=0, group_col=gc, layout=layout)
+    x = rs.randn(n)
+    got = device.tiles_matvec(img, x)
+    want = A.dot(x)
+    assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
+    if layout == 1:
+        # every entry once: the non-dummy entries count nnz (+ halo copies)
+        e = img['ent'][:4 * img['nquads']].astype(np.int64)
+        live = int(np.sum((e >> 16) != H + halo))
+        extra = sum(int(A.indptr[r + 1] - A.indptr[r]) for r in range(H, m, H)) if halo else 0
+        assert live == A.nnz + extra
