@@ -27,7 +27,10 @@ import os
 import sys
 import time
 
-os.environ.setdefault('OPENBLAS_NUM_THREADS', '1')   # CPU baseline = 1 thread, like the reference
+# the 1-thread CPU baseline leg runs like the reference (single-threaded BLAS);
+# the box presets OPENBLAS_NUM_THREADS / OMP_NUM_THREADS to its CPU share
+HOST_THREADS = int(os.environ.get('OMP_NUM_THREADS') or os.cpu_count() or 1)
+os.environ['OPENBLAS_NUM_THREADS'] = '1'
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
 for _p in (ROOT, PKG):
@@ -102,6 +105,41 @@ def cpu_baseline_bb(A, b, sizes, budget_s=12.0):
         el = time.perf_counter() - t0
         if el >= budget_s or it >= 200:
             return it / el, it, el
+
+
+def cpu_baseline_bb_omp(A, b, sizes, threads, budget_s=10.0):
+    """The z-space BB loop in C + OpenMP (oracle/bsls_cpu_bb.c: the reference's
+    work per iteration, rows / blocks over `threads` threads): calibrated on 3
+    iterations, then a fixed count of about `budget_s` seconds."""
+    from oracle import oracle as orc
+    AT = sps_csr(A).T.tocsr()
+    t0 = time.perf_counter()
+    orc.cpu_bb_run(A, b, sizes, 3, threads=threads, AT=AT)
+    per = (time.perf_counter() - t0) / 3
+    iters = int(max(5, min(400, budget_s / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    orc.cpu_bb_run(A, b, sizes, iters, threads=threads, AT=AT)
+    el = time.perf_counter() - t0
+    return iters / el, iters, el
+
+
+def sps_csr(A):
+    import scipy.sparse as sps
+    return sps.csr_matrix(A)
+
+
+def bench_stored_values(sh, b, steps, warmup):
+    """The C3 BB loop on the general-CSR images (values stored, 8 B per entry:
+    what a matrix that is not a scaled incidence runs) -- BBEngine(general=True)."""
+    import torch
+    from device import BBEngine
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 10 ** 12, 'opt_tol': 1e-30},
+                   early_exit=False, AT=sh['AT'], general=True)
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    eng.prologue()
+    el = time_run(eng.iterate, steps, warmup, None)
+    return {'value': steps / el, 'unit': 'BB iterations/s (C3, values stored)',
+            'ms_per_step': el / steps * 1e3, 'formats': {'K1': eng.fmt_A, 'K2': eng.fmt_AT}}
 
 
 def bench_proj(reps=30, batch=16):
@@ -524,6 +562,8 @@ def main():
                                             'achieved_GB_s': ib3 * its3 / 1e9,
                                             'frac': ib3 * its3 / HBM_PEAK}}
         del eng3, run3
+        out['c3_stored_values'] = bench_stored_values(sh3, b3, max(args.steps, 50), args.warmup)
+        torch.cuda.empty_cache()
         out['proj_simplex'] = bench_proj()
         log('C2 projection done')
         out['isotonic'] = bench_iso()
@@ -532,11 +572,17 @@ def main():
         log('extras done')
         if not args.no_cpu_baseline:
             cps, cit, cel = cpu_baseline_bb(sh3['A'], b3, sh3['block_sizes'])
+            aps, ait, ael = cpu_baseline_bb_omp(sh3['A'], b3, sh3['block_sizes'], HOST_THREADS)
             out['cpu_baseline'] = {
                 'value': cps, 'unit': 'BB it/s (C3)', 'cores': 1, 'kind': 'port',
                 'sample': '%d BB iterations (%.1f s) of the C3 problem: oracle restatement of '
                           'BB.py over SciPy csr_matvec + C PAVA' % (cit, cel),
-                'host': host_info(1)}
+                'host': host_info(1),
+                'all_cores': {'value': aps, 'unit': 'BB it/s (C3)', 'cores': HOST_THREADS,
+                              'kind': 'port',
+                              'sample': '%d BB iterations (%.1f s) of the C3 problem: the BB '
+                                        'loop in C + OpenMP (oracle/bsls_cpu_bb.c)' % (ait, ael),
+                              'host': host_info(HOST_THREADS)}}
             log('CPU baseline done')
     if out is not None:
         print(json.dumps(out), flush=True)

@@ -132,6 +132,7 @@ _SIGS = {
     'bsls_csr_spmv': (_int, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _dbl, _vp, _vp, _int, _vp,
                              _sz, _vp]),
     'bsls_bb_workspace_size': (_sz, [_i64, _i64, _i64]),
+    'bsls_bb_dz_offset': (_sz, [_i64, _i64, _i64]),
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),

@@ -786,6 +786,10 @@ extern "C" size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz) {
     return bb_layout(nullptr, m, n, nz).bytes;
 }
 
+extern "C" size_t bsls_bb_dz_offset(int64_t m, int64_t n, int64_t nz) {
+    return (size_t)((char *)bb_layout(nullptr, m, n, nz).dz - (char *)nullptr);
+}
+
 extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream) {
     const int rc = check_problem(p);
     if (rc != BSLS_OK) return rc;

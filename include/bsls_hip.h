@@ -288,6 +288,9 @@ typedef struct bsls_bb_problem {
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
+/* Byte offset in `work` of dz = z - z_prev (nz doubles), the hand-off K3 writes
+ * for the next K2 (and the prologue for iteration 1); for tests and tools. */
+size_t bsls_bb_dz_offset(int64_t m, int64_t n, int64_t nz);
 /* BB.py:14-15 and the first f(z0): resets scal/tickets, g[0] = grad(z0 + 1),
  * r = r(z0), scal[FX] = f(z0).  z[0] must hold z0. */
 int bsls_bb_prologue(const bsls_bb_problem *p, void *stream);

@@ -41,6 +41,7 @@ import scipy.sparse.linalg as sla
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, 'libbsls_oracle.so')
+CPUBB_SO = os.path.join(HERE, 'libbsls_cpubb.so')
 REF_SO = os.path.join(HERE, '_ref', 'libbsls_ref.so')
 
 _D = ctypes.POINTER(ctypes.c_double)
@@ -82,6 +83,43 @@ def lib():
         L.orc_csr_matvec.argtypes = [_i64, _I32, _I32, _D, _D, _D]
         _lib = L
     return _lib
+
+
+_cpubb = None
+
+
+def cpu_bb_run(A, b, block_sizes, iters, threads=1, AT=None, z0=None):
+    """The z-space BB loop as a C + OpenMP port (bsls_cpu_bb.c: BB.py over
+    main.py's closures, the reference's work per iteration, early exits off):
+    `iters` iterations from z0 (default x2z(particular_x0) = 0) on `threads`
+    threads.  Returns (z, f).  bench.py's all-cores CPU baseline."""
+    global _cpubb
+    if _cpubb is None:
+        if not os.path.exists(CPUBB_SO):
+            build()
+        L = ctypes.CDLL(CPUBB_SO)
+        L.cpubb_run.argtypes = [_i64, _i64, _i64, _I64, _I64, _I32, _D, _I64, _I32, _D, _D, _D,
+                                _i64, ctypes.c_int]
+        L.cpubb_run.restype = ctypes.c_double
+        _cpubb = L
+    A = sps.csr_matrix(A)
+    AT = sps.csr_matrix(AT) if AT is not None else A.T.tocsr()
+    sizes = np.asarray(block_sizes, dtype=np.int64)
+    xs = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+    m, n = A.shape
+    x0 = particular_x0(sizes)
+    target = np.ascontiguousarray(A.dot(x0) - b, dtype=np.float64)
+    z = np.zeros(n - sizes.size) if z0 is None else np.array(z0, dtype=np.float64)
+    ip, ix, v = _p64c(A.indptr), np.ascontiguousarray(A.indices, np.int32), A.data
+    ipt, ixt, vt = _p64c(AT.indptr), np.ascontiguousarray(AT.indices, np.int32), AT.data
+    v, vt = np.ascontiguousarray(v, np.float64), np.ascontiguousarray(vt, np.float64)
+    fx = _cpubb.cpubb_run(m, n, sizes.size, _p64(xs), _p64(ip), _p32(ix), _pd(v), _p64(ipt),
+                          _p32(ixt), _pd(vt), _pd(target), _pd(z), int(iters), int(threads))
+    return z, fx
+
+
+def _p64c(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
 
 
 def ref_lib():

@@ -207,6 +207,11 @@ def test_k3_wave_pava_bit_exact(cuda, orc):
         assert np.array_equal(got.view(np.int64), ref.view(np.int64)), trial
         xr = orc.block_sizes_to_N(sizes).dot(ref)
         assert np.array_equal(eng.x.cpu().numpy(), xr), trial
+        # the dz = z - z_prev hand-off K3 writes for the next K2 (every block,
+        # the serial > 64 path too)
+        off = _native.load().bsls_bb_dz_offset(eng.m, eng.n, nz)
+        dz = eng.work[off:off + 8 * nz].view(torch.float64).cpu().numpy()
+        assert np.array_equal(dz.view(np.int64), (got - zc).view(np.int64)), trial
 
 
 def test_dense_row_network_falls_back_to_tiles(cuda, orc):
@@ -234,3 +239,27 @@ def test_dense_row_network_falls_back_to_tiles(cuda, orc):
         assert rel_err(rec[i], ref[i]) < 1e-6, i
     op = SparseLSQ(A, b, panels=True)
     assert op.lsq is None
+
+
+def test_bb_iterates_with_long_blocks_vs_oracle(cuda, orc):
+    """BB iterates over blocks of 66..300 routes (K3's serial path, and the dz it
+    hands to the next K2 on that path) next to short ones, vs the oracle."""
+    from device import BBEngine
+    from synthetic import make_shard, add_noise
+    rs = np.random.RandomState(12)
+    sizes = np.concatenate([rs.randint(66, 300, 40), rs.randint(2, 20, 400)])
+    rs.shuffle(sizes)
+    n = int(sizes.sum())
+    sh = make_shard(n + 1000, 100, 3_000, per_col=16, seed=12)
+    A = sh['A'][:, :n].tocsr()
+    b = add_noise(A.dot(rs.rand(n)), 0.02, seed=12)
+    eng = BBEngine(A, b, sizes, options={'max_iter': 15, 'opt_tol': 1e-30})
+    rec = {}
+
+    def log(i, s, dt):
+        rec[i] = s
+        return 0.0
+    eng.solve(log=log, record_every=1, poll=1)
+    ref = orc.bb_trace(A, b, sizes, 15, record_every=1)
+    for i in (1, 2, 5, 15):
+        assert rel_err(rec[i], ref[i]) < 1e-6, (i, rel_err(rec[i], ref[i]))

@@ -9,6 +9,8 @@ Every oracle function is checked bit-for-bit against
   * oracle/_ref/libbsls_ref.so (reference headers compiled here) on fresh
     random inputs, when that library is present.
 """
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sps
@@ -350,3 +352,20 @@ def test_golden_batch_solve_md(orc, golden, tag):
         sol = orc.batch_solve_md(obj, starts, step, x0.copy(), max_iter=k)
         assert exact(sol['x'], d['%s_md%d_x' % (tag, k)]), (tag, k)
         assert exact(sol['progress'], d['%s_md%d_prog' % (tag, k)])
+
+
+@pytest.mark.parametrize('threads', [1, 4])
+def test_cpu_bb_port_follows_restatement(orc, threads):
+    """bench.py's all-cores CPU baseline (oracle/bsls_cpu_bb.c, OpenMP) does the
+    same iterations as the 1-thread restatement of BB.py (to rounding: its
+    SpMV rows and dot products sum in another order)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)),
+                                    'block-simplex-least-squares_amd'))
+    from synthetic import make_shard, add_noise
+    sh = make_shard(20_000, 1_000, 2_000, per_col=16, seed=5)
+    b = add_noise(sh['Ax'], 0.02, seed=5)
+    ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], 12, record_every=1)
+    z, fx = orc.cpu_bb_run(sh['A'], b, sh['block_sizes'], 12, threads=threads)
+    assert np.max(np.abs(z - ref[12])) <= 1e-9 * max(1.0, np.max(np.abs(ref[12])))
+    assert np.isfinite(fx)
