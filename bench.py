@@ -249,6 +249,60 @@ def bench_xspace(sh, b, rounds=40, reps=5):
             'backtracks': bts, 'finite': ok}
 
 
+def bench_dore(sh, b, iters=30):
+    """DORE (python/DORE.py:6-90 through gradient_descent.py:55-67's setup) on
+    the C3 problem: linop / linop_T on the engine's K1 / K2 images (A and the
+    target scaled by 0.99 / lsv, lsv from ARPACK over the same operators, not
+    timed), proj = PAVA v1 + clip.  `iters` iterations after 3 untimed ones,
+    eps < 0 so the norm-change exit never fires; the host makes the
+    reference's branch decisions (one device->host read each).  Roofline:
+    the algorithmic bytes of the kernels the iterations actually launched
+    (K1 / K2 general-CSR bytes per linop / linop_T, 16 n_z + 4 (p+1) per
+    projection) over the wall time."""
+    import torch
+    import DORE
+    from device import BBEngine
+    from bsls_utils import lsv_operator
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], AT=sh['AT'])
+    lsv = lsv_operator(eng, None)
+    scale = 0.99 / lsv
+    calls = {'A': 0, 'AT': 0, 'proj': 0}
+
+    def linop(z):
+        calls['A'] += 1
+        return eng.apply_A(z, alpha=scale)
+
+    def linop_T(r):
+        calls['AT'] += 1
+        return eng.apply_AT(r, alpha=scale)
+
+    def proj(z):
+        calls['proj'] += 1
+        return eng.proj(z)
+    z0 = torch.zeros(eng.nz, dtype=torch.float64, device='cuda')
+    tgt = eng.target * scale
+    log = lambda i, s, d: 0.0
+    DORE.solve(z0, linop, linop_T, tgt, proj=proj, log=log, options={'max_iter': 3, 'opt_tol': -1.0})
+    torch.cuda.synchronize()
+    for k in calls:
+        calls[k] = 0
+    t0 = time.perf_counter()
+    x = DORE.solve(z0, linop, linop_T, tgt, proj=proj, log=log,
+                   options={'max_iter': iters, 'opt_tol': -1.0})
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    m, n, nz, p, nnz = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
+    kb = kernel_bytes(m, n, nz, p, nnz, nnz)
+    byt = (calls['A'] * kb['K1_spmv_A'] + calls['AT'] * kb['K2_spmvT_Nt_dots']
+           + calls['proj'] * (16 * nz + 4 * (p + 1)))
+    return {'operator': 'K1/K2 images (%s, %s)' % (eng.fmt_A, eng.fmt_AT), 'lsv': float(lsv),
+            'iterations': iters, 'us_per_iter': el * 1e6 / iters, 'iterations_per_s': iters / el,
+            'launches': dict(calls),
+            'roofline': {'bound': 'hbm', 'alg_bytes': byt, 'achieved': byt / el / 1e9,
+                         'peak': HBM_PEAK / 1e9, 'unit': 'GB/s', 'frac': byt / el / HBM_PEAK},
+            'finite': bool(torch.isfinite(x).all())}
+
+
 def bench_md(sh, b, iters=30):
     """Mirror descent (mirror_descent.least_squares, SURVEY.md §8 row a12;
     BASELINE config C4) on the same C3 problem: r = A x - b and A' r on the
@@ -569,6 +623,7 @@ def main():
         out['isotonic'] = bench_iso()
         out['xspace_bb'] = bench_xspace(sh3, b3)
         out['mirror_descent'] = bench_md(sh3, b3)
+        out['dore'] = bench_dore(sh3, b3)
         log('extras done')
         if not args.no_cpu_baseline:
             cps, cit, cel = cpu_baseline_bb(sh3['A'], b3, sh3['block_sizes'])

@@ -814,19 +814,58 @@ class BBEngine:
               'bsls_nt_apply')
         return out[:self.nz]
 
+    # The closures run on the fused kernels' images (K1 / K2 stages), not on
+    # general CSR copies: z goes through z[0] (stage 6: x = colv * N z), K1
+    # (stage 1: A x; stage 7: A x + target, ||r||^2, f) and K2 (stage 3 at
+    # iteration 0: N'A'r).  They share the engine's buffers with the fused BB
+    # loop, so they must not run while a solve() is in flight.
+    def _x_of(self, z):
+        torch = _torch()
+        z = torch.as_tensor(z, dtype=torch.float64, device='cuda').reshape(-1)
+        if z.numel() != self.nz:
+            raise ValueError('z has %d entries, expected %d' % (z.numel(), self.nz))
+        self.z[0][:self.nz].copy_(z)
+        self.stage(6, 0)
+
+    def apply_A(self, z, alpha=1.0):
+        """alpha A N z (DORE's linop with A scaled by alpha, gradient_descent.py:57-63)."""
+        self._x_of(z)
+        self.stage(1, 0)
+        return self.r * alpha if alpha != 1.0 else self.r.clone()
+
+    def apply_AT(self, r, alpha=1.0):
+        """alpha N' A' r (DORE's linop_T)."""
+        self.r.copy_(r)
+        self.stage(3, 0)
+        g = self.g[0][:self.nz]
+        return g * alpha if alpha != 1.0 else g.clone()
+
     def residual(self, z, alpha=1.0):
-        """alpha A N z + alpha target (DORE scales A and target by alpha)."""
-        r = self.A.matvec(self.n_apply(z), alpha=alpha)
-        return r.add_(self.target, alpha=alpha) if alpha != 1.0 else r.add_(self.target)
+        """alpha (A N z + target) (DORE scales A and target by alpha)."""
+        self._x_of(z)
+        self.stage(7, 0)
+        return self.r * alpha if alpha != 1.0 else self.r.clone()
 
     def f(self, z):
-        """0.5 ||A N z + target||^2 (main.py:53)."""
-        nr = float(self.residual(z).norm())
-        return 0.5 * nr ** 2
+        """0.5 ||A N z + target||^2 (main.py:53), f as K1's finish forms it."""
+        self._x_of(z)
+        self.stage(7, 0)
+        return float(self.scal[_native.S_FX].item())
 
     def nabla_f(self, z):
         """N' A' (A N z + target) (main.py:54)."""
-        return self.nt_apply(self.AT.matvec(self.residual(z)))
+        self._x_of(z)
+        self.stage(7, 0)
+        self.stage(3, 0)
+        return self.g[0][:self.nz].clone()
+
+    def apply_A_x(self, x):
+        """A x for an x-space vector (LS_postprocess's A x_true)."""
+        torch = _torch()
+        x = torch.as_tensor(x, dtype=torch.float64, device='cuda').reshape(-1)
+        self.x.copy_(self.colv * x if self.scaled else x)
+        self.stage(1, 0)
+        return self.r.clone()
 
     def proj(self, z):
         """isotonic_regression_multi_c on the z-blocks, then clip to [0, 1]
@@ -846,11 +885,10 @@ class BBEngine:
         return torch.clamp(y, 0.0, 1.0)
 
     def lsv_matvec(self, v):
-        """N'A'A N v for ARPACK (bsls_utils.lsv_operator), on the device."""
+        """N'A'A N v for ARPACK (bsls_utils.lsv_operator), on the fused images."""
         torch = _torch()
         vd = torch.from_numpy(np.ascontiguousarray(np.real(v), dtype=np.float64)).cuda()
-        w = self.AT.matvec(self.A.matvec(self.n_apply(vd)))
-        return self.nt_apply(w).cpu().numpy()
+        return self.apply_AT(self.apply_A(vd)).cpu().numpy()
 
     def scalars(self):
         return self.scal.cpu().numpy()

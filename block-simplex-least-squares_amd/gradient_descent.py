@@ -7,9 +7,9 @@ iteration 0, every `record_every` iterations and at the end.
 On MI355X the z-space problem is carried by a device.BBEngine (`engine=`):
   'BB'    -> the fused device loop (three kernels per iteration, no host sync
              between polls) -- the hot path;
-  'DORE'  -> DORE.solve over device closures (SpMV + N / N' kernels), with the
-             largest singular value of A N from ARPACK driving device matvecs;
-  'LBFGS' -> LBFGS.solve over the same device closures.
+  'DORE'  -> DORE.solve over the engine's linops (its K1 / K2 images), with
+             the largest singular value of A N from ARPACK over the same;
+  'LBFGS' -> LBFGS.solve over the engine's closures f / nabla_f / proj.
 Without an engine the plain closures f / nabla_f / proj are used (they must
 then already compute on the device).
 """
@@ -84,10 +84,10 @@ class GradientDescent:
             b_t = e.target * scale
 
             def linop(z):
-                return e.A.matvec(e.n_apply(z), alpha=scale)
+                return e.apply_A(z, alpha=scale)
 
             def linop_T(r):
-                return e.nt_apply(e.AT.matvec(r, alpha=scale)).clone()
+                return e.apply_AT(r, alpha=scale)
             DORE.solve(self._z0_device(), linop, linop_T, b_t, proj=e.proj, log=self.log,
                        options=self.options, record_every=100)
             self.lsv = lsv

@@ -76,8 +76,16 @@ def LS_postprocess(states, x0, A, b, x_true, scaling=None, block_sizes=None, out
         output = {}
     d = len(states)
     from device import DeviceCSR, BlockLayout
-    Ad = engine.A if engine is not None else DeviceCSR(A)
     bt = torch.from_numpy(np.asarray(b, dtype=np.float64)).cuda()
+    if engine is not None:
+        # A x on the engine's K1 image (no general CSR copy of A)
+        def a_minus_b(x):
+            return engine.apply_A_x(x) - bt
+    else:
+        Ad = DeviceCSR(A)
+
+        def a_minus_b(x):
+            return Ad.matvec(x, add=-bt)
     cols = []
     if not is_x and (N is None or N.size > 0):
         lay = engine.layout if engine is not None else BlockLayout(block_sizes)
@@ -100,11 +108,11 @@ def LS_postprocess(states, x0, A, b, x_true, scaling=None, block_sizes=None, out
     output['blocks'] = block_sizes.shape if block_sizes is not None else None
     x0d = torch.from_numpy(np.asarray(x0, dtype=np.float64)).cuda()
     xtd = torch.from_numpy(np.asarray(x_true, dtype=np.float64)).cuda()
-    r0 = Ad.matvec(x0d, add=-bt)
-    rs = Ad.matvec(xtd, add=-bt)
+    r0 = a_minus_b(x0d)
+    rs = a_minus_b(xtd)
     starting_error = 0.5 * float(r0.norm()) ** 2
     opt_error = 0.5 * float(rs.norm()) ** 2
-    err = np.array([0.5 * float(Ad.matvec(X[:, k].contiguous(), add=-bt).square().sum())
+    err = np.array([0.5 * float(a_minus_b(X[:, k].contiguous()).square().sum())
                     for k in range(d)])
     output['0.5norm(Ax-b)^2'], output['0.5norm(Ax_init-b)^2'] = err, starting_error
     output['0.5norm(Ax*-b)^2'] = opt_error
