@@ -489,13 +489,17 @@ def kernel_table(eng, it0, reps, world, m, n, nz, p, nnz):
     return kern
 
 
-def roofline_of(kern, traffic_file=None):
+def roofline_of(kern, traffic_file=None, config=None):
+    """The dominant kernel's roofline; traffic = its HBM bytes per launch from
+    the rocprofv3 PMC passes of the same build (tools/traffic.py, keyed by
+    workload), None when absent."""
     names = [k for k in kern if k != 'formats']
     dom = max(names, key=lambda k: kern[k]['avg_us'])
     traffic = None
     if traffic_file and os.path.exists(traffic_file):
         try:
-            traffic = json.load(open(traffic_file)).get(dom, {}).get('hbm_bytes_per_launch')
+            traffic = (json.load(open(traffic_file)).get(config, {}).get(dom, {})
+                       .get('hbm_bytes_per_launch'))
         except Exception:
             traffic = None
     return {'bound': 'hbm', 'kernel': dom, 'achieved': kern[dom]['GB_s'],
@@ -588,7 +592,7 @@ def main():
                        'routes_rank0': n_g, 'nnz_rank0': nnz_g,
                        'parallelism': 'column-shard x%d' % world,
                        'residual_allreduce_parts': args.parts if world > 1 else None},
-            'roofline': roofline_of(kern, tfile) if kern else None,
+            'roofline': roofline_of(kern, tfile, wl) if kern else None,
             'iteration_roofline': {'survey_bytes_per_iter': ib, 'achieved_GB_s': ib * it_s / 1e9,
                                    'frac': ib * it_s / HBM_PEAK,
                                    'note': 'whole job over all GPUs; peak is one GPU'},
@@ -611,7 +615,7 @@ def main():
                                             '100k links / 16M nnz, 1 GPU)',
                      'ms_per_step': el3 / max(args.steps, 50) * 1e3, 'kernels': kern3,
                      'roofline': roofline_of(kern3, os.path.join(ROOT, 'profiles',
-                                                                 'traffic_r02.json')),
+                                                                 'traffic_r02.json'), 'C3'),
                      'iteration_roofline': {'survey_bytes_per_iter': ib3,
                                             'achieved_GB_s': ib3 * its3 / 1e9,
                                             'frac': ib3 * its3 / HBM_PEAK}}

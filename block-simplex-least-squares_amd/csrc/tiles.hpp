@@ -57,6 +57,18 @@ __device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t
 
 typedef uint32_t tile_quad __attribute__((ext_vector_type(4)));
 
+// BSLS_TILE_NT=1: the dealt walk's entry stream by non-temporal loads (A/B)
+#ifndef BSLS_TILE_NT
+#define BSLS_TILE_NT 0
+#endif
+__device__ __forceinline__ tile_quad tq_load(const tile_quad *p) {
+#if BSLS_TILE_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 // Walk this thread's stream of tile (rb, g) into rows[] (LDS, zeroed by the
 // caller, barrier after):
 //   MODE 0  rows[lr] += src[c]                 (pattern / scaled incidence, K1)
@@ -133,7 +145,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
     int4 bring[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        ring[k] = (k < nq) ? Q[(int64_t)k * 1024] : tile_quad{0, 0, 0, 0};
+        ring[k] = (k < nq) ? tq_load(Q + (int64_t)k * 1024) : tile_quad{0, 0, 0, 0};
         bring[k] = (k < nq) ? Bq[(int64_t)k * 16] : int4{0, 0, 0, 0};
     }
     double v[4], vn[4], a[4], an[4];
@@ -154,7 +166,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
             const tile_quad cur = ring[k];
             if (q + k + 1 < nq) gat(ring[(k + 1) % P], bring[(k + 1) % P], q + k + 1, vn, an);
             if (q + k + P < nq) {
-                ring[k] = Q[(q + k + P) * 1024];
+                ring[k] = tq_load(Q + (q + k + P) * 1024);
                 bring[k] = Bq[(q + k + P) * 16];
             }
             if (q + k < nq) {

@@ -38,15 +38,19 @@ for s in $STEPS; do
       timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1
       rc=$?; echo "list rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
     pmc)
-      # one rocprofv3 pass per counter group (FETCH_SIZE and WRITE_SIZE cannot share a pass)
-      i=0
-      for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"; do
-        i=$((i+1))
-        timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc \
-            -- python3 tools/kprof.py --iters 10 --proj 10 > $OUT/pmc$i.log 2>&1
-        rc=$?; echo "pmc$i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
-      done
-      python3 tools/traffic.py $OUT/pmc1 $OUT/pmc2 > $OUT/traffic.json 2> $OUT/traffic.err ;;
+      # one rocprofv3 pass per counter group (FETCH_SIZE and WRITE_SIZE cannot share a pass),
+      # over tools/kprof.py on each workload; traffic -> profiles/traffic_r02.json
+      for cfg in C3 C5; do
+        i=0
+        for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"; do
+          i=$((i+1))
+          timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_${cfg}_$i -o pmc \
+              -- python3 tools/kprof.py --config $cfg --iters 10 --proj 10 > $OUT/pmc_${cfg}_$i.log 2>&1
+          rc=$?; echo "pmc $cfg $i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
+        done
+        python3 tools/traffic.py $cfg $OUT/traffic.json $OUT/pmc_${cfg}_1 $OUT/pmc_${cfg}_2 > /dev/null 2> $OUT/traffic_$cfg.err
+        python3 tools/pmc_summary.py $OUT/pmc_${cfg}_* > $OUT/pmc_summary_$cfg.txt 2>&1
+      done ;;
   esac
 done
 echo done | tee -a $OUT/status.txt

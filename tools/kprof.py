@@ -27,10 +27,14 @@ def main():
     import _native
     from _native import ptr, stream_handle, check
     c = CONFIGS[args.config]
-    sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+    if args.config == 'C5':
+        from synthetic import make_partitioned
+        sh = make_partitioned(c['n'], c['p'], c['m'], c['per_col'], rank=0, world=1)
+    else:
+        sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
     b = add_noise(sh['Ax'], 0.02)
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 10 ** 9, 'opt_tol': 1e-30},
-                   early_exit=False, AT=sh['AT'])
+                   early_exit=False, AT=sh['AT'], colv=sh.get('colv'))
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
     eng.prologue()
     eng.iterate(1, 5)

@@ -4,7 +4,8 @@
 over tools/kprof.py).  MI355X_MICROARCH.md "HBM / rocprofv3": FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
 coalesced reads, so traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes).
-Usage: python tools/traffic.py gpurun_out/pmc1 gpurun_out/pmc2 > profiles/traffic_r01.json"""
+Usage: python tools/traffic.py CONFIG OUT.json pmc_dir... -- adds CONFIG's kernels
+(C3: panels, C5: dealt tiles) to OUT.json (keyed by config, read by bench.py)."""
 import csv
 import glob
 import json
@@ -14,10 +15,13 @@ from collections import defaultdict
 
 # bench.py kernel names -> device kernels (demangled prefixes) in one launch of the stage
 KERNELS = {
-    'K2_spmvT_Nt_dots': ['bsls::bb_k2<2, true>'],
-    'K3_pava_clip_z2x': ['bsls::bb_k3('],
-    'K1_spmv_A': ['bsls::bb_k1<0, true, true, true>'],
-    'proj_simplex_C2': ['bsls::proj_lds_kernel<false>'],
+    'C3': {'K2_spmvT_Nt_dots': ['bsls::bb_k2<2, true>'],
+           'K3_pava_clip_z2x': ['bsls::bb_k3('],
+           'K1_spmv_A': ['bsls::bb_k1<0, true, true, true>'],
+           'proj_simplex_C2': ['bsls::proj_lds_kernel<false>']},
+    'C5': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<2, true>'],
+           'K3_pava_clip_z2x': ['bsls::bb_k3('],
+           'K1_spmv_A': ['bsls::bb_k1t<0, true, true, true>']},
 }
 
 
@@ -34,9 +38,10 @@ def load(dirs):
 
 
 def main():
-    vals = load(sys.argv[1:])
+    cfg, path = sys.argv[1], sys.argv[2]
+    vals = load(sys.argv[3:])
     out = {}
-    for name, parts in KERNELS.items():
+    for name, parts in KERNELS[cfg].items():
         fetch = write = 0.0
         ok = True
         for pfx in parts:
@@ -55,6 +60,9 @@ def main():
             out[name] = {'fetch_kib': fetch, 'write_kib': write,
                          'hbm_bytes_per_launch': (2 * fetch + write) * 1024,
                          'formula': '(2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH correction'}
+    allc = json.load(open(path)) if os.path.exists(path) else {}
+    allc[cfg] = out
+    json.dump(allc, open(path, 'w'), indent=1)
     print(json.dumps(out, indent=1))
 
 
