@@ -15,8 +15,10 @@
 // windows 2q and 2q + 1 as one pack when their blocks span at most 64
 // elements, else each window's blocks as a pack of at most 63 elements (every
 // block but a window's last is shorter than 32, the last is taken on its own
-// when it is longer), so no host plan is needed.
+// when it is longer; one longer than a wave goes to iso_long_kernel, a
+// workgroup per block, pava_long.hpp), so no host plan is needed.
 #include "pava.hpp"
+#include "pava_long.hpp"
 #include "pava_wave.hpp"
 
 namespace bsls {
@@ -77,11 +79,43 @@ constexpr int ISO_WIN = 32;   // pack window (elements)
 
 inline int64_t iso_nwin(int64_t n) { return (n + ISO_WIN - 1) / ISO_WIN; }
 
+// workspace: [Y0 n][Y1 n] doubles, [wscratch n][W0 n][W1 n][CH n+1][plan nwin+1]
+// [long count 4][long list n/65+1] int32 (long-block runs indexed by element)
+struct IsoWork {
+    double *Y0, *Y1;
+    int32_t *ws, *W0, *W1, *CH, *plan, *lcnt, *llist;
+    size_t bytes;
+};
+
+static IsoWork iso_layout(void *base, int64_t n) {
+    IsoWork w{};
+    char *p = (char *)base;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char *q = p + off;
+        off += (bytes + 15) & ~(size_t)15;
+        return q;
+    };
+    w.Y0 = (double *)take((size_t)n * 8);
+    w.Y1 = (double *)take((size_t)n * 8);
+    w.ws = (int32_t *)take((size_t)n * 4);
+    w.W0 = (int32_t *)take((size_t)n * 4);
+    w.W1 = (int32_t *)take((size_t)n * 4);
+    w.CH = (int32_t *)take((size_t)(n + 1) * 4);
+    w.plan = (int32_t *)take((size_t)(iso_nwin(n) + 1) * 4);
+    w.lcnt = (int32_t *)take(16);
+    w.llist = (int32_t *)take((size_t)(n / (WAVE + 1) + 1) * 4);
+    w.bytes = off;
+    return w;
+}
+
 // win_first[w] = first block starting at or after element 32 w (w = 0 .. nwin)
 __global__ __launch_bounds__(256) void iso_plan_kernel(const int64_t *__restrict__ starts,
                                                        int64_t nb, int64_t nwin,
-                                                       int32_t *__restrict__ win_first) {
+                                                       int32_t *__restrict__ win_first,
+                                                       int32_t *__restrict__ lcnt) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b == 0 && lcnt) *lcnt = 0;
     if (b > nb) return;
     const int64_t lo = (b == 0) ? 0 : (starts[b - 1] / ISO_WIN) + 1;
     const int64_t hi = (b == nb) ? nwin : starts[b] / ISO_WIN;
@@ -103,7 +137,8 @@ __device__ __forceinline__ void iso_wave_pack(double *__restrict__ y, int64_t s0
 __device__ __forceinline__ void iso_window(double *__restrict__ y,
                                            const int64_t *__restrict__ starts, int64_t nb,
                                            int64_t n, int64_t f, int64_t e,
-                                           int32_t *__restrict__ wscratch, double *ys, int *ps,
+                                           int32_t *__restrict__ lcnt,
+                                           int32_t *__restrict__ llist, double *ys, int *ps,
                                            int *cst) {
     const int l = lane_id();
     if (f >= e) return;
@@ -123,8 +158,7 @@ __device__ __forceinline__ void iso_window(double *__restrict__ y,
         if (len <= WAVE) {
             iso_wave_pack(y, sl, (int)len, 1ull, ys, ps, cst);
         } else if (l == 0) {
-            for (int64_t j = sl; j < el; ++j) wscratch[j] = 1;
-            pava_v1(y, wscratch, sl, el, 1);
+            llist[atomicAdd(lcnt, 1)] = (int32_t)(e - 1);   // iso_long_kernel's
         }
     }
 }
@@ -135,7 +169,8 @@ __global__ __launch_bounds__(256) void iso_pack_kernel(double *__restrict__ y,
                                                        const int64_t *__restrict__ starts,
                                                        int64_t nb, int64_t n, int64_t nwin,
                                                        const int32_t *__restrict__ win_first,
-                                                       int32_t *__restrict__ wscratch) {
+                                                       int32_t *__restrict__ lcnt,
+                                                       int32_t *__restrict__ llist) {
     const int l = lane_id();
     const int wv = threadIdx.x / WAVE;
     const int64_t q = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);
@@ -158,8 +193,22 @@ __global__ __launch_bounds__(256) void iso_pack_kernel(double *__restrict__ y,
         const uint64_t B = __ballot(l < span && ps[l] != 0);
         iso_wave_pack(y, s0, (int)span, B, pv_y[wv], ps, pv_c[wv]);
     } else {
-        iso_window(y, starts, nb, n, f, m, wscratch, pv_y[wv], ps, pv_c[wv]);
-        iso_window(y, starts, nb, n, m, e, wscratch, pv_y[wv], ps, pv_c[wv]);
+        iso_window(y, starts, nb, n, f, m, lcnt, llist, pv_y[wv], ps, pv_c[wv]);
+        iso_window(y, starts, nb, n, m, e, lcnt, llist, pv_y[wv], ps, pv_c[wv]);
+    }
+}
+
+// one workgroup per listed long block (> 64 elements), grid-strided
+__global__ __launch_bounds__(LONG_T) void iso_long_kernel(double *__restrict__ y,
+                                                          const int64_t *__restrict__ starts,
+                                                          int64_t nb, int64_t n, IsoWork w) {
+    __shared__ int64_t sh[LONG_T / 64 + 1];
+    __shared__ int flag;
+    const int cnt = *w.lcnt;
+    for (int idx = blockIdx.x; idx < cnt; idx += gridDim.x) {
+        const int64_t b = w.llist[idx];
+        const int64_t s = starts[b], k = block_end(starts, nb, b, n) - s;
+        pava_v1_long(y + s, k, w.Y0 + s, w.Y1 + s, w.W0 + s, w.W1 + s, w.CH + s, sh, &flag);
     }
 }
 
@@ -168,31 +217,35 @@ __global__ __launch_bounds__(256) void iso_pack_kernel(double *__restrict__ y,
 using namespace bsls;
 
 extern "C" size_t bsls_isotonic_workspace_size(int64_t n) {
-    // unit run lengths (n int32) + the pack plan (nwin + 1 int32)
-    const int64_t b = n * 4 + (iso_nwin(n) + 1) * 4;
-    return (size_t)((b + 15) & ~(int64_t)15);
+    return iso_layout(nullptr, n).bytes;
 }
 
 extern "C" int bsls_isotonic_multi(int variant, double *d_y, const int64_t *d_starts,
                                    int64_t nblocks, int64_t n, int32_t *d_weight, int expand,
                                    int64_t max_block, void *d_work, size_t work_bytes,
                                    int32_t *d_status, void *stream) {
-    (void)max_block;
     if (nblocks <= 0 || n <= 0 || !d_y || !d_starts) return BSLS_E_ARG;
     if (variant < 1 || variant > 3) return BSLS_E_ARG;
     if (variant != 2 && !d_weight && (!d_work || work_bytes < bsls_isotonic_workspace_size(n)))
         return BSLS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
     const int grid = grid_for(nblocks, WAVE);
-    int32_t *ws = (int32_t *)d_work;
+    const IsoWork w = iso_layout(d_work, n);
+    int32_t *ws = w.ws;
     if (variant == 1 && !d_weight && expand) {
         const int64_t nwin = iso_nwin(n);
-        int32_t *wf = ws + n;
-        iso_plan_kernel<<<grid_for(nblocks + 1, 256), 256, 0, st>>>(d_starts, nblocks, nwin, wf);
+        iso_plan_kernel<<<grid_for(nblocks + 1, 256), 256, 0, st>>>(d_starts, nblocks, nwin,
+                                                                    w.plan, w.lcnt);
         BSLS_LAUNCH_CHECK();
-        iso_pack_kernel<<<grid_for((nwin + 1) / 2, 4), 256, 0, st>>>(d_y, d_starts, nblocks, n, nwin, wf,
-                                                           ws);
+        iso_pack_kernel<<<grid_for((nwin + 1) / 2, 4), 256, 0, st>>>(d_y, d_starts, nblocks, n, nwin,
+                                                                    w.plan, w.lcnt, w.llist);
         BSLS_LAUNCH_CHECK();
+        if (max_block > WAVE) {
+            const int64_t most = n / (WAVE + 1) + 1;
+            iso_long_kernel<<<(int)(most < 1024 ? most : 1024), LONG_T, 0, st>>>(d_y, d_starts,
+                                                                              nblocks, n, w);
+            BSLS_LAUNCH_CHECK();
+        }
         return BSLS_OK;
     }
     if (variant == 1)

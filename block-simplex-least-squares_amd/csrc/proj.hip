@@ -20,6 +20,8 @@
 //                thread into LDS, conditions + last-index search in parallel;
 //   k > 8192     one workgroup, sort in a global workspace (rare: the
 //                reference's stack VLA already segfaults near k = 1M).
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "bsls_common.hpp"
 
 namespace bsls {
@@ -567,32 +569,91 @@ __global__ __launch_bounds__(LARGE_THREADS) void proj_large_kernel(
     }
 }
 
+// Blocks longer than LDS_MAX (the reference's stress shapes go to 1e6 in one
+// block, python/experiments/test_stress_proj_simplex.py:24-44): the whole
+// chip sorts them -- every element of such a block keyed (value, block id),
+// sorted by value descending then stably by block id (rocPRIM radix sorts:
+// each block's values contiguous, in the reference's std::sort(greater)
+// order) -- then one workgroup per block runs the reference's chain on its
+// sorted run (S_i += u_i in order, the test at every i with the reference's
+// division) only until it is settled: the exact e_i = (i+1) u_i + 1 - S_i is
+// non-increasing, so once the computed e_i < -margin (margin >= every rounding
+// error of the chain, as chain_steps) no later i passes; and writes
+// y = max(lambda + y, 0).  The ball variant clamps first (ball_prepass,
+// python/c_extensions/proj_simplex.h:50-74) and skips a block whose clamped
+// sum is <= 1.
 template <bool BALL>
-__global__ __launch_bounds__(HUGE_THREADS) void proj_huge_kernel(
+__global__ __launch_bounds__(HUGE_THREADS) void proj_huge_fill(
     double *__restrict__ y, const int64_t *__restrict__ starts, int64_t nb, int64_t n,
     const int64_t *__restrict__ big_list, const unsigned *__restrict__ big_count,
-    double *__restrict__ U, double *__restrict__ S) {
+    double *__restrict__ keys, int32_t *__restrict__ ids) {
     __shared__ int64_t scr[SCRATCH_WORDS];
+    // (every other element: key 0.0, id 0x7F7F7F7F by the launcher's memsets,
+    // so it sorts after every huge block)
     const unsigned cnt = *big_count;
-    for (unsigned idx = 0; idx < cnt; ++idx) {
+    for (unsigned idx = blockIdx.x; idx < cnt; idx += gridDim.x) {
         const int64_t b = big_list[idx];
         const int64_t s = starts[b];
         const int64_t k = block_end(starts, nb, b, n) - s;
         if (k <= LDS_MAX) continue;
-        const int64_t P = pow2_ceil(k);
-        for (int64_t j = threadIdx.x; j < P; j += blockDim.x) U[j] = (j < k) ? y[s + j] : -INFINITY;
-        __syncthreads();
-        if (BALL && !ball_prepass(U, k, scr)) {
-            for (int64_t j = threadIdx.x; j < k; j += blockDim.x) y[s + j] = U[j];
-            __syncthreads();
-            continue;
+        if (BALL && !ball_prepass(y + s, k, scr)) continue;   // clamped in place, done
+        for (int64_t j = threadIdx.x; j < k; j += HUGE_THREADS) {
+            keys[s + j] = y[s + j];
+            ids[s + j] = (int32_t)b;
         }
-        bitonic_desc_shared(U, P);
-        const double lam = lambda_shared(U, S, k, scr);
-        for (int64_t j = threadIdx.x; j < k; j += blockDim.x) {
-            double o = y[s + j];
-            if (BALL) o = (o < 0.0) ? 0.0 : o;
-            y[s + j] = relu_ref(lam + o);
+    }
+}
+
+template <bool BALL>
+__global__ __launch_bounds__(HUGE_THREADS) void proj_huge_apply(
+    double *__restrict__ y, const int64_t *__restrict__ starts, int64_t nb, int64_t n,
+    const int64_t *__restrict__ big_list, const unsigned *__restrict__ big_count,
+    const double *__restrict__ u_all, const int32_t *__restrict__ ids) {
+    __shared__ double lam_sh;
+    __shared__ int64_t pos_sh;
+    const unsigned cnt = *big_count;
+    for (unsigned idx = blockIdx.x; idx < cnt; idx += gridDim.x) {
+        const int64_t b = big_list[idx];
+        const int64_t s = starts[b];
+        const int64_t k = block_end(starts, nb, b, n) - s;
+        if (k <= LDS_MAX) continue;
+        if (threadIdx.x == 0) {
+            // this block's sorted run: the first id >= b
+            int64_t lo = 0, hi = n;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (ids[mid] < (int32_t)b) lo = mid + 1;
+                else hi = mid;
+            }
+            pos_sh = lo;
+        }
+        __syncthreads();
+        const int64_t pos = pos_sh;
+        const bool active = pos < n && ids[pos] == (int32_t)b;   // ball: not skipped
+        if (active && threadIdx.x == 0) {
+            const double *u = u_all + pos;
+            const double Mx = fmax(fabs(u[0]), fabs(u[k - 1]));
+            const double kk = (double)k;
+            const double margin = kk * 0x1p-49 * (1. + 2. * kk * Mx);
+            double run = u[0];
+            double lam = 1. - run;                      // proj_simplex.h:27-28
+            for (int64_t i = 1; i < k; ++i) {
+                run = run + u[i];
+                const double tmp = (1. - run) / ((double)i + 1.);
+                if (u[i] + tmp > 0) lam = tmp;          // the last i that passes wins
+                const double E = __builtin_fma((double)i + 1., u[i], 1. - run);
+                if (E < -margin) break;                 // settled: no later i passes
+            }
+            lam_sh = lam;
+        }
+        __syncthreads();
+        if (active) {
+            const double lam = lam_sh;
+            for (int64_t j = threadIdx.x; j < k; j += HUGE_THREADS) {
+                double o = y[s + j];
+                if (BALL) o = (o < 0.0) ? 0.0 : o;
+                y[s + j] = relu_ref(lam + o);
+            }
         }
         __syncthreads();
     }
@@ -601,7 +662,10 @@ __global__ __launch_bounds__(HUGE_THREADS) void proj_huge_kernel(
 struct ProjWork {
     unsigned *count;
     int64_t *list;
-    double *U, *S;
+    double *K0, *K1;      // huge path: sort keys (values), double-buffered
+    int32_t *I0, *I1;     // huge path: block ids
+    void *tmp;            // rocPRIM temporary storage
+    size_t tmp_bytes;
     size_t bytes;
 };
 
@@ -617,11 +681,17 @@ static ProjWork proj_layout(void *base, int64_t n, int64_t nb, int64_t max_block
     w.list = (int64_t *)(p + off);
     off += align16((size_t)nbig * sizeof(int64_t));
     if (max_block > LDS_MAX) {
-        const int64_t P = pow2_ceil(max_block);
-        w.U = (double *)(p + off);
-        off += align16((size_t)P * sizeof(double));
-        w.S = (double *)(p + off);
-        off += align16((size_t)max_block * sizeof(double));
+        w.K0 = (double *)(p + off);
+        off += align16((size_t)n * 8);
+        w.K1 = (double *)(p + off);
+        off += align16((size_t)n * 8);
+        w.I0 = (int32_t *)(p + off);
+        off += align16((size_t)n * 4);
+        w.I1 = (int32_t *)(p + off);
+        off += align16((size_t)n * 4);
+        w.tmp = (void *)(p + off);
+        w.tmp_bytes = align16((size_t)n * 4 + ((size_t)1 << 20));
+        off += w.tmp_bytes;
     }
     w.bytes = off;
     return w;
@@ -656,7 +726,28 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
         BSLS_LAUNCH_CHECK();
     }
     if (max_block > LDS_MAX) {
-        proj_huge_kernel<BALL><<<1, HUGE_THREADS, 0, st>>>(y, starts, nb, n, w.list, w.count, w.U, w.S);
+        const int64_t most = n / (LDS_MAX + 1) + 1;
+        const int grid = (int)(most < 1024 ? most : 1024);
+        BSLS_CHECK(hipMemsetAsync(w.K0, 0, (size_t)n * 8, st));
+        BSLS_CHECK(hipMemsetAsync(w.I0, 0x7F, (size_t)n * 4, st));
+        proj_huge_fill<BALL><<<grid, HUGE_THREADS, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                            w.K0, w.I0);
+        BSLS_LAUNCH_CHECK();
+        // by value (descending), then stably by block id: each huge block's
+        // values contiguous and in std::sort(greater) order
+        rocprim::double_buffer<double> keys(w.K0, w.K1);
+        rocprim::double_buffer<int32_t> ids(w.I0, w.I1);
+        size_t need = 0;
+        BSLS_CHECK(rocprim::radix_sort_pairs_desc(nullptr, need, keys, ids, (size_t)n, 0, 64, st));
+        if (need > w.tmp_bytes) return BSLS_E_WORKSPACE;
+        BSLS_CHECK(rocprim::radix_sort_pairs_desc(w.tmp, need, keys, ids, (size_t)n, 0, 64, st));
+        const unsigned idbits = 31;   // block ids < 2^31, the filler 0x7F7F7F7F
+        need = 0;
+        BSLS_CHECK(rocprim::radix_sort_pairs(nullptr, need, ids, keys, (size_t)n, 0, idbits, st));
+        if (need > w.tmp_bytes) return BSLS_E_WORKSPACE;
+        BSLS_CHECK(rocprim::radix_sort_pairs(w.tmp, need, ids, keys, (size_t)n, 0, idbits, st));
+        proj_huge_apply<BALL><<<grid, HUGE_THREADS, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                             keys.current(), ids.current());
         BSLS_LAUNCH_CHECK();
     }
     return BSLS_OK;

@@ -52,7 +52,10 @@ int bsls_proj_multi_ball(double *d_y, const int64_t *d_starts, int64_t nblocks, 
  * isotonic_regression_multi{,_2,_3} (isotonic_regression.h:85-102,157-164).
  * d_weight: run-length array of n int32 (NULL = fresh ones, as weight=None);
  * updated in place like the reference's int weight buffer.  expand = the
- * reference's `update` flag.  Variant 1 is what python/main.py:64 calls. */
+ * reference's `update` flag.  Variant 1 is what python/main.py:64 calls.
+ * max_block bounds every block length (as for the projections); with
+ * variant 1, weight NULL and expand = 1 blocks of <= 64 elements run
+ * wave-parallel and longer ones one workgroup each (bit-identical either way). */
 size_t bsls_isotonic_workspace_size(int64_t n);
 int bsls_isotonic_multi(int variant, double *d_y, const int64_t *d_starts, int64_t nblocks,
                         int64_t n, int32_t *d_weight, int expand, int64_t max_block,

@@ -264,3 +264,60 @@ def test_spmv_vs_scipy(cuda, shape, per_row):
         D.group = G
         o = D.matvec(torch.from_numpy(x).cuda())
         np.testing.assert_allclose(o.cpu().numpy(), A.dot(x), rtol=1e-13, atol=1e-13)
+
+
+# ------------------------------------------------------------------ stress shapes
+
+def test_proj_stress_shapes_bit_exact(cx, orc):
+    """python/experiments/test_stress_proj_simplex.py:24-44: single U[0,1) blocks
+    up to 1e6 and 1e6 elements in 10 / 100 / 1e4 random blocks (the whole-chip
+    sort path for blocks > 8192), simplex and l1-ball, vs the oracle."""
+    np.random.seed(SEED)
+    for n in (20_000, 1_000_000):
+        y = np.random.rand(n)
+        a, r = y.copy(), y.copy()
+        cx.proj_simplex_c(a, 0, n)
+        orc.proj_simplex_c(r, 0, n)
+        assert exact(a, r), n
+    for nb in (10, 100, 10_000):
+        y = np.random.rand(1_000_000)
+        blocks = np.sort(np.random.choice(1_000_000, nb, replace=False)).astype(np.int64)
+        for gpu, cpu in ((cx.proj_multi_simplex_c, orc.proj_multi_simplex_c),
+                         (cx.proj_multi_ball_c, orc.proj_multi_ball_c)):
+            a, r = y.copy(), y.copy()
+            gpu(a, blocks)
+            cpu(r, blocks)
+            assert exact(a, r), nb
+    # ball blocks whose clamped sum is <= 1 (left clamped, not projected)
+    y = np.random.rand(100_000) * 1e-6 - 2e-7
+    a, r = y.copy(), y.copy()
+    cx.proj_multi_ball_c(a, np.array([0, 30_000]))
+    orc.proj_multi_ball_c(r, np.array([0, 30_000]))
+    assert exact(a, r)
+
+
+def test_pava_stress_shapes_bit_exact(cx, orc):
+    """python/experiments/PAVA_worst_case.py:12-40 on variant 1 (main.py's):
+    the log-trend data up to 1e6 in one block and the worst case (arange with
+    y[-1] = -1e12, one pooling per pass), one workgroup per long block."""
+    rs = np.random.RandomState(0)
+    for n in (1000, 100_000, 1_000_000):
+        y = rs.randint(-50, 50, size=(n,)) + 50. * np.log(1 + np.arange(n))
+        a, r = y.copy(), y.copy()
+        cx.isotonic_regression_c(a, 0, n)
+        orc.isotonic_regression_c(r, 0, n)
+        assert exact(a, r), n
+    for n in (100, 2000):
+        y = np.arange(n).astype(float)
+        y[-1] = -1e12
+        a, r = y.copy(), y.copy()
+        cx.isotonic_regression_c(a, 0, n)
+        orc.isotonic_regression_c(r, 0, n)
+        assert exact(a, r), n
+    # several long blocks next to short ones, one pass
+    y = rs.randn(300_000)
+    blocks = np.sort(np.concatenate(([0], rs.choice(np.arange(1, 300_000), 40, replace=False))))
+    a, r = y.copy(), y.copy()
+    cx.isotonic_regression_multi_c(a, blocks)
+    orc.isotonic_regression_multi_c(r, blocks)
+    assert exact(a, r)

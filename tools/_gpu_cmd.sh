@@ -1,9 +1,6 @@
 set -u
 mkdir -p gpurun_out
-{
-for V in "" _nt; do
-  echo "== variant '$V' C5"; BSLS_LIB=block-simplex-least-squares_amd/lib/libbsls_hip$V.so timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 | grep -E "K1|K2|iteration" || exit 1
-  echo "== variant '$V' shard"; BSLS_LIB=block-simplex-least-squares_amd/lib/libbsls_hip$V.so timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 --world 8 | grep -E "K1|K2|iteration" || exit 1
-done
-} > gpurun_out/st18.log 2>&1
-echo "stage rc=$?"
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_kernels.py > gpurun_out/t20.log 2>&1
+echo "tests rc=$?"
+timeout -k 10 300 python tools/stress_time.py --what proj,multi > gpurun_out/stress3.log 2>&1
+echo "stress rc=$?"
