@@ -73,7 +73,8 @@ class BBProblem(ctypes.Structure):
                 ('work', _vp),
                 ('max_zblock', _i64), ('max_iter', _i64), ('opt_tol', _dbl),
                 ('early_exit', _i32), ('reserved', _i32),
-                ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz)]
+                ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz),
+                ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp)]
 
 
 class CSR(ctypes.Structure):
@@ -133,6 +134,7 @@ _SIGS = {
                              _sz, _vp]),
     'bsls_bb_workspace_size': (_sz, [_i64, _i64, _i64]),
     'bsls_bb_dz_offset': (_sz, [_i64, _i64, _i64]),
+    'bsls_bb_long_scratch_size': (_sz, [_i64]),
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),

@@ -33,6 +33,7 @@
 // workgroup (bsls_common.hpp last_block_sum), so runs are bit-reproducible.
 // Scalars live in device memory (scal[]); the host only polls them.
 #include "pava.hpp"
+#include "pava_long.hpp"
 #include "pava_wave.hpp"
 #include "panels.hpp"
 #include "tiles.hpp"
@@ -595,8 +596,9 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
                 wt_store_f64(rx, xo, P.colv ? cv[q] * d : d);
                 if (bend) wt_store_f64(rx, xo + 8, P.colv ? cv2[q] * (0.0 - v) : (0.0 - v));
             }
-        } else if (l == 0) {
+        } else if (!P.long_packs && l == 0) {
             // one block longer than a wave: serial PAVA in global memory
+            // (with P.long_packs bb_k3_long takes it, a workgroup per block)
             const int64_t xs = P.xstarts[b0[q]];
             for (int64_t j = z0[q]; j < z0[q] + L[q]; ++j) {
                 zn[j] = zc[j] - t * g[j];
@@ -614,6 +616,45 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
             }
             x_put(P, xo, 0.0 - prev);
         }
+    }
+}
+
+// K3 for one z-block longer than a wave, one 1024-thread workgroup per block
+// (after bb_k3 in the same stream): z - t g, PAVA v1 by the whole workgroup
+// (pava_long.hpp, bit-identical), clip, dz and x as bb_k3's serial path.
+// t as bb_step_t, without its writes (bb_k3 made them).
+__global__ __launch_bounds__(LONG_T) void bb_k3_long(bsls_bb_problem P, int64_t iter,
+                                                     const double *__restrict__ zc,
+                                                     const double *__restrict__ g,
+                                                     double *__restrict__ zn,
+                                                     double *__restrict__ dzo) {
+    __shared__ int64_t sh[LONG_T / 64 + 1];
+    __shared__ int flag;
+    const double *s = P.scal;
+    if (s[BSLS_S_STOP] != 0.0) return;
+    if (P.early_exit && s[BSLS_S_SUMDG] == 0.0) return;
+    const double t = s[BSLS_S_DZDG] / s[BSLS_S_DGDG];
+    const int64_t q = P.long_packs[blockIdx.x];
+    const int64_t z0 = P.pk_z0[q], b0 = P.pk_b0[q], L = P.pk_len[q];
+    const int64_t off = P.long_off[blockIdx.x], tot = P.long_off[P.nlong];
+    double *Y0 = (double *)P.long_scratch + off;
+    double *Y1 = (double *)P.long_scratch + tot + off;
+    int32_t *W = (int32_t *)((double *)P.long_scratch + 2 * tot);
+    int32_t *W0 = W + off, *W1 = W + tot + off, *CH = W + 2 * tot + blockIdx.x + off;
+    for (int64_t j = threadIdx.x; j < L; j += LONG_T) zn[z0 + j] = zc[z0 + j] - t * g[z0 + j];
+    __syncthreads();
+    pava_v1_long(zn + z0, L, Y0, Y1, W0, W1, CH, sh, &flag);
+    for (int64_t j = threadIdx.x; j < L; j += LONG_T) {
+        const double v = clip01(zn[z0 + j]);
+        zn[z0 + j] = v;
+        dzo[z0 + j] = v - zc[z0 + j];
+    }
+    __syncthreads();
+    const int64_t xs = P.xstarts[b0];
+    for (int64_t j = threadIdx.x; j <= L; j += LONG_T) {
+        const double v = (j < L) ? zn[z0 + j] : 0.0;
+        const double prev = (j > 0) ? zn[z0 + j - 1] : 0.0;
+        x_put(P, xs + j, v - prev);
     }
 }
 
@@ -728,6 +769,8 @@ static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
                       double *zn, const BBWork &w, hipStream_t st) {
     bb_k3<<<grid_for(P.npacks, 4 * K3_PPW), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+    if (P.long_packs && P.nlong > 0)
+        bb_k3_long<<<(int)P.nlong, LONG_T, 0, st>>>(P, iter, zc, g, zn, w.dz);
 }
 
 static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t halo,
@@ -776,6 +819,8 @@ static int check_problem(const bsls_bb_problem *p) {
     if (!p->pk_z0 || !p->pk_b0 || !p->pk_mask || !p->pk_len || p->npacks < 1) return BSLS_E_ARG;
     if (!p->z[0] || !p->z[1] || !p->g[0] || !p->g[1] || !p->x || !p->r || !p->scal || !p->work)
         return BSLS_E_ARG;
+    if (p->long_packs && (p->nlong < 0 || (p->nlong > 0 && (!p->long_off || !p->long_scratch))))
+        return BSLS_E_ARG;
     return BSLS_OK;
 }
 
@@ -785,6 +830,11 @@ using namespace bsls;
 
 extern "C" size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz) {
     return bb_layout(nullptr, m, n, nz).bytes;
+}
+
+extern "C" size_t bsls_bb_long_scratch_size(int64_t total) {
+    // Y0, Y1 (doubles), W0, W1, CH (int32; CH one more per block, <= total)
+    return (size_t)(total > 0 ? total : 0) * 32 + 64;
 }
 
 extern "C" size_t bsls_bb_dz_offset(int64_t m, int64_t n, int64_t nz) {

@@ -731,6 +731,18 @@ class BBEngine:
         P.pk_z0, P.pk_b0, P.pk_mask, P.pk_len = (pk['z0'].data_ptr(), pk['b0'].data_ptr(),
                                                  pk['mask'].data_ptr(), pk['len'].data_ptr())
         P.npacks = pk['n']
+        # packs of one z-block longer than a wave: a workgroup each (bb_k3_long)
+        ln = pk['len'].cpu().numpy()
+        longs = np.nonzero(ln > 64)[0].astype(np.int32)
+        self.long_packs = None
+        if longs.size:
+            off = np.concatenate(([0], np.cumsum(ln[longs]))).astype(np.int64)
+            self.long_packs = torch.from_numpy(longs).cuda()
+            self.long_off = torch.from_numpy(off).cuda()
+            self.long_scratch = torch.zeros(L.bsls_bb_long_scratch_size(int(off[-1])),
+                                            dtype=torch.uint8, device='cuda')
+            P.long_packs, P.nlong = self.long_packs.data_ptr(), int(longs.size)
+            P.long_off, P.long_scratch = self.long_off.data_ptr(), self.long_scratch.data_ptr()
         P.z[0], P.z[1] = self.z[0].data_ptr(), self.z[1].data_ptr()
         P.g[0], P.g[1] = self.g[0].data_ptr(), self.g[1].data_ptr()
         P.x, P.r, P.scal, P.work = (self.x.data_ptr(), self.r.data_ptr(), self.scal.data_ptr(),

@@ -288,12 +288,24 @@ typedef struct bsls_bb_problem {
     bsls_tiles ATt;
     double *wpart;
     size_t work_bytes;              /* size of work; < bsls_bb_workspace_size -> BSLS_E_WORKSPACE */
+    /* K3's packs of one z-block longer than a wave (pk_len > 64): with
+     * long_packs set, K3 leaves them to a follow-up launch of one workgroup per
+     * block (PAVA v1 with the whole workgroup, csrc/pava_long.hpp); long_off
+     * (nlong + 1) = prefix of their z lengths, long_scratch =
+     * bsls_bb_long_scratch_size(long_off[nlong]) bytes.  NULL / 0: K3 runs
+     * them serially in one lane. */
+    const int32_t *long_packs;
+    int64_t nlong;
+    const int64_t *long_off;
+    void *long_scratch;
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
 /* Byte offset in `work` of dz = z - z_prev (nz doubles), the hand-off K3 writes
  * for the next K2 (and the prologue for iteration 1); for tests and tools. */
 size_t bsls_bb_dz_offset(int64_t m, int64_t n, int64_t nz);
+/* Scratch bytes for K3's long blocks of `total` z entries in all. */
+size_t bsls_bb_long_scratch_size(int64_t total);
 /* BB.py:14-15 and the first f(z0): resets scal/tickets, g[0] = grad(z0 + 1),
  * r = r(z0), scal[FX] = f(z0).  z[0] must hold z0. */
 int bsls_bb_prologue(const bsls_bb_problem *p, void *stream);
