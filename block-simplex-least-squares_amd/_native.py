@@ -52,6 +52,7 @@ class Panels(ctypes.Structure):
 TILE_THREADS = 1024       # BSLS_TILE_THREADS
 TILE_MAXSLOTS = 20        # BSLS_TILE_MAXSLOTS
 TILE_LDS_BYTES = 163840 - 512   # dynamic LDS a tile kernel may take (bb.hip PANEL_LDS_MAX)
+TILE_NT = 0x100                  # bsls_tiles.layout flag BSLS_TILE_NT
 
 
 class Tiles(ctypes.Structure):

@@ -38,7 +38,7 @@ __host__ __device__ inline int64_t tile_nslots(const bsls_tiles &T) {
 // dynamic LDS doubles of a tile kernel: the row sums (+ the dummy slot), and
 // with `colv` the rows' column scales (K2 on a scaled incidence)
 __host__ __device__ inline size_t tile_lds_doubles(const bsls_tiles &T, bool colv) {
-    if (T.layout == 1) return (size_t)(T.H + T.halo + 1) * (colv ? 2 : 1);
+    if ((T.layout & 0xFF) == 1) return (size_t)(T.H + T.halo + 1) * (colv ? 2 : 1);
     return (size_t)(tile_nslots(T) + 1) * TILE_T * (colv ? 2 : 1);
 }
 
@@ -57,16 +57,15 @@ __device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t
 
 typedef uint32_t tile_quad __attribute__((ext_vector_type(4)));
 
-// BSLS_TILE_NT=1: the dealt walk's entry stream by non-temporal loads (A/B)
-#ifndef BSLS_TILE_NT
-#define BSLS_TILE_NT 0
-#endif
+// the dealt walk's entry stream: non-temporal loads when the image is larger
+// than the Infinity Cache (layout flag BSLS_TILE_NT: the stream would only
+// evict the gathered vector; C5 on one GPU K1 368 -> 357, K2 505 -> 492 us),
+// plain loads when it stays resident across iterations (a C5 shard / 8:
+// K1 60 vs 70, K2 79 vs 87 us with nt)
+template <bool NT>
 __device__ __forceinline__ tile_quad tq_load(const tile_quad *p) {
-#if BSLS_TILE_NT
-    return __builtin_nontemporal_load(p);
-#else
+    if (NT) return __builtin_nontemporal_load(p);
     return *p;
-#endif
 }
 
 // Walk this thread's stream of tile (rb, g) into rows[] (LDS, zeroed by the
@@ -129,7 +128,7 @@ __device__ __forceinline__ void tile_walk(const bsls_tiles &T, int64_t rb, int64
 // (rb, g) quad-step by quad-step -- one 16-B entry load (4 slots) and one
 // scalar 16-B base load per step, loaded P steps ahead, the gathers of step
 // s + 1 issued before the LDS atomic adds of step s.  MODE as tile_walk.
-template <int MODE, int P = 4>
+template <int MODE, bool NT, int P = 4>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
                                                 const double *rcol) {
@@ -145,7 +144,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
     int4 bring[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        ring[k] = (k < nq) ? tq_load(Q + (int64_t)k * 1024) : tile_quad{0, 0, 0, 0};
+        ring[k] = (k < nq) ? tq_load<NT>(Q + (int64_t)k * 1024) : tile_quad{0, 0, 0, 0};
         bring[k] = (k < nq) ? Bq[(int64_t)k * 16] : int4{0, 0, 0, 0};
     }
     double v[4], vn[4], a[4], an[4];
@@ -166,7 +165,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
             const tile_quad cur = ring[k];
             if (q + k + 1 < nq) gat(ring[(k + 1) % P], bring[(k + 1) % P], q + k + 1, vn, an);
             if (q + k + P < nq) {
-                ring[k] = tq_load(Q + (q + k + P) * 1024);
+                ring[k] = tq_load<NT>(Q + (q + k + P) * 1024);
                 bring[k] = Bq[(q + k + P) * 16];
             }
             if (q + k < nq) {
@@ -194,7 +193,8 @@ template <int MODE>
 __device__ __forceinline__ void tile_walk_any(const bsls_tiles &T, int64_t rb, int64_t g,
                                               const double *__restrict__ src, double *rows,
                                               const double *rcol) {
-    if (T.layout == 1) tile_walk_dealt<MODE>(T, rb, g, src, rows, rcol);
+    if (T.layout == 1) tile_walk_dealt<MODE, false>(T, rb, g, src, rows, rcol);
+    else if (T.layout == (1 | BSLS_TILE_NT)) tile_walk_dealt<MODE, true>(T, rb, g, src, rows, rcol);
     else tile_walk<MODE>(T, rb, g, src, rows, rcol);
 }
 

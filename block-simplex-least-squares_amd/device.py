@@ -431,6 +431,17 @@ def _dealt_matvec(img, x, colv=None, group_sums=False):
     return (out, parts) if group_sums else out
 
 
+NT_BYTES = 256 << 20
+
+
+def self_bytes(img):
+    """Bytes of a tile image's entry stream (+ values)."""
+    b = img['ent'].nbytes
+    if img.get('val') is not None:
+        b += img['val'].nbytes
+    return b
+
+
 class DeviceTiles:
     """A tile image on the device + the ctypes struct pointing at it."""
 
@@ -461,7 +472,9 @@ class DeviceTiles:
         if layout == 1:
             self.t['base'] = torch.from_numpy(img['base']).cuda()
         S = _native.Tiles()
-        S.layout = layout
+        # dealt images larger than the Infinity Cache stream their entries
+        # non-temporally (csrc/tiles.hpp tq_load)
+        S.layout = layout | (_native.TILE_NT if layout == 1 and self_bytes(img) > NT_BYTES else 0)
         S.base = self.t['base'].data_ptr() if layout == 1 else None
         S.rows, S.cols, S.H, S.halo = R, C, H, halo
         S.nrb, S.ngroups, S.order, S.nquads = img['nrb'], G, order, img['nquads']

@@ -200,6 +200,7 @@ typedef struct bsls_panels {
  * one after the other over the launch's row blocks (b / 8 = j * nrb' + rb, g =
  * x + 8 j, nrb' = the row blocks of the launch). */
 #define BSLS_TILE_THREADS 1024
+#define BSLS_TILE_NT 0x100
 #define BSLS_TILE_MAXSLOTS 20       /* LDS: (nslots + 1) * 1024 doubles (x2 with colv) */
 /* layout 1 ("dealt"; bsls_tiles_build_dealt): the entries of tile (rb, g) are
  * sorted by column and dealt to the workgroup in that order, so the 64 gathers
@@ -224,7 +225,8 @@ typedef struct bsls_tiles {
     const int64_t *wave_off;        /* layout 0: nrb * ngroups * 16 + 1 (in quads); 1: see above */
     const uint32_t *ent;
     const double *val;              /* 4 * nquads, or NULL (scaled incidence) */
-    int64_t layout;                 /* 0: thread streams (CSR order per row), 1: dealt */
+    int64_t layout;                 /* 0: thread streams (CSR order per row), 1: dealt;
+                                       | BSLS_TILE_NT: dealt, entries by non-temporal loads */
     const int32_t *base;            /* layout 1: 4 * nquads / 64 instruction bases */
 } bsls_tiles;
 

@@ -84,6 +84,8 @@ def test_panel_limits_match_header(native):
     assert '#define BSLS_PANEL_CHUNK %d' % native.PANEL_CHUNK in hdr
     assert '#define BSLS_PANEL_ROWS %d' % native.PANEL_ROWS in hdr
     assert '#define BSLS_PANEL_WAVES %d' % native.PANEL_WAVES in hdr
+    assert '#define BSLS_TILE_THREADS %d' % native.TILE_THREADS in hdr
+    assert '#define BSLS_TILE_NT 0x%x' % native.TILE_NT in hdr
 
 
 def test_tile_planner(native):
