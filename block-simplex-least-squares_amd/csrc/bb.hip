@@ -289,6 +289,12 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     __syncthreads();
     const int64_t G = T.ngroups;
     bool fin = true;
+    if (MODE == 3 && G == 1) {
+        // dealt image, one group: w_i = colv_i * (sum of r over row i), one
+        // product per row (the sums' order is not fixed anyway)
+        for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x) rows[i] = P.colv[i0 + i] * rows[i];
+        __syncthreads();
+    }
     if (G > 1) {
         double *wp = P.wpart + (g * T.nrb + rb) * (T.H + 1);
         for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x)
@@ -757,7 +763,7 @@ static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
                       const BBWork &w, hipStream_t st) {
     if (P.ATt.ent) {
         if (!P.colv) launch_k2t_mode<1, ITER>(P, gp, gout, w, st);
-        else if (P.ATt.ngroups == 1) launch_k2t_mode<2, ITER>(P, gp, gout, w, st);
+        else if (P.ATt.ngroups == 1 && P.ATt.layout == 0) launch_k2t_mode<2, ITER>(P, gp, gout, w, st);
         else launch_k2t_mode<3, ITER>(P, gp, gout, w, st);
     } else if (P.colv) {
         launch_k2_mode<2, ITER>(P, gp, gout, w, st);
@@ -809,7 +815,8 @@ static int check_problem(const bsls_bb_problem *p) {
         return BSLS_E_ARG;
     }
     if (p->ATt.ent) {
-        if (!tiles_ok(p->ATt, p->n, p->m, 1, general, !general && p->ATt.ngroups == 1))
+        if (!tiles_ok(p->ATt, p->n, p->m, 1, general,
+                      !general && p->ATt.ngroups == 1 && p->ATt.layout == 0))
             return BSLS_E_ARG;
         if (p->ATt.ngroups > 1 && !p->wpart) return BSLS_E_ARG;
     } else if (!panels_ok(p->AT, p->n, p->m, 1, general) || p->AT.ngroups != 1) {

@@ -685,7 +685,11 @@ class BBEngine:
             except PanelOverflow:
                 self.fmt_AT = 'tiles'
         if self.fmt_AT == 'tiles':
-            self.AT_til = DeviceTiles(AT, 1, values=not self.scaled, colv_lds=self.scaled,
+            # (the thread-stream K2 keeps each row's colv in LDS beside its sum:
+            # every term colv_i * r_j, SciPy's product; the dealt K2 scales
+            # the row sum once, so its LDS holds twice the rows)
+            self.AT_til = DeviceTiles(AT, 1, values=not self.scaled,
+                                      colv_lds=self.scaled and tile_layouts[1] == 0,
                                       plan=tile_plans[1], layout=tile_layouts[1])
         opts = options or {}
         self.options = dict(opts)

@@ -1,11 +1,13 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_c5.py tests/test_gpu_distributed.py > gpurun_out/t22.log 2>&1
-echo "tests rc=$?"
 {
-echo "== C5"; timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 | grep -E "K1|K2|K3|iteration" || exit 1
-echo "== shard"; timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 --world 8 | grep -E "K1|K2|K3|iteration" || exit 1
-echo "== shard/2"; timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 --world 2 | grep -E "K1|K2|K3|iteration" || exit 1
-echo "== shard/4"; timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 --world 4 | grep -E "K1|K2|K3|iteration" || exit 1
-} > gpurun_out/st22.log 2>&1
+for PT in 9766,2 19532,4 6510,1; do
+echo "== shard K2 $PT"; BSLS_TILE_PLAN_AT=$PT timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 --world 8 | grep -E "K2|iteration" || exit 1
+done
+for PT in 19532,2 9766,1; do
+echo "== shard/4 K2 $PT"; BSLS_TILE_PLAN_AT=$PT timeout -k 10 200 python tools/stage_time.py --iters 50 --reps 10 --shape C5 --world 4 | grep -E "K2|iteration" || exit 1
+done
+} > gpurun_out/st24.log 2>&1
 echo "stage rc=$?"
+timeout -k 10 700 python bench.py --no-cpu-baseline > gpurun_out/b24.log 2>&1
+echo "bench rc=$?"
