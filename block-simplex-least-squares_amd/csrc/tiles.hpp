@@ -57,6 +57,12 @@ __device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t
 
 typedef uint32_t tile_quad __attribute__((ext_vector_type(4)));
 
+// BSLS_TILE_KO (timing knock-outs of the dealt walk, never in the product
+// build): 1 = plain LDS add instead of ds_add_f64, 2 = no LDS accumulation
+#ifndef BSLS_TILE_KO
+#define BSLS_TILE_KO 0
+#endif
+
 // the dealt walk's entry stream: non-temporal loads when the image is larger
 // than the Infinity Cache (layout flag BSLS_TILE_NT: the stream would only
 // evict the gathered vector; C5 on one GPU K1 368 -> 357, K2 505 -> 492 us),
@@ -148,6 +154,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
         bring[k] = (k < nq) ? Bq[(int64_t)k * 16] : int4{0, 0, 0, 0};
     }
     double v[4], vn[4], a[4], an[4];
+    double ko = 0.0;
     auto gat = [&](const tile_quad &u, const int4 &b, int64_t q, double (&o)[4], double (&w)[4]) {
         o[0] = xb[b.x + (u[0] & 0xFFFFu)];
         o[1] = xb[b.y + (u[1] & 0xFFFFu)];
@@ -176,7 +183,13 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
                     if (MODE == 0) term = v[j];
                     else if (MODE == 1) term = a[j] * v[j];
                     else term = rcol[lr] * v[j];
+#if BSLS_TILE_KO == 1
+                    rows[lr] += term;                 // (knock-out: racy plain add)
+#elif BSLS_TILE_KO == 2
+                    ko += term;                       // (knock-out: no LDS)
+#else
                     atomicAdd(&rows[lr], term);
+#endif
                 }
             }
 #pragma unroll
@@ -186,6 +199,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
             }
         }
     }
+    if (BSLS_TILE_KO == 2) rows[threadIdx.x] += ko;
 }
 
 // the walk of either layout

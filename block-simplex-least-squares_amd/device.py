@@ -283,8 +283,9 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
     The environment variable `env` ("H,groups") overrides it."""
     plan = os.environ.get(env) if env else None
     if plan:
-        H, G = (int(v) for v in plan.split(','))
-        return H, G, (1 if G > 8 else 0)
+        v = [int(a) for a in plan.split(',')]
+        H, G = v[0], v[1]
+        return H, G, (v[2] if len(v) > 2 else (1 if G > 8 else 0))
     if layout == 1:
         # dealt image: one workgroup per CU at most, as few column groups as
         # fill the CUs (each extra group costs m partial sums written and read
