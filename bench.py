@@ -12,8 +12,8 @@ routes / 500k blocks / 1M links / 160M nnz, the same for every N
 (synthetic.make_partitioned), column-sharded by whole blocks over the N ranks
 (one process per GPU, torchrun); strong scaling: value = iterations/s of the
 whole job, the 1-GPU run being the N = 1 point.  Per iteration one RCCL
-all-reduce of the four BB sums and one of the residual r (8 MB), the latter
-in --parts row parts pipelined behind K1 (distributed.ShardedBB).
+all-reduce of the four BB sums and one of the residual r (8 MB) after K1
+(distributed.ShardedBB; --parts > 1 pipelines it behind K1 by row parts).
 At N = 1 the line also carries "c3": the BASELINE metric's 1M-route problem
 (C3: 1M routes / 50k blocks / 100k links / 16M nnz) with its kernels and
 roofline, the C2 projection, the x-space BB, mirror descent and the standalone
@@ -392,14 +392,17 @@ def log(msg):
 T0 = time.perf_counter()
 
 
-def build_problem(name, world, rank, dist):
+def build_problem(name, world, rank, dist, shard_of=None):
     """The rank's column shard of workload `name` and the full b (SURVEY §8(d)
-    recipe, 2 % multiplicative noise so the exact-zero exit never fires)."""
+    recipe, 2 % multiplicative noise so the exact-zero exit never fires).
+    shard_of (rehearsal on one GPU): rank 0's shard of that many ranks, b its
+    own A x (the timing does not depend on b)."""
     import torch
     from synthetic import make_partitioned, make_shard, add_noise, CONFIGS, SEED
     c = CONFIGS[name]
     if name == 'C5':
-        sh = make_partitioned(c['n'], c['p'], c['m'], c['per_col'], rank=rank, world=world)
+        sh = make_partitioned(c['n'], c['p'], c['m'], c['per_col'], rank=rank,
+                              world=shard_of or world)
     else:
         if world != 1:
             raise SystemExit('workload %s is a single-GPU configuration' % name)
@@ -413,13 +416,15 @@ def build_problem(name, world, rank, dist):
     return sh, b
 
 
-def build_engine(sh, b, world, dist, parts):
+def build_engine(sh, b, world, dist, parts, sharded=False):
     """(engine, run(first, count)) for one rank: the fused single-GPU loop, or
-    the column-sharded stages with the RCCL all-reduces (distributed.ShardedBB)."""
+    the column-sharded stages with the RCCL all-reduces (distributed.ShardedBB;
+    `sharded` forces them at world 1 -- the per-rank host and launch path of
+    an N-GPU run, rehearsed on one GPU)."""
     import torch
     from device import BBEngine
     opts = {'max_iter': 10 ** 12, 'opt_tol': 1e-30}
-    if world == 1:
+    if world == 1 and not sharded:
         eng = BBEngine(sh['A'], b, sh['block_sizes'], options=opts, early_exit=False,
                        AT=sh['AT'], colv=sh.get('colv'))
         eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
@@ -528,11 +533,17 @@ def main():
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--workload', default='C5', choices=['C5', 'C3'])
-    ap.add_argument('--parts', type=int, default=4,
-                    help='row parts of the pipelined residual all-reduce (N > 1)')
+    ap.add_argument('--parts', type=int, default=1,
+                    help='row parts of the pipelined residual all-reduce (N > 1); 1 = one K1 '
+                         'launch then one all-reduce: rehearsed on one GPU (--rehearse-shard 8), '
+                         '4 parts cost 457 us per iteration against 207 for 1 -- a part of K1 '
+                         'is a quarter of the grid, the GPU is not filled')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-extras', action='store_true', help='skip the C3 / C2 / x-space / MD legs')
     ap.add_argument('--profile-iters', type=int, default=20)
+    ap.add_argument('--rehearse-shard', type=int, default=0,
+                    help='one GPU, one process: time rank 0 of an N-way C5 partition through '
+                         'the sharded (RCCL) driver -- per-rank cost without the fabric')
     args = ap.parse_args()
 
     import torch
@@ -545,8 +556,12 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or args.rehearse_shard:
         import torch.distributed as dist
+        if world == 1:
+            for k, v in (('MASTER_ADDR', '127.0.0.1'), ('MASTER_PORT', '29533'), ('RANK', '0'),
+                         ('WORLD_SIZE', '1')):
+                os.environ.setdefault(k, v)
         backend = os.environ.get('BSLS_DIST_BACKEND', 'nccl')
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
@@ -554,10 +569,10 @@ def main():
             dist.init_process_group(backend)
 
     wl = args.workload
-    sh, b = build_problem(wl, world, rank, dist)
+    sh, b = build_problem(wl, world, rank, dist, shard_of=args.rehearse_shard or None)
     log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
         % (wl, rank, world, sh['n'], sh['p'], sh['m'], sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
-    eng, run = build_engine(sh, b, world, dist, args.parts)
+    eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(args.rehearse_shard))
     log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
     el = time_run(run, args.steps, args.warmup, dist)
     it_s = args.steps / el
@@ -599,7 +614,11 @@ def main():
             'kernels': kern, 'finite': finite,
         }
     # --- N = 1 extras: the BASELINE metric's C3 problem and the other legs ---------
-    if world == 1 and not args.no_extras:
+    if args.rehearse_shard and out is not None:
+        out['config']['rehearsal'] = ('rank 0 of a %d-way C5 partition on one GPU through the '
+                                      'sharded driver (RCCL with one rank: no fabric)'
+                                      % args.rehearse_shard)
+    if world == 1 and not args.no_extras and not args.rehearse_shard:
         del eng, run
         torch.cuda.empty_cache()
         sh3, b3 = build_problem('C3', 1, 0, None)
