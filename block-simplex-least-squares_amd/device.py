@@ -287,24 +287,30 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
         H, G = v[0], v[1]
         return H, G, (v[2] if len(v) > 2 else (1 if G > 8 else 0))
     if layout == 1:
-        # dealt image: one workgroup per CU at most, as few column groups as
-        # fill the CUs (each extra group costs m partial sums written and read
-        # back); every workgroup sweeps its group's columns in order, so the
-        # workgroups of an XCD share the sweep front in L2 whatever the slice
-        # width.  Measured on C5 (tools/stage_time.py): K1 G = 4 x 64 row blocks
-        # 374 us (G = 8: 400, 16: 526, 32: 812; G = 2 / 1 leave CUs idle: 698 /
-        # 1303); K2 (the routes' rows: partial sums of n rows are dear) one
-        # group of 1024 row blocks 503 us (2: 611, 4: 775).
+        # dealt image: one round of workgroups (one per CU); K1 with as many
+        # column groups, up to 8, as keep its row blocks within the LDS -- a
+        # narrower group puts more of a tile's entries on each gathered line,
+        # past 8 the last-arriving workgroups' group sums make a tail.
+        # Measured (tools/stage_time.py): C3 K1 G x row blocks 8 x 32 34.0 us
+        # (4 x 64: 36.5, 16 x 16: 51.8, 2 x 128: 46.9, 8 x 64: 46.6, 32 x 8:
+        # 126); C5 K1 4 x 64 374 us (the most the LDS allows in one round;
+        # 8 x 64: 400, 16: 526, 32: 812; 2 / 1 groups leave CUs idle: 698 /
+        # 1303).  K2 (the routes' rows: partial sums of n rows are dear) one
+        # group: C3 256 row blocks 36.9 us (128: 48.9, 500: 47.0), C5 512
+        # row blocks 370 us (before the row-sum scaling: 2 groups 611, 4: 775
+        # against 503).
         mult = 2 if colv_lds else 1
         hmax = _native.TILE_LDS_BYTES // (8 * mult) - 1 - halo
-        nmin = -(-rows // hmax)
         G = 1
-        while not halo and 2 * G * nmin <= cus and 2 * G <= cols:
-            G *= 2
+        if not halo:
+            G = 8
+            while G > 1 and (-(-rows * G // cus) > hmax or G > cols):
+                G //= 2
+        nmin = -(-rows // hmax)
         nrb = max(nmin, cus // G)
         nrb = -(-(nrb * G) // cus) * cus // G if nrb * G > cus else nrb
         H = max(64, -(-rows // nrb))
-        return int(H), int(G), (1 if G > 8 and G % 8 == 0 else 0)
+        return int(H), int(G), 0
     if l2_slice is None:
         # measured on the C5 shard (tools/stage_time.py): K1 fastest with
         # 2.5-MB slices of x (4 groups: 112 us, 8: 148 us), K2 with the whole
@@ -328,17 +334,22 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
     return int(H), int(G), int(order)
 
 
-def spmv_format(M, fmt=None):
-    """'panels' or 'tiles' for the fused SpMV over matrix M (rows x cols):
-    tiles when a panel chunk (BSLS_PANEL_CHUNK columns) holds under one entry
-    per row on average -- the sparse row blocks of C5 (0.3), where the panel
-    walk idles (csrc/tiles.hpp); panels for C3 (3.2).  fmt / BSLS_SPMV_FORMAT
-    force one."""
+def spmv_format(M, fmt=None, dealt=True):
+    """'panels' or 'tiles' for the fused SpMV over matrix M (rows x cols).
+    With the dealt tile layout available (`dealt`, i.e. not a deterministic
+    engine) always tiles: measured on C3 (tools/stage_time.py --fmt) K1 34.0
+    against the panels' 43.0 us, K2 36.9 against 41.4; on C5 the panels idle
+    (0.3 entries per row per chunk).  Deterministic engines keep the panels
+    while a panel chunk (BSLS_PANEL_CHUNK columns) holds at least one entry
+    per row on average (C3: 3.2), the thread-stream tiles below that
+    (csrc/tiles.hpp).  fmt / BSLS_SPMV_FORMAT force one."""
     fmt = fmt or os.environ.get('BSLS_SPMV_FORMAT') or 'auto'
     if fmt != 'auto':
         if fmt not in ('panels', 'tiles'):
             raise ValueError('unknown SpMV format %r' % fmt)
         return fmt
+    if dealt:
+        return 'tiles'
     R, C = M.shape
     lam = (M.nnz / max(R, 1)) * min(_native.PANEL_CHUNK, C) / max(C, 1)
     return 'tiles' if lam < 1.0 else 'panels'
@@ -657,15 +668,6 @@ class BBEngine:
         elif general:
             colv = None
         self.scaled = colv is not None
-        # per matrix: panels (dense row blocks, C3) or streamed tiles (C5)
-        self.fmt_A, self.fmt_AT = spmv_format(A, fmt), spmv_format(AT, fmt)
-        self.A_pan = self.AT_pan = self.A_til = self.AT_til = None
-        if self.fmt_A == 'panels':
-            prow, groups = k1_plan(self.m)
-            try:
-                self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
-            except PanelOverflow:
-                self.fmt_A = 'tiles'      # dense rows: the tiles have no such limit
         # tile layouts (K1, K2): the dealt images (column-sorted gathers, LDS
         # atomic sums: the same sums to rounding, not run-to-run bit-identical;
         # C5 K1 1334 -> 374 us, K2 984 -> 503 us) unless `deterministic`, which
@@ -676,6 +678,16 @@ class BBEngine:
             tile_layouts = (tuple(int(v) for v in env.split(',')) if env
                             else ((0, 0) if deterministic else (1, 1)))
         self.tile_layouts = tile_layouts
+        # per matrix: panels or streamed tiles (spmv_format)
+        self.fmt_A = spmv_format(A, fmt, dealt=tile_layouts[0] == 1)
+        self.fmt_AT = spmv_format(AT, fmt, dealt=tile_layouts[1] == 1)
+        self.A_pan = self.AT_pan = self.A_til = self.AT_til = None
+        if self.fmt_A == 'panels':
+            prow, groups = k1_plan(self.m)
+            try:
+                self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
+            except PanelOverflow:
+                self.fmt_A = 'tiles'      # dense rows: the tiles have no such limit
         if self.fmt_A == 'tiles':
             self.A_til = DeviceTiles(A, 0, values=not self.scaled, plan=tile_plans[0],
                                      layout=tile_layouts[0])

@@ -2,7 +2,9 @@
 100k links, 16M nonzeros), the configuration bench.py measures.  Needs an
 MI355X.
 
-* K2 (g = N'A'r) bit-identical to SciPy on the whole problem;
+* K2 (g = N'A'r) bit-identical to SciPy on the whole problem with the
+  deterministic engine (panels, every row in CSR order), within 1e-12 with the
+  default dealt tiles (LDS atomic sums);
 * K1 (r = A x + target) within 1e-12 relative of SciPy;
 * K3 (PAVA + clip + N z) bit-identical to the oracle on all 950k z entries;
 * BB iterates after 1 and 3 iterations within 1e-6 relative of the oracle's
@@ -29,19 +31,29 @@ def c3(cuda):
     b = add_noise(sh['Ax'], 0.02, seed=SEED)
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 3, 'opt_tol': 1e-30},
                    AT=sh['AT'])
+    assert eng.fmt_A == eng.fmt_AT == 'tiles' and eng.tile_layouts == (1, 1)
     return sh, b, eng
 
 
-def test_c3_k2_bit_exact(c3, orc):
+@pytest.mark.parametrize('deterministic', [True, False])
+def test_c3_k2_vs_scipy(c3, orc, deterministic):
     import torch
+    from device import BBEngine
     sh, b, eng = c3
+    if deterministic:
+        eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 3, 'opt_tol': 1e-30},
+                       AT=sh['AT'], deterministic=True)
+        assert eng.fmt_A == eng.fmt_AT == 'panels'
     r = np.random.RandomState(5).randn(eng.m)
     eng.r.copy_(torch.from_numpy(r))
     eng.stage(3, 0)
     got = eng.g[0][:eng.nz].cpu().numpy()
     N = orc.block_sizes_to_N(sh['block_sizes'])
     want = N.T.tocsr().dot(sh['AT'].dot(r))
-    assert np.array_equal(got.view(np.int64), want.view(np.int64))
+    if deterministic:
+        assert np.array_equal(got.view(np.int64), want.view(np.int64))
+    else:
+        assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
 
 
 def test_c3_k1_residual(c3):
