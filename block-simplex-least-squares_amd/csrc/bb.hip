@@ -210,6 +210,46 @@ __global__ __launch_bounds__(1024) void bb_k1(bsls_bb_problem P, int64_t iter, u
     k1_finish<ADD, REDUCE>(P, iter, ITER, rb, nrb, r0, r1, G, nullptr, part, ticket, lds);
 }
 
+// BSLS_K1_SPLIT (default 1): a K1 tile launch with several column groups ends
+// once its partials are stored, and bb_k1_sum finishes the rows in a launch of
+// its own -- the kernel boundary replaces the in-kernel hand-off (partials
+// drained, a ticket per row block, the last arriver's loads, a second ticket
+// for ||r||^2: a chain of dependent round trips that took ~half of C3's K1)
+#ifndef BSLS_K1_SPLIT
+#define BSLS_K1_SPLIT 1
+#endif
+
+// K1's finish as its own launch (rows [r0, r1), one thread per row): r = the G
+// partials in group order (+ target, ADD), ||r||^2 and f by the last block
+// (REDUCE), as k1_finish.
+template <bool ITER, bool ADD, bool REDUCE>
+__global__ __launch_bounds__(256) void bb_k1_sum(bsls_bb_problem P, int64_t iter, int64_t G,
+                                                 int64_t r0, int64_t r1, double *part,
+                                                 unsigned *ticket) {
+    __shared__ double red[4];
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    const int64_t row = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double sq[1] = {0.0};
+    if (row < r1) {
+        double v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = (c < G) ? P.rpart[c * P.m + row] : 0.0;
+        double o = v[0];
+#pragma unroll
+        for (int c = 1; c < 8; ++c)
+            if (c < G) o += v[c];
+        for (int64_t c = 8; c < G; ++c) o += P.rpart[c * P.m + row];
+        if (ADD) o += P.target[row];
+        P.r[row] = o;
+        sq[0] = o * o;
+    }
+    if (!REDUCE) return;
+    block_sum<1>(sq, red);
+    double tot[1];
+    if (last_block_sum<1>(sq, part, ticket, tot, red) && threadIdx.x == 0)
+        bb_record_f(P, iter, tot[0], ITER);
+}
+
 // K1 on a tile image (tiles.hpp): workgroup (rb, g) sums its rows over group
 // g's columns of x in LDS; with one group it finishes the block itself,
 // otherwise it publishes its partials (rpart, sc1) and the last of the block's
@@ -235,6 +275,12 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
     if (G == 1) {
         k1_finish<ADD, REDUCE>(P, iter, ITER, rb, (unsigned)T.nrb, r0, r1, 1, lds, part, ticket,
                                red);
+        return;
+    }
+    if (BSLS_K1_SPLIT) {
+        // the partials only; bb_k1_sum (next in the stream) finishes the rows
+        for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+            P.rpart[g * P.m + row] = lds[row - r0];
         return;
     }
     for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
@@ -289,12 +335,10 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     __syncthreads();
     const int64_t G = T.ngroups;
     bool fin = true;
-    if (MODE == 3 && G == 1) {
-        // dealt image, one group: w_i = colv_i * (sum of r over row i), one
-        // product per row (the sums' order is not fixed anyway)
-        for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x) rows[i] = P.colv[i0 + i] * rows[i];
-        __syncthreads();
-    }
+    // dealt image, one group (MODE 3): w_i = colv_i * (sum of r over row i),
+    // one product per row (the sums' order is not fixed anyway), formed in the
+    // epilogue below; several groups: by the finishing workgroup
+    const bool scale_epi = MODE == 3 && G == 1;
     if (G > 1) {
         double *wp = P.wpart + (g * T.nrb + rb) * (T.H + 1);
         for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x)
@@ -324,19 +368,50 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     }
     double sums[4] = {0.0, 0.0, 0.0, 0.0};
     if (fin) {
+        // K2E rows per thread per batch: every z index, then every operand of
+        // the batch in flight at once (two round trips per batch instead of
+        // two per row: C5's 19 rows per thread made the epilogue ~90 us)
         const int64_t iend = (nloc < T.H) ? nloc : T.H;
-        for (int64_t i = threadIdx.x; i < iend; i += blockDim.x) {
-            const int32_t j = P.xz[i0 + i];
-            if (j < 0) continue;   // a block's last x entry (also the matrix's last row)
-            const double gv = rows[i] - rows[i + 1];
-            gout[j] = gv;
-            if (ITER) {
-                const double dg = gv - gp[j];
-                const double dz = dzv[j];
-                sums[0] += dg;
-                sums[1] += dz * dg;
-                sums[2] += dg * dg;
-                sums[3] += gv * gv;
+        constexpr int K2E = 8;
+        for (int64_t ib = threadIdx.x; ib < iend; ib += K2E * blockDim.x) {
+            int32_t jq[K2E];
+            double ca[K2E], cb[K2E], gq[K2E], dq[K2E];
+#pragma unroll
+            for (int q = 0; q < K2E; ++q) {
+                const int64_t i = ib + (int64_t)q * blockDim.x;
+                // (j < 0: a block's last x entry, also the matrix's last row)
+                jq[q] = (i < iend) ? P.xz[i0 + i] : -1;
+                ca[q] = cb[q] = 1.0;
+                if (scale_epi && i < iend) {
+                    ca[q] = P.colv[i0 + i];
+                    cb[q] = (i + 1 < nloc) ? P.colv[i0 + i + 1] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < K2E; ++q) {
+                gq[q] = dq[q] = 0.0;
+                if (ITER && jq[q] >= 0) {
+                    gq[q] = gp[jq[q]];
+                    dq[q] = dzv[jq[q]];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < K2E; ++q) {
+                const int64_t i = ib + (int64_t)q * blockDim.x;
+                const int32_t j = jq[q];
+                if (j < 0) continue;
+                const double wa = scale_epi ? ca[q] * rows[i] : rows[i];
+                const double wb = scale_epi ? cb[q] * rows[i + 1] : rows[i + 1];
+                const double gv = wa - wb;
+                gout[j] = gv;
+                if (ITER) {
+                    const double dg = gv - gq[q];
+                    const double dz = dq[q];
+                    sums[0] += dg;
+                    sums[1] += dz * dg;
+                    sums[2] += dg * dg;
+                    sums[3] += gv * gv;
+                }
             }
         }
     }
@@ -725,6 +800,11 @@ static void launch_k1t_mode(const bsls_bb_problem &P, int64_t iter, const BBWork
     bb_k1t<MODE, ITER, ADD, REDUCE><<<(int)((rb1 - rb0) * P.At.ngroups), BSLS_TILE_THREADS,
                                       tile_lds_doubles(P.At, false) * 8, st>>>(P, iter, w.tkrb,
                                                                                 w.p1, w.tk1, rb0);
+    if (BSLS_K1_SPLIT && P.At.ngroups > 1) {
+        const int64_t r0 = rb0 * P.At.H, r1 = (rb1 * P.At.H < P.m) ? rb1 * P.At.H : P.m;
+        bb_k1_sum<ITER, ADD, REDUCE><<<grid_for(r1 - r0, 256), 256, 0, st>>>(
+            P, iter, P.At.ngroups, r0, r1, w.pf, w.tkf);
+    }
 }
 
 template <bool ADD, bool REDUCE, bool ITER>

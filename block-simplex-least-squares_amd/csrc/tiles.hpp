@@ -58,7 +58,8 @@ __device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t
 typedef uint32_t tile_quad __attribute__((ext_vector_type(4)));
 
 // BSLS_TILE_KO (timing knock-outs of the dealt walk, never in the product
-// build): 1 = plain LDS add instead of ds_add_f64, 2 = no LDS accumulation
+// build): 1 = plain LDS add instead of ds_add_f64, 2 = no LDS accumulation,
+// 3 = no walk at all (what is left: the LDS clear, the finish, the tail)
 #ifndef BSLS_TILE_KO
 #define BSLS_TILE_KO 0
 #endif
@@ -133,11 +134,19 @@ __device__ __forceinline__ void tile_walk(const bsls_tiles &T, int64_t rb, int64
 // Layout 1 (dealt, include/bsls_hip.h): wave w walks its instructions of tile
 // (rb, g) quad-step by quad-step -- one 16-B entry load (4 slots) and one
 // scalar 16-B base load per step, loaded P steps ahead, the gathers of step
-// s + 1 issued before the LDS atomic adds of step s.  MODE as tile_walk.
-template <int MODE, bool NT, int P = 4>
+// s + D issued before the LDS atomic adds of step s.  MODE as tile_walk.
+#ifndef BSLS_TILE_P
+#define BSLS_TILE_P 4
+#endif
+#ifndef BSLS_TILE_D
+#define BSLS_TILE_D 1
+#endif
+template <int MODE, bool NT, int P = BSLS_TILE_P, int D = BSLS_TILE_D>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
                                                 const double *rcol) {
+    static_assert(D >= 1 && D < P, "gathers run ahead of the entry loads");
+    if (BSLS_TILE_KO == 3) return;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int64_t t = rb * T.ngroups + g;
@@ -153,7 +162,8 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
         ring[k] = (k < nq) ? tq_load<NT>(Q + (int64_t)k * 1024) : tile_quad{0, 0, 0, 0};
         bring[k] = (k < nq) ? Bq[(int64_t)k * 16] : int4{0, 0, 0, 0};
     }
-    double v[4], vn[4], a[4], an[4];
+    // v[d] / a[d]: the gathered values (and stored values) of step s + d
+    double v[D + 1][4], a[D + 1][4];
     double ko = 0.0;
     auto gat = [&](const tile_quad &u, const int4 &b, int64_t q, double (&o)[4], double (&w)[4]) {
         o[0] = xb[b.x + (u[0] & 0xFFFFu)];
@@ -165,12 +175,14 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
             for (int j = 0; j < 4; ++j) w[j] = V[q * 4096 + j];
         }
     };
-    gat(ring[0], bring[0], 0, v, a);
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (d < nq) gat(ring[d], bring[d], d, v[d], a[d]);
     for (int64_t q = 0; q < nq; q += P) {
 #pragma unroll
         for (int k = 0; k < P; ++k) {
             const tile_quad cur = ring[k];
-            if (q + k + 1 < nq) gat(ring[(k + 1) % P], bring[(k + 1) % P], q + k + 1, vn, an);
+            if (q + k + D < nq) gat(ring[(k + D) % P], bring[(k + D) % P], q + k + D, v[D], a[D]);
             if (q + k + P < nq) {
                 ring[k] = tq_load<NT>(Q + (q + k + P) * 1024);
                 bring[k] = Bq[(q + k + P) * 16];
@@ -180,9 +192,9 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
                 for (int j = 0; j < 4; ++j) {
                     const int lr = (int)(cur[j] >> 16);
                     double term;
-                    if (MODE == 0) term = v[j];
-                    else if (MODE == 1) term = a[j] * v[j];
-                    else term = rcol[lr] * v[j];
+                    if (MODE == 0) term = v[0][j];
+                    else if (MODE == 1) term = a[0][j] * v[0][j];
+                    else term = rcol[lr] * v[0][j];
 #if BSLS_TILE_KO == 1
                     rows[lr] += term;                 // (knock-out: racy plain add)
 #elif BSLS_TILE_KO == 2
@@ -193,10 +205,12 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                v[j] = vn[j];
-                if (MODE == 1) a[j] = an[j];
-            }
+            for (int d = 0; d < D; ++d)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v[d][j] = v[d + 1][j];
+                    if (MODE == 1) a[d][j] = a[d + 1][j];
+                }
         }
     }
     if (BSLS_TILE_KO == 2) rows[threadIdx.x] += ko;
