@@ -588,18 +588,15 @@ __device__ __forceinline__ void wt_store_f64(const __amdgpu_buffer_rsrc_t &rs, i
         __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, v), rs, off, 0, 16);
 }
 
-#ifndef BSLS_K3_PPW
-#define BSLS_K3_PPW 1
-#endif
-constexpr int K3_PPW = BSLS_K3_PPW;   // packs per wave
 #ifndef BSLS_DZ_PLAIN
 #define BSLS_DZ_PLAIN 0   // 1: dz through an ordinary store (A/B variant)
 #endif
 
 // Each wave takes K3_PPW packs (w, w + W, ...; W = waves in the grid) and
 // issues every load of all of them -- metadata, then z, g and the column
-// scales -- before the first PAVA, so the round trips of the second pack
-// overlap the first one's passes and the grid is resident in one round.
+// scales -- before the first PAVA.  MERGE (K3_PPW = 2): the two packs' PAVA
+// share the wave after their first passes (pava_v1_wave_pair).
+template <int K3_PPW, bool MERGE>
 __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
                                              const double *__restrict__ zc,
                                              const double *__restrict__ g,
@@ -613,7 +610,7 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
     const int64_t nw = (int64_t)gridDim.x * 4;
     const int64_t w0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);   // wave-uniform
     __shared__ double pv_y[4][64];
-    __shared__ int pv_p[4][64];
+    __shared__ int pv_p[4][128];
     __shared__ int pv_c[4][65];
     int64_t z0[K3_PPW], b0[K3_PPW];
     int L[K3_PPW];
@@ -646,6 +643,22 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
     }
     double t;
     if (!bb_step_t(P, iter, sc, t)) return;
+    double yv[K3_PPW];
+#pragma unroll
+    for (int q = 0; q < K3_PPW; ++q)   // x_next = x - t g (BB.py:29)
+        yv[q] = (l < L[q] && L[q] <= WAVE) ? zv[q] - t * gv[q] : 0.0;
+    if (BSLS_K3_KO != 1) {
+        if (MERGE && K3_PPW == 2 && L[0] > 0 && L[0] <= WAVE && L[K3_PPW - 1] > 0 &&
+            L[K3_PPW - 1] <= WAVE) {
+            pava_v1_wave_pair(yv[0], L[0], B[0], yv[K3_PPW - 1], L[K3_PPW - 1], B[K3_PPW - 1],
+                              pv_y[wv], pv_p[wv], pv_c[wv]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < K3_PPW; ++q)
+                if (L[q] > 0 && L[q] <= WAVE)
+                    pava_v1_wave_c(yv[q], L[q], B[q], pv_y[wv], pv_p[wv], pv_c[wv]);
+        }
+    }
 #pragma unroll
     for (int q = 0; q < K3_PPW; ++q) {
         if (L[q] == 0) break;
@@ -654,9 +667,7 @@ __global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
             const bool bstart = (B[q] >> l) & 1ull;
             const int bl = __popcll(B[q] & mask_le(l)) - 1;   // block within the pack
             const bool bend = (l == L[q] - 1) || (l < 63 && ((B[q] >> (l + 1)) & 1ull));
-            double yq = act ? zv[q] - t * gv[q] : 0.0;  // x_next = x - t g (BB.py:29)
-            if (BSLS_K3_KO != 1) pava_v1_wave_c(yq, L[q], B[q], pv_y[wv], pv_p[wv], pv_c[wv]);
-            const double v = clip01(yq);
+            const double v = clip01(yv[q]);
             const double vprev = shfl_d(v, l > 0 ? l - 1 : 0);
             const int nb = __popcll(B[q]);
             const __amdgpu_buffer_rsrc_t rz =
@@ -852,9 +863,23 @@ static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
     }
 }
 
+// Two packs per wave sharing their passes after the first
+// (pava_v1_wave_pair) pay where the grid runs many rounds of resident waves:
+// C5 (172k packs) K3 153 -> 141 us; C3 (16.7k packs, two rounds of 8 waves
+// per SIMD) 18.8 -> 20.6 us, the longer wave outlasting its rounds.  So from
+// 64k packs (8 rounds); BSLS_K3_MERGE (environment, read per launch: tests
+// switch it) forces 0 / 1.
+static bool k3_merge(const bsls_bb_problem &P) {
+    const char *e = getenv("BSLS_K3_MERGE");
+    return e ? atoi(e) != 0 : P.npacks >= 65536;
+}
+
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
                       double *zn, const BBWork &w, hipStream_t st) {
-    bb_k3<<<grid_for(P.npacks, 4 * K3_PPW), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+    if (k3_merge(P))
+        bb_k3<2, true><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+    else
+        bb_k3<1, false><<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
     if (P.long_packs && P.nlong > 0)
         bb_k3_long<<<(int)P.nlong, LONG_T, 0, st>>>(P, iter, zc, g, zn, w.dz);
 }

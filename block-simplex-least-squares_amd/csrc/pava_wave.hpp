@@ -123,79 +123,154 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Run state of the compacted form: lane t < nh holds run t (value Y, length
+// W, block-start flag BS, first element O).
+struct WaveRuns {
+    double Y;
+    int W, BS, O, nh;
+};
+
+__device__ __forceinline__ WaveRuns wave_runs(double y, int L, uint64_t B, int obase) {
+    const int t = lane_id();
+    return WaveRuns{y, 1, (int)((B >> t) & 1ull), t + obase, L};
+}
+
+// One reference pass over the runs: false (state unchanged) when no chain
+// pools, else the pooled chains merged and the survivors packed into lanes
+// 0 .. nh-1.  ys / ps / cst: this wave's 64 doubles / 64 ints / 65 ints of LDS.
+__device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int *cst) {
+    const int t = lane_id();
+    const bool act = t < s.nh;
+    const double yp = dpp_shr1_d(s.Y);
+    const bool cs = act && (s.BS || !(s.Y <= yp));     // lane 0 is always a block start
+    const uint64_t CS = __ballot(cs);
+    // chain c of this lane (lanes >= nh: the last chain, unused); the
+    // table holds every chain's first run, then nh
+    const int c = mbcnt64(CS) - (cs ? 0 : 1);
+    if (cs) cst[c] = t;
+    if (t == 0) cst[__popcll(CS)] = s.nh;
+    const int mycs = cst[c], nxt = cst[c + 1];
+    const int last = nxt - 1;                      // this chain's last run
+    const double yfirst = shfl_d(s.Y, mycs);
+    const double ylast = shfl_d(s.Y, last);
+    // the chain pools iff its first and last values differ (the reference's
+    // y[i] != y[j]); every member sees both
+    const bool inpool = act && (yfirst != ylast);
+    const bool pool = cs && inpool;
+    if (!__ballot(pool)) return false;
+    const int depth = t - mycs;
+    const double pr = s.Y * (double)s.W;
+    double num = 0.0 + pr;
+    int den = s.W;
+    // k = 1 .. the deepest pooled member (a ballot per step instead of a
+    // six-round shuffle max up front: 2-4 steps are typical)
+    for (int k = 1; __ballot(inpool && depth >= k); ++k) {
+        const double np = dpp_shr1_d(num);
+        const int dp = dpp_shr1_i(den);
+        const bool upd = inpool && depth == k;
+        num = upd ? np + pr : num;
+        den = upd ? dp + s.W : den;
+    }
+    const double tn = shfl_d(num, last);
+    const int td = shfl_i(den, last);
+    if (pool) {
+        s.Y = tn / (double)td;
+        s.W = td;
+    }
+    // pack the surviving runs into lanes 0 .. nh-1
+    const bool surv = act && !(inpool && depth > 0);
+    const uint64_t S = __ballot(surv);
+    if (surv) {
+        const int idx = mbcnt64(S);
+        ys[idx] = s.Y;
+        ps[idx] = s.W | (s.BS << 8) | (s.O << 9);
+    }
+    s.nh = __popcll(S);
+    if (t < s.nh) {
+        s.Y = ys[t];
+        const int pk = ps[t];
+        s.W = pk & 255;
+        s.BS = (pk >> 8) & 1;
+        s.O = pk >> 9;
+    }
+    return true;
+}
+
+// expand: element e (< L) takes the value of the last run starting at or
+// before it (runs with first elements O - obase in [0, L))
+__device__ __forceinline__ double wave_expand(const WaveRuns &s, double y, int L, int obase,
+                                              int *ps) {
+    const int t = lane_id();
+    ps[t] = 0;
+    if (t < s.nh) ps[s.O - obase] = 1;
+    const uint64_t RS = __ballot(t < L && ps[t] != 0);
+    const int idx = mbcnt64(RS) + (int)((RS >> t) & 1ull) - 1;
+    const double v = shfl_d(s.Y, idx < 0 ? 0 : idx);
+    return (t < L) ? v : y;
+}
+
 // y: this lane's element (lanes < L); B: block starts (bit 0 set).  ys / ps /
 // cst: this wave's 64 doubles / 64 ints / 65 ints of LDS.  On return y = the
 // expanded fit.  (The pass is VALU-bound: chain bounds come from a chain-start
 // table in LDS, not from 64-bit mask searches.)
 __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, double *ys,
                                                int *ps, int *cst) {
-    const int t = lane_id();
-    double Y = y;
-    int W = 1, BS = (int)((B >> t) & 1ull), O = t;
-    int nh = L;
+    WaveRuns s = wave_runs(y, L, B, 0);
     const int maxpass = BSLS_K3_KO >= 2 ? BSLS_K3_KO - 2 : L;
-    for (int pass = 0; pass <= maxpass; ++pass) {
-        const bool act = t < nh;
-        const double yp = dpp_shr1_d(Y);
-        const bool cs = act && (BS || !(Y <= yp));     // lane 0 is always a block start
-        const uint64_t CS = __ballot(cs);
-        // chain c of this lane (lanes >= nh: the last chain, unused); the
-        // table holds every chain's first run, then nh
-        const int c = mbcnt64(CS) - (cs ? 0 : 1);
-        if (cs) cst[c] = t;
-        if (t == 0) cst[__popcll(CS)] = nh;
-        const int mycs = cst[c], nxt = cst[c + 1];
-        const int last = nxt - 1;                      // this chain's last run
-        const double yfirst = shfl_d(Y, mycs);
-        const double ylast = shfl_d(Y, last);
-        // the chain pools iff its first and last values differ (the reference's
-        // y[i] != y[j]); every member sees both
-        const bool inpool = act && (yfirst != ylast);
-        const bool pool = cs && inpool;
-        if (!__ballot(pool)) break;
-        const int depth = t - mycs;
-        const double pr = Y * (double)W;
-        double num = 0.0 + pr;
-        int den = W;
-        // k = 1 .. the deepest pooled member (a ballot per step instead of a
-        // six-round shuffle max up front: 2-4 steps are typical)
-        for (int k = 1; __ballot(inpool && depth >= k); ++k) {
-            const double np = dpp_shr1_d(num);
-            const int dp = dpp_shr1_i(den);
-            const bool upd = inpool && depth == k;
-            num = upd ? np + pr : num;
-            den = upd ? dp + W : den;
+    for (int pass = 0; pass <= maxpass; ++pass)
+        if (!wave_pass(s, ys, ps, cst)) break;
+    y = wave_expand(s, y, L, 0, ps);
+}
+
+// Two packs in one wave (La, Lb <= 64 elements, one each per lane in ya /
+// yb): the first pass of each on its own, then -- when their surviving runs
+// fit one wave (C3-like inputs: ~30 of ~55 runs survive the first pass) --
+// both run lists in one (b's after a's; chains never cross a block start, and
+// a pack starts at one) for the remaining passes, which then cost one pass
+// for the two packs.  Each pack's passes and roundings are the reference's:
+// a pack that stopped pooling is left unchanged by the passes the other still
+// needs.  ps: 128 ints.
+__device__ __forceinline__ void pava_v1_wave_pair(double &ya, int La, uint64_t Ba, double &yb,
+                                                  int Lb, uint64_t Bb, double *ys, int *ps,
+                                                  int *cst) {
+    const int t = lane_id();
+    WaveRuns a = wave_runs(ya, La, Ba, 0), b = wave_runs(yb, Lb, Bb, 64);
+    bool pa = wave_pass(a, ys, ps, cst);
+    bool pb = wave_pass(b, ys, ps, cst);
+    if (a.nh + b.nh <= WAVE) {
+        if (t < b.nh) {
+            ys[a.nh + t] = b.Y;
+            ps[a.nh + t] = b.W | (b.BS << 8) | (b.O << 9);
         }
-        const double tn = shfl_d(num, last);
-        const int td = shfl_i(den, last);
-        if (pool) {
-            Y = tn / (double)td;
-            W = td;
-        }
-        // pack the surviving runs into lanes 0 .. nh-1
-        const bool surv = act && !(inpool && depth > 0);
-        const uint64_t S = __ballot(surv);
-        if (surv) {
-            const int idx = mbcnt64(S);
-            ys[idx] = Y;
-            ps[idx] = W | (BS << 8) | (O << 9);
-        }
-        nh = __popcll(S);
-        if (t < nh) {
-            Y = ys[t];
+        WaveRuns m = a;
+        m.nh = a.nh + b.nh;
+        if (t >= a.nh && t < m.nh) {
+            m.Y = ys[t];
             const int pk = ps[t];
-            W = pk & 255;
-            BS = (pk >> 8) & 1;
-            O = pk >> 9;
+            m.W = pk & 255;
+            m.BS = (pk >> 8) & 1;
+            m.O = pk >> 9;
         }
+        bool more = pa || pb;
+        for (int pass = 0; more && pass <= 2 * WAVE; ++pass) more = wave_pass(m, ys, ps, cst);
+        // expand over the 128 element slots (a's at 0.., b's at 64..)
+        ps[t] = 0;
+        ps[WAVE + t] = 0;
+        if (t < m.nh) ps[m.O] = 1;
+        const uint64_t RA = __ballot(t < La && ps[t] != 0);
+        const uint64_t RB = __ballot(t < Lb && ps[WAVE + t] != 0);
+        const int ia = mbcnt64(RA) + (int)((RA >> t) & 1ull) - 1;
+        const int ib = __popcll(RA) + mbcnt64(RB) + (int)((RB >> t) & 1ull) - 1;
+        const double va = shfl_d(m.Y, ia < 0 ? 0 : ia);
+        const double vb = shfl_d(m.Y, ib < 0 ? 0 : ib);
+        if (t < La) ya = va;
+        if (t < Lb) yb = vb;
+        return;
     }
-    // expand: element e takes the value of the last run starting at or before e
-    ps[t] = 0;
-    if (t < nh) ps[O] = 1;
-    const uint64_t RS = __ballot(t < L && ps[t] != 0);
-    const int idx = mbcnt64(RS) + (int)((RS >> t) & 1ull) - 1;
-    const double v = shfl_d(Y, idx < 0 ? 0 : idx);
-    if (t < L) y = v;
+    for (int pass = 0; pa && pass <= La; ++pass) pa = wave_pass(a, ys, ps, cst);
+    for (int pass = 0; pb && pass <= Lb; ++pass) pb = wave_pass(b, ys, ps, cst);
+    ya = wave_expand(a, ya, La, 0, ps);
+    yb = wave_expand(b, yb, Lb, WAVE, ps);
 }
 
 }  // namespace bsls

@@ -166,11 +166,14 @@ def test_bb_deterministic(cuda, fmt):
     assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64))
 
 
-def test_k3_wave_pava_bit_exact(cuda, orc):
+@pytest.mark.parametrize('merge', ['1', '0'])
+def test_k3_wave_pava_bit_exact(cuda, orc, monkeypatch, merge):
     """K3 alone (stage 4): z_new = clip01(PAVA_v1(z - t g)) and x = N z_new, bit for
-    bit against the oracle, on blocks of 2..150 routes (wave packs and the
-    serial fallback for z-blocks longer than 64)."""
+    bit against the oracle, on blocks of 2..150 routes (wave packs -- two per
+    wave sharing their later passes, or one -- and the paths for z-blocks
+    longer than 64)."""
     import torch
+    monkeypatch.setenv('BSLS_K3_MERGE', merge)
     import _native
     from device import BBEngine
     rs = np.random.RandomState(7)
