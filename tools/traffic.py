@@ -5,7 +5,7 @@ over tools/kprof.py).  MI355X_MICROARCH.md "HBM / rocprofv3": FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
 coalesced reads, so traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes).
 Usage: python tools/traffic.py CONFIG OUT.json pmc_dir... -- adds CONFIG's kernels
-(C3: panels, C5: dealt tiles) to OUT.json (keyed by config, read by bench.py)."""
+(dealt tiles; K1 = the walk + its finish launch) to OUT.json (keyed by config, read by bench.py)."""
 import csv
 import glob
 import json
@@ -15,13 +15,13 @@ from collections import defaultdict
 
 # bench.py kernel names -> device kernels (demangled prefixes) in one launch of the stage
 KERNELS = {
-    'C3': {'K2_spmvT_Nt_dots': ['bsls::bb_k2<2, true>'],
-           'K3_pava_clip_z2x': ['bsls::bb_k3('],
-           'K1_spmv_A': ['bsls::bb_k1<0, true, true, true>'],
+    'C3': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<3, true>'],
+           'K3_pava_clip_z2x': ['bsls::bb_k3<1, false>'],
+           'K1_spmv_A': ['bsls::bb_k1t<0, true, true, true>', 'bsls::bb_k1_sum<true, true, true>'],
            'proj_simplex_C2': ['bsls::proj_lds_kernel<false>']},
-    'C5': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<2, true>'],
-           'K3_pava_clip_z2x': ['bsls::bb_k3('],
-           'K1_spmv_A': ['bsls::bb_k1t<0, true, true, true>']},
+    'C5': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<3, true>'],
+           'K3_pava_clip_z2x': ['bsls::bb_k3<2, true>'],
+           'K1_spmv_A': ['bsls::bb_k1t<0, true, true, true>', 'bsls::bb_k1_sum<true, true, true>']},
 }
 
 
