@@ -273,7 +273,8 @@ class DevicePanels:
         return sum(v.numel() * v.element_size() for v in self.t.values())
 
 
-def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=None, layout=0):
+def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=None, layout=0,
+              nnz=None):
     """(H, ngroups, order) of a tile image (include/bsls_hip.h struct bsls_tiles,
     csrc/tiles.hpp): column groups (a power of two) until one group's slice of
     the gathered vector fits an XCD's L2 (order 1, XCD-sequential, past 8
@@ -310,6 +311,13 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
         nrb = max(nmin, cus // G)
         nrb = -(-(nrb * G) // cus) * cus // G if nrb * G > cus else nrb
         H = max(64, -(-rows // nrb))
+        if halo and nnz and nrb % 2 == 0 and 2 * H <= hmax and cols >= 2 and \
+                nnz / nrb / cols < 0.15:
+            # K2 tiles this sparse (a C5 shard over 8 GPUs: 0.08 entries per
+            # column) take two groups of twice the rows, 4x the density: C5/8
+            # K2 78.0 -> 72.5 us (C3 at 0.62 and C5 at 0.31 entries per column
+            # stay at one group: 2 groups measured 45.7 / 510 against 35.6 / 358)
+            G, nrb, H = 2, nrb // 2, 2 * H
         return int(H), int(G), 0
     if l2_slice is None:
         # measured on the C5 shard (tools/stage_time.py): K1 fastest with
@@ -464,7 +472,7 @@ class DeviceTiles:
         R, C = M.shape
         H, G, order = plan or tile_plan(R, C, halo, colv_lds,
                                         env='BSLS_TILE_PLAN_AT' if halo else 'BSLS_TILE_PLAN_A',
-                                        layout=layout)
+                                        layout=layout, nnz=M.nnz)
         gc = np.round(np.linspace(0, C, G + 1)).astype(np.int64)
         if np.any(np.diff(gc) < 1):
             raise ValueError('more column groups than columns')
