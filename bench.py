@@ -251,14 +251,15 @@ def bench_xspace(sh, b, rounds=40, reps=5):
 
 def bench_dore(sh, b, iters=30):
     """DORE (python/DORE.py:6-90 through gradient_descent.py:55-67's setup) on
-    the C3 problem: linop / linop_T on the engine's K1 / K2 images (A and the
-    target scaled by 0.99 / lsv, lsv from ARPACK over the same operators, not
-    timed), proj = PAVA v1 + clip.  `iters` iterations after 3 untimed ones,
-    eps < 0 so the norm-change exit never fires; the host makes the
-    reference's branch decisions (one device->host read each).  Roofline:
-    the algorithmic bytes of the kernels the iterations actually launched
-    (K1 / K2 general-CSR bytes per linop / linop_T, 16 n_z + 4 (p+1) per
-    projection) over the wall time."""
+    the C3 problem, the loop gradient_descent runs: DORE.solve_engine, every
+    step and branch on the device (bsls_dore_iterate: linop / linop_T on the
+    engine's K1 / K2 images with A and the target scaled by 0.99 / lsv -- lsv
+    from ARPACK over the same operators, not timed -- proj = PAVA v1 + clip
+    by K3).  `iters` iterations after 3 untimed ones, eps < 0 so the
+    norm-change exit never fires.  Roofline: the algorithmic bytes of the
+    kernels an iteration launches (3 K1 general-CSR passes, 1 K2, 2
+    projections at 16 n_z + 4 (p+1) each) over the wall time; the
+    host-decided closure loop (DORE.solve) is timed beside it."""
     import torch
     import DORE
     from device import BBEngine
@@ -266,38 +267,32 @@ def bench_dore(sh, b, iters=30):
     eng = BBEngine(sh['A'], b, sh['block_sizes'], AT=sh['AT'])
     lsv = lsv_operator(eng, None)
     scale = 0.99 / lsv
-    calls = {'A': 0, 'AT': 0, 'proj': 0}
-
-    def linop(z):
-        calls['A'] += 1
-        return eng.apply_A(z, alpha=scale)
-
-    def linop_T(r):
-        calls['AT'] += 1
-        return eng.apply_AT(r, alpha=scale)
-
-    def proj(z):
-        calls['proj'] += 1
-        return eng.proj(z)
     z0 = torch.zeros(eng.nz, dtype=torch.float64, device='cuda')
     tgt = eng.target * scale
     log = lambda i, s, d: 0.0
-    DORE.solve(z0, linop, linop_T, tgt, proj=proj, log=log, options={'max_iter': 3, 'opt_tol': -1.0})
+    DORE.solve_engine(eng, z0, scale, tgt, log=log, options={'max_iter': 3, 'opt_tol': -1.0})
     torch.cuda.synchronize()
-    for k in calls:
-        calls[k] = 0
     t0 = time.perf_counter()
-    x = DORE.solve(z0, linop, linop_T, tgt, proj=proj, log=log,
-                   options={'max_iter': iters, 'opt_tol': -1.0})
+    x = DORE.solve_engine(eng, z0, scale, tgt, log=log, record_every=10 ** 9,
+                          options={'max_iter': iters, 'opt_tol': -1.0})
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    taken = bool(eng.dore_scalars[3] != 0.0)
+    # the closure loop (host branch decisions), for comparison
+    t1 = time.perf_counter()
+    DORE.solve(z0, lambda z: eng.apply_A(z, alpha=scale), lambda r: eng.apply_AT(r, alpha=scale),
+               tgt, proj=eng.proj, log=log, options={'max_iter': 10, 'opt_tol': -1.0})
+    torch.cuda.synchronize()
+    host_us = (time.perf_counter() - t1) * 1e6 / 10
+    calls = {'A': 3 * iters, 'AT': iters, 'proj': 2 * iters}
     m, n, nz, p, nnz = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
     kb = kernel_bytes(m, n, nz, p, nnz, nnz)
     byt = (calls['A'] * kb['K1_spmv_A'] + calls['AT'] * kb['K2_spmvT_Nt_dots']
            + calls['proj'] * (16 * nz + 4 * (p + 1)))
     return {'operator': 'K1/K2 images (%s, %s)' % (eng.fmt_A, eng.fmt_AT), 'lsv': float(lsv),
+            'loop': 'device (DORE.solve_engine)', 'extrapolation_taken': taken,
             'iterations': iters, 'us_per_iter': el * 1e6 / iters, 'iterations_per_s': iters / el,
-            'launches': dict(calls),
+            'host_decided_loop_us_per_iter': host_us, 'launches': dict(calls),
             'roofline': {'bound': 'hbm', 'alg_bytes': byt, 'achieved': byt / el / 1e9,
                          'peak': HBM_PEAK / 1e9, 'unit': 'GB/s', 'frac': byt / el / HBM_PEAK},
             'finite': bool(torch.isfinite(x).all())}

@@ -78,6 +78,17 @@ class BBProblem(ctypes.Structure):
                 ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp)]
 
 
+class DoreState(ctypes.Structure):
+    """Mirror of struct bsls_dore_state (include/bsls_hip.h)."""
+    _fields_ = [('X', _vp * 3), ('X1', _vp), ('D', _vp), ('X2', _vp), ('AX', _vp * 3),
+                ('AX2', _vp), ('err', _vp), ('b', _vp), ('S', _vp), ('S2', _vp), ('dsc', _vp),
+                ('part', _vp), ('tickets', _vp), ('scale', _dbl), ('eps', _dbl)]
+
+
+DORE_NC, DORE_EE, DORE_A1, DORE_A2, DORE_SEL, DORE_STOPIT = range(6)
+DORE_COUNT = 16
+
+
 class CSR(ctypes.Structure):
     """Mirror of struct bsls_csr (include/bsls_hip.h)."""
     _fields_ = [('rows', _i64), ('indptr', _vp), ('indices', _vp), ('data', _vp),
@@ -138,6 +149,9 @@ _SIGS = {
     'bsls_bb_long_scratch_size': (_sz, [_i64]),
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
+    'bsls_dore_work_size': (_sz, [_i64, _i64]),
+    'bsls_dore_iterate': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(DoreState), _i64,
+                                 _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
     'bsls_bb_row_blocks': (_i64, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_residual_rows': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _i64, _vp]),

@@ -937,9 +937,197 @@ static int check_problem(const bsls_bb_problem *p) {
     return BSLS_OK;
 }
 
+// ---- DORE on the fused images (include/bsls_hip.h bsls_dore_iterate) --------
+// Vector steps of python/DORE.py:31-80 with the reference's elementwise
+// roundings; dot products as fixed-order block sums; every branch decided by
+// the last block of a reduction and read by the kernels after it.
+
+// Ax = scale * r (DORE's linop), err = b - Ax; norm_change = ||x - x_prev||^2
+// (la.norm(.)**2: the square of the rooted sum) and the break test
+__global__ __launch_bounds__(256) void dore_top(bsls_bb_problem P, bsls_dore_state D, int64_t it,
+                                                const double *__restrict__ x,
+                                                const double *__restrict__ xp) {
+    __shared__ double red[4];
+    if (D.S[BSLS_S_STOP] != 0.0) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        D.S2[BSLS_S_STOP] = 1.0;     // the extrapolated path stays off unless dore_mid opens it
+        D.dsc[BSLS_DORE_SEL] = 0.0;
+    }
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < P.m) {
+        const double ax = P.r[i] * D.scale;
+        D.err[i] = D.b[i] - ax;
+    }
+    double v[1] = {0.0};
+    if (i < P.nz) {
+        const double t = x[i] - xp[i];
+        v[0] = t * t;
+    }
+    block_sum<1>(v, red);
+    double tot[1];
+    if (last_block_sum<1>(v, D.part, D.tickets, tot, red) && threadIdx.x == 0) {
+        const double nr = sqrt(tot[0]);
+        const double nc = nr * nr;
+        D.dsc[BSLS_DORE_NC] = nc;
+        if (it > 0 && nc <= D.eps) {
+            D.S[BSLS_S_STOP] = 1.0;
+            D.dsc[BSLS_DORE_STOPIT] = (double)it;
+        }
+    }
+}
+
+// Ax = linop(x_new) -> axo; err; ||err||^2; i > 2: dAx = Ax - Ax_prev, dp, dAx.err
+__global__ __launch_bounds__(256) void dore_mid(bsls_bb_problem P, bsls_dore_state D, int64_t it,
+                                                double *__restrict__ axo,
+                                                const double *__restrict__ axp) {
+    __shared__ double red[3 * 4];
+    if (D.S[BSLS_S_STOP] != 0.0) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double v[3] = {0.0, 0.0, 0.0};
+    if (i < P.m) {
+        const double ax = P.r[i] * D.scale;
+        axo[i] = ax;
+        const double e = D.b[i] - ax;
+        D.err[i] = e;
+        v[0] = e * e;
+        if (it > 2) {
+            const double d = ax - axp[i];
+            v[1] = d * d;
+            v[2] = d * e;
+        }
+    }
+    block_sum<3>(v, red);
+    double tot[3];
+    if (last_block_sum<3>(v, D.part, D.tickets, tot, red) && threadIdx.x == 0) {
+        D.dsc[BSLS_DORE_EE] = tot[0];
+        const bool ext = it > 2 && tot[1] > 0;
+        if (ext) D.dsc[BSLS_DORE_A1] = tot[2] / tot[1];
+        D.S2[BSLS_S_STOP] = ext ? 0.0 : 1.0;
+    }
+}
+
+// first extrapolation: Ax_1 = (1 + a1) Ax - a1 Ax_prev, err_1 = b - Ax_1,
+// dAx = Ax_1 - Ax_prev_prev (dp, dAx.err_1); x_1 = x_new + a1 (x_new - x) and
+// x_1 - x_prev for the second; a2 and the K3 step t = -a2 into S2
+__global__ __launch_bounds__(256) void dore_ext(bsls_bb_problem P, bsls_dore_state D,
+                                                const double *__restrict__ ax,
+                                                const double *__restrict__ axp,
+                                                const double *__restrict__ axpp,
+                                                const double *__restrict__ x,
+                                                const double *__restrict__ xp,
+                                                const double *__restrict__ xn) {
+    __shared__ double red[2 * 4];
+    if (D.S[BSLS_S_STOP] != 0.0 || D.S2[BSLS_S_STOP] != 0.0) return;
+    const double a1 = D.dsc[BSLS_DORE_A1];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double v[2] = {0.0, 0.0};
+    if (i < P.m) {
+        const double ax1 = (1 + a1) * ax[i] - a1 * axp[i];
+        const double e1 = D.b[i] - ax1;
+        const double d = ax1 - axpp[i];
+        v[0] = d * d;
+        v[1] = d * e1;
+    }
+    if (i < P.nz) {
+        const double x1 = xn[i] + a1 * (xn[i] - x[i]);
+        D.X1[i] = x1;
+        D.D[i] = x1 - xp[i];
+    }
+    block_sum<2>(v, red);
+    double tot[2];
+    if (last_block_sum<2>(v, D.part, D.tickets, tot, red) && threadIdx.x == 0) {
+        if (tot[0] > 0) {
+            const double a2 = tot[1] / tot[0];
+            D.dsc[BSLS_DORE_A2] = a2;
+            D.S2[BSLS_S_SUMDG] = 1.0;
+            D.S2[BSLS_S_DZDG] = -a2;    // K3: x_1 - (-a2) (x_1 - x_prev) = x_1 + a2 (...)
+            D.S2[BSLS_S_DGDG] = 1.0;
+        } else {
+            D.S2[BSLS_S_STOP] = 1.0;
+        }
+    }
+}
+
+// Ax_2 = linop(x_2), err_2; keep x_2 when ||err_2||^2 / ||err||^2 < 1
+__global__ __launch_bounds__(256) void dore_sel(bsls_bb_problem P, bsls_dore_state D) {
+    __shared__ double red[4];
+    if (D.S[BSLS_S_STOP] != 0.0 || D.S2[BSLS_S_STOP] != 0.0) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double v[1] = {0.0};
+    if (i < P.m) {
+        const double ax2 = P.r[i] * D.scale;
+        D.AX2[i] = ax2;
+        const double e = D.b[i] - ax2;
+        v[0] = e * e;
+    }
+    block_sum<1>(v, red);
+    double tot[1];
+    if (last_block_sum<1>(v, D.part, D.tickets, tot, red) && threadIdx.x == 0)
+        D.dsc[BSLS_DORE_SEL] = (tot[0] / D.dsc[BSLS_DORE_EE] < 1) ? 1.0 : 0.0;
+}
+
+// x_select = x_2, Ax = Ax_2 when selected
+__global__ __launch_bounds__(256) void dore_copy(bsls_bb_problem P, bsls_dore_state D,
+                                                 double *__restrict__ xn,
+                                                 double *__restrict__ axo) {
+    if (D.S[BSLS_S_STOP] != 0.0 || D.S2[BSLS_S_STOP] != 0.0 || D.dsc[BSLS_DORE_SEL] == 0.0)
+        return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < P.nz) xn[i] = D.X2[i];
+    if (i < P.m) axo[i] = D.AX2[i];
+}
+
 }  // namespace bsls
 
 using namespace bsls;
+
+extern "C" size_t bsls_dore_work_size(int64_t nz, int64_t m) {
+    const int64_t n = (nz > m ? nz : m);
+    return (size_t)((n + 255) / 256 + 1) * 3 * sizeof(double);
+}
+
+extern "C" int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state *d,
+                                 int64_t first_iter, int64_t count, void *stream) {
+    const int rc = check_problem(p);
+    if (rc != BSLS_OK) return rc;
+    if (!d || first_iter < 0 || count < 0 || !d->X1 || !d->D || !d->X2 || !d->AX2 || !d->err ||
+        !d->b || !d->S || !d->S2 || !d->dsc || !d->part || !d->tickets)
+        return BSLS_E_ARG;
+    for (int k = 0; k < 3; ++k)
+        if (!d->X[k] || !d->AX[k]) return BSLS_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const BBWork w = bb_layout(*p);
+    bsls_bb_problem PS = *p, P2 = *p, PE = *p;
+    PS.scal = d->S;
+    PE.scal = d->S;
+    PE.r = d->err;                       // K2 reads err as its r
+    P2.scal = d->S2;
+    const bsls_dore_state D = *d;
+    const int64_t big = (p->nz > p->m ? p->nz : p->m);
+    const int gb = grid_for(big, 256), gm = grid_for(p->m, 256);
+    for (int64_t i = first_iter; i < first_iter + count; ++i) {
+        double *x = d->X[i % 3], *xp = d->X[(i + 2) % 3], *xn = d->X[(i + 1) % 3];
+        double *axo = d->AX[i % 3], *axp = d->AX[(i + 2) % 3], *axpp = d->AX[(i + 1) % 3];
+        // Ax = linop(x), err, norm_change (DORE.py:31-37)
+        bb_z2x<<<grid_for(p->n, 256), 256, 0, st>>>(PS, x);
+        launch_k1<false, false, true>(PS, i, w, st);
+        dore_top<<<gb, 256, 0, st>>>(PS, D, i, x, xp);
+        // x_new = proj(x + linop_T(err)) (DORE.py:38-40; K3 with t = -scale)
+        launch_k2<false>(PE, nullptr, p->g[0], w, st);
+        launch_k3(PS, i, x, p->g[0], xn, w, st);
+        // Ax = linop(x_new), err (DORE.py:41-42) and the first extrapolation
+        launch_k1<false, false, true>(PS, i, w, st);
+        dore_mid<<<gm, 256, 0, st>>>(PS, D, i, axo, axp);
+        dore_ext<<<gb, 256, 0, st>>>(PS, D, axo, axp, axpp, x, xp, xn);
+        // x_2 = proj(x_1 + a2 (x_1 - x_prev)), Ax_2 = linop(x_2), selection (DORE.py:55-69)
+        launch_k3(P2, i, d->X1, d->D, d->X2, w, st);
+        launch_k1<false, false, true>(P2, i, w, st);
+        dore_sel<<<gm, 256, 0, st>>>(P2, D);
+        dore_copy<<<gb, 256, 0, st>>>(P2, D, xn, axo);
+        BSLS_LAUNCH_CHECK();
+    }
+    return BSLS_OK;
+}
 
 extern "C" size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz) {
     return bb_layout(nullptr, m, n, nz).bytes;

@@ -83,13 +83,10 @@ class GradientDescent:
             scale = alpha / lsv
             b_t = e.target * scale
 
-            def linop(z):
-                return e.apply_A(z, alpha=scale)
-
-            def linop_T(r):
-                return e.apply_AT(r, alpha=scale)
-            DORE.solve(self._z0_device(), linop, linop_T, b_t, proj=e.proj, log=self.log,
-                       options=self.options, record_every=100)
+            # the whole loop on the device (linop = scale A N, linop_T =
+            # scale N'A', proj = PAVA v1 + clip on the engine's images)
+            DORE.solve_engine(e, self._z0_device(), scale, b_t, log=self.log,
+                              options=self.options, record_every=100)
             self.lsv = lsv
         else:
             raise ValueError('unknown method %r' % self.method)

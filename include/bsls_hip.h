@@ -335,6 +335,43 @@ int64_t bsls_bb_row_blocks(const bsls_bb_problem *p, int64_t *rows_per_block);
 int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
                           void *stream);
 
+/* ---- DORE on the fused images (python/DORE.py:6-90, gradient_descent.py:55-67)
+ * The reference loop with linop = scale * A N, linop_T = scale * N'A',
+ * proj = PAVA v1 + clip, every branch decided on the device: per iteration i
+ *   Ax = linop(x), err = b - Ax, norm_change = ||x - x_prev||^2 (break if i > 0
+ *   and <= eps); x_new = proj(x + linop_T(err)) (K2, then K3 with t = -scale);
+ *   Ax = linop(x_new), err; i > 2: the two residual extrapolations (a1, a2),
+ *   x_2 = proj(x_1 + a2 (x_1 - x_prev)) (K3 with t = -a2), Ax_2, and x_2 kept
+ *   when ||err_2||^2 / ||err||^2 < 1.
+ * Buffers rotate by iteration: x = X[i%3], x_prev = X[(i+2)%3], the new x is
+ * written to X[(i+1)%3]; AX[i%3] = Ax at the end of iteration i.  S / S2 are
+ * scal[] blocks (BSLS_S_*) gating the main and the extrapolated path (S:
+ * SUMDG = 1, DZDG = -scale, DGDG = 1, STOP = 0 before the first call);
+ * dsc[BSLS_DORE_*] the loop's scalars.  K1 / K2 / K3 use p's images and work. */
+enum {
+    BSLS_DORE_NC = 0,      /* norm_change of the last iteration */
+    BSLS_DORE_EE = 1,      /* err.err after linop(x_new) */
+    BSLS_DORE_A1 = 2,
+    BSLS_DORE_A2 = 3,
+    BSLS_DORE_SEL = 4,     /* 1: x_2 selected in the last iteration */
+    BSLS_DORE_STOPIT = 5,  /* iteration of the norm-change break (S[STOP] = 1) */
+    BSLS_DORE_COUNT = 16
+};
+typedef struct bsls_dore_state {
+    double *X[3];          /* nz each */
+    double *X1, *D, *X2;   /* x_1, x_1 - x_prev, x_2: nz each */
+    double *AX[3];         /* m each */
+    double *AX2, *err, *b; /* m each; b = -scale * target (DORE.py:23) */
+    double *S, *S2;        /* BSLS_S_COUNT doubles each */
+    double *dsc;           /* BSLS_DORE_COUNT doubles */
+    double *part;          /* bsls_dore_work_size(nz, m) bytes: reduction partials */
+    unsigned *tickets;     /* 576 zeroed bytes (nine 64-B ticket words) */
+    double scale, eps;
+} bsls_dore_state;
+size_t bsls_dore_work_size(int64_t nz, int64_t m);
+int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state *d, int64_t first_iter,
+                      int64_t count, void *stream);
+
 /* ---- x-space least-squares operator on panel images -------------------------
  * Replaces sparse_least_squares_obj's two SciPy products
  * (python/algorithm_utils.py:88-94; python/mirror_descent.py:31-34):

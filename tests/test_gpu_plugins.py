@@ -121,6 +121,50 @@ def test_dore_vs_reference(cuda, golden):
         assert rel(s, G['dore_states'][k]) < 1e-6, (k, iters[k])
 
 
+@pytest.mark.parametrize('eps', [-1.0, 1e30])
+def test_dore_device_loop_vs_closures(cuda, eps):
+    """DORE.solve_engine (every step and branch on the device, what
+    GradientDescent('DORE') runs) against DORE.solve over the engine's
+    closures (host branch decisions) on a 60k-route problem: every logged
+    iterate within 1e-8 (the dot products round in different orders), the
+    extrapolated path taken, and the norm-change break (eps = 1e30: stop at
+    iteration 1 with the iterate of iteration 0) at the same iteration."""
+    import torch
+    import DORE
+    from device import BBEngine
+    from bsls_utils import lsv_operator
+    from synthetic import make_shard, add_noise
+    sh = make_shard(60000, 3000, 8000, per_col=16, seed=3)
+    b = add_noise(sh['Ax'], 0.02, seed=3)
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], AT=sh['AT'])
+    scale = 0.99 / lsv_operator(eng, None)
+    tgt = eng.target * scale
+    z0 = torch.zeros(eng.nz, dtype=torch.float64, device='cuda')
+    opts = {'max_iter': 40, 'opt_tol': eps}
+    runs = []
+    for fused in (False, True):
+        rec = []
+
+        def log(i, st, dt):
+            rec.append((i, st.detach().cpu().numpy().copy()))
+            return 0.0
+        if fused:
+            DORE.solve_engine(eng, z0, scale, tgt, record_every=1, log=log, options=opts)
+        else:
+            DORE.solve(z0, lambda z: eng.apply_A(z, alpha=scale),
+                       lambda r: eng.apply_AT(r, alpha=scale), tgt, record_every=1,
+                       proj=eng.proj, log=log, options=opts)
+        runs.append(rec)
+    ref, got = runs
+    assert [i for i, _ in got] == [i for i, _ in ref]
+    for (i, a), (_, bb) in zip(got, ref):
+        assert rel(a, bb) < 1e-8, i
+    if eps < 0:
+        assert eng.dore_scalars[3] != 0.0          # a2: the extrapolated path ran
+    else:
+        assert got[-1][0] == 1
+
+
 def test_lbfgs_vs_reference(cuda, golden):
     """GradientDescent('LBFGS') over the engine's device closures, 5 iterations
     (the fixture's run): LBFGS on this problem is ill-conditioned in the
