@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void iso_pack_kernel(double *__restrict__ y,
     const int wv = threadIdx.x / WAVE;
     const int64_t q = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);
     __shared__ double pv_y[4][64];
-    __shared__ int pv_p[4][64];
+    __shared__ int pv_p[4][128];
     __shared__ int pv_c[4][65];
     const int64_t p0 = 2 * q;
     if (p0 >= nwin) return;
@@ -193,8 +193,31 @@ __global__ __launch_bounds__(256) void iso_pack_kernel(double *__restrict__ y,
         const uint64_t B = __ballot(l < span && ps[l] != 0);
         iso_wave_pack(y, s0, (int)span, B, pv_y[wv], ps, pv_c[wv]);
     } else {
-        iso_window(y, starts, nb, n, f, m, lcnt, llist, pv_y[wv], ps, pv_c[wv]);
-        iso_window(y, starts, nb, n, m, e, lcnt, llist, pv_y[wv], ps, pv_c[wv]);
+        // two packs, one per window; with no long last block (the common
+        // case) both run in the wave together, sharing their passes after
+        // the first (pava_v1_wave_pair) instead of one after the other
+        const int64_t ea = (m > f) ? block_end(starts, nb, m - 1, n) : 0;
+        const int64_t eb = (e > m) ? block_end(starts, nb, e - 1, n) : 0;
+        const bool pair = m > f && e > m && ea - starts[m - 1] <= ISO_WIN &&
+                          eb - starts[e - 1] <= ISO_WIN;
+        if (pair) {
+            const int64_t sa = s0, sb = starts[m];
+            const int La = (int)(ea - sa), Lb = (int)(eb - sb);   // <= 63 each
+            ps[l] = 0;
+            if (l < m - f) ps[(int)(starts[f + l] - sa)] = 1;
+            const uint64_t Ba = __ballot(l < La && ps[l] != 0);
+            ps[l] = 0;
+            if (l < e - m) ps[(int)(starts[m + l] - sb)] = 1;
+            const uint64_t Bb = __ballot(l < Lb && ps[l] != 0);
+            double va = (l < La) ? y[sa + l] : 0.0;
+            double vb = (l < Lb) ? y[sb + l] : 0.0;
+            pava_v1_wave_pair(va, La, Ba, vb, Lb, Bb, pv_y[wv], ps, pv_c[wv]);
+            if (l < La) y[sa + l] = va;
+            if (l < Lb) y[sb + l] = vb;
+        } else {
+            iso_window(y, starts, nb, n, f, m, lcnt, llist, pv_y[wv], ps, pv_c[wv]);
+            iso_window(y, starts, nb, n, m, e, lcnt, llist, pv_y[wv], ps, pv_c[wv]);
+        }
     }
 }
 
