@@ -166,6 +166,8 @@ _SIGS = {
                                 _i64]),
     'bsls_tiles_build_dealt': (_i64, [_i64, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
                                       _vp, _vp, _i64]),
+    'bsls_tiles_build_dealt3': (_i64, [_i64, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp,
+                                      _vp, _vp, _i64]),
     'bsls_version': (ctypes.c_char_p, []),
     'bsls_device_arch': (_int, [ctypes.c_char_p, _int]),
 }
@@ -297,9 +299,10 @@ def tiles_build(M, H, halo, group_col, values=True):
     return dict(wave_off=wo, ent=ent, val=val, nquads=int(nq), nrb=nrb)
 
 
-def tiles_build_dealt(M, H, halo, group_col, values=True):
+def tiles_build_dealt(M, H, halo, group_col, values=True, packed=False):
     """Host arrays of the layout-1 (dealt) tile image of CSR matrix M
-    (bsls_tiles_build_dealt, host only): dict(wave_off, ent, base, val or None,
+    (bsls_tiles_build_dealt, host only), or with `packed` layout 2 (3-byte
+    entries, bsls_tiles_build_dealt3): dict(wave_off, ent, base, val or None,
     nquads, nrb)."""
     import numpy as np
     ip = np.ascontiguousarray(M.indptr, dtype=np.int64)
@@ -310,18 +313,18 @@ def tiles_build_dealt(M, H, halo, group_col, values=True):
     G = gc.shape[0] - 1
     L = load()
     vp = lambda a: ctypes.c_void_p(a.ctypes.data) if a is not None else ctypes.c_void_p(0)
-    nq = L.bsls_tiles_build_dealt(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc),
-                                  None, None, None, None, 0)
+    fn = L.bsls_tiles_build_dealt3 if packed else L.bsls_tiles_build_dealt
+    nq = fn(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc), None, None, None, None, 0)
     if nq < 0:
         raise ValueError('dealt tile image: invalid layout (H %d, halo %d, %d groups)'
                          % (H, halo, G))
     nrb = -(-R // int(H))
     wo = np.zeros(nrb * G + 1, dtype=np.int64)
-    ent = np.zeros(4 * nq + 256, dtype=np.uint32)
+    ent = np.zeros((3 if packed else 4) * nq + 256, dtype=np.uint32)
     base = np.zeros(4 * nq // 64 + 64, dtype=np.int32)
     val = np.zeros(4 * nq + 256, dtype=np.float64) if values else None
-    rc = L.bsls_tiles_build_dealt(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc),
-                                  vp(wo), vp(ent), vp(base), vp(val), nq)
+    rc = fn(R, C, vp(ip), vp(ix), vp(dv), int(H), int(halo), G, vp(gc), vp(wo), vp(ent), vp(base),
+            vp(val), nq)
     if rc != nq:
         raise RuntimeError('bsls_tiles_build_dealt failed (%d)' % rc)
     return dict(wave_off=wo, ent=ent, base=base, val=val, nquads=int(nq), nrb=nrb)

@@ -38,7 +38,7 @@ __host__ __device__ inline int64_t tile_nslots(const bsls_tiles &T) {
 // dynamic LDS doubles of a tile kernel: the row sums (+ the dummy slot), and
 // with `colv` the rows' column scales (K2 on a scaled incidence)
 __host__ __device__ inline size_t tile_lds_doubles(const bsls_tiles &T, bool colv) {
-    if ((T.layout & 0xFF) == 1) return (size_t)(T.H + T.halo + 1) * (colv ? 2 : 1);
+    if ((T.layout & 0xFF) >= 1) return (size_t)(T.H + T.halo + 1) * (colv ? 2 : 1);
     return (size_t)(tile_nslots(T) + 1) * TILE_T * (colv ? 2 : 1);
 }
 
@@ -131,45 +131,90 @@ __device__ __forceinline__ void tile_walk(const bsls_tiles &T, int64_t rb, int64
     }
 }
 
+// Layout 2's entries: 3 uint32 per lane hold four 24-bit entries
+typedef uint32_t tile_tri __attribute__((ext_vector_type(3)));
+
+template <bool NT>
+__device__ __forceinline__ tile_tri tt_load(const uint32_t *p) {
+    const tile_tri *q = reinterpret_cast<const tile_tri *>(p);
+    if (NT) return __builtin_nontemporal_load(q);
+    return *q;
+}
+
+__device__ __forceinline__ uint32_t tri_entry(const tile_tri &t, int j) {
+    switch (j) {
+        case 0: return t[0] & 0xFFFFFFu;
+        case 1: return (t[0] >> 24) | ((t[1] & 0xFFFFu) << 8);
+        case 2: return (t[1] >> 16) | ((t[2] & 0xFFu) << 16);
+        default: return t[2] >> 8;
+    }
+}
+
 // Layout 1 (dealt, include/bsls_hip.h): wave w walks its instructions of tile
 // (rb, g) quad-step by quad-step -- one 16-B entry load (4 slots) and one
 // scalar 16-B base load per step, loaded P steps ahead, the gathers of step
 // s + D issued before the LDS atomic adds of step s.  MODE as tile_walk.
+// PK3 (layout 2): the step's entries are one 12-B load (four 24-bit entries:
+// 25 % less stream), unpacked where they are used.
 #ifndef BSLS_TILE_P
 #define BSLS_TILE_P 4
 #endif
 #ifndef BSLS_TILE_D
 #define BSLS_TILE_D 1
 #endif
-template <int MODE, bool NT, int P = BSLS_TILE_P, int D = BSLS_TILE_D>
+template <bool PK3>
+struct TileEnt {
+    typedef tile_quad type;
+};
+template <>
+struct TileEnt<true> {
+    typedef tile_tri type;
+};
+
+template <int MODE, bool NT, bool PK3 = false, int P = BSLS_TILE_P, int D = BSLS_TILE_D>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
                                                 const double *rcol) {
     static_assert(D >= 1 && D < P, "gathers run ahead of the entry loads");
     if (BSLS_TILE_KO == 3) return;
+    typedef typename TileEnt<PK3>::type ent_t;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int64_t t = rb * T.ngroups + g;
     const int64_t q0 = T.wave_off[t], nq = T.wave_off[t + 1] - q0;
-    const tile_quad *Q = reinterpret_cast<const tile_quad *>(T.ent) + (q0 * 16 + wv) * 64 + lane;
+    // entries: lane (q0 * 16 + wv) * 64 + lane of the image, 1024 lanes per step
+    const int64_t l0 = (q0 * 16 + wv) * 64 + lane;
+    const uint32_t *E = T.ent + (PK3 ? 3 : 4) * l0;
+    constexpr int64_t STEP = (PK3 ? 3 : 4) * 1024;   // uint32 per quad-step
+    // layout 2: column offset in the low cb bits, the local row above
+    const int cb = PK3 ? 24 - (32 - __builtin_clz((unsigned)(T.H + T.halo))) : 16;
+    const uint32_t cmask = (1u << cb) - 1u;
+    auto ld = [&](int64_t s) -> ent_t {
+        if constexpr (PK3) return tt_load<NT>(E + s * STEP);
+        else return tq_load<NT>(reinterpret_cast<const tile_quad *>(E + s * STEP));
+    };
+    auto ent = [&](const ent_t &u, int j) -> uint32_t {
+        if constexpr (PK3) return tri_entry(u, j);
+        else return u[j];
+    };
     const int4 *Bq = reinterpret_cast<const int4 *>(T.base) + q0 * 16 + wv;
-    const double *V = (MODE == 1) ? T.val + 4 * ((q0 * 16 + wv) * 64 + lane) : nullptr;
+    const double *V = (MODE == 1) ? T.val + 4 * l0 : nullptr;
     const double *xb = src + T.group_col[g];
-    tile_quad ring[P];
+    ent_t ring[P];
     int4 bring[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        ring[k] = (k < nq) ? tq_load<NT>(Q + (int64_t)k * 1024) : tile_quad{0, 0, 0, 0};
+        ring[k] = (k < nq) ? ld(k) : ent_t{};
         bring[k] = (k < nq) ? Bq[(int64_t)k * 16] : int4{0, 0, 0, 0};
     }
     // v[d] / a[d]: the gathered values (and stored values) of step s + d
     double v[D + 1][4], a[D + 1][4];
     double ko = 0.0;
-    auto gat = [&](const tile_quad &u, const int4 &b, int64_t q, double (&o)[4], double (&w)[4]) {
-        o[0] = xb[b.x + (u[0] & 0xFFFFu)];
-        o[1] = xb[b.y + (u[1] & 0xFFFFu)];
-        o[2] = xb[b.z + (u[2] & 0xFFFFu)];
-        o[3] = xb[b.w + (u[3] & 0xFFFFu)];
+    auto gat = [&](const ent_t &u, const int4 &b, int64_t q, double (&o)[4], double (&w)[4]) {
+        o[0] = xb[b.x + (ent(u, 0) & cmask)];
+        o[1] = xb[b.y + (ent(u, 1) & cmask)];
+        o[2] = xb[b.z + (ent(u, 2) & cmask)];
+        o[3] = xb[b.w + (ent(u, 3) & cmask)];
         if (MODE == 1) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) w[j] = V[q * 4096 + j];
@@ -181,16 +226,16 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
     for (int64_t q = 0; q < nq; q += P) {
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            const tile_quad cur = ring[k];
+            const ent_t cur = ring[k];
             if (q + k + D < nq) gat(ring[(k + D) % P], bring[(k + D) % P], q + k + D, v[D], a[D]);
             if (q + k + P < nq) {
-                ring[k] = tq_load<NT>(Q + (q + k + P) * 1024);
+                ring[k] = ld(q + k + P);
                 bring[k] = Bq[(q + k + P) * 16];
             }
             if (q + k < nq) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int lr = (int)(cur[j] >> 16);
+                    const int lr = (int)(ent(cur, j) >> cb);
                     double term;
                     if (MODE == 0) term = v[0][j];
                     else if (MODE == 1) term = a[0][j] * v[0][j];
@@ -223,6 +268,9 @@ __device__ __forceinline__ void tile_walk_any(const bsls_tiles &T, int64_t rb, i
                                               const double *rcol) {
     if (T.layout == 1) tile_walk_dealt<MODE, false>(T, rb, g, src, rows, rcol);
     else if (T.layout == (1 | BSLS_TILE_NT)) tile_walk_dealt<MODE, true>(T, rb, g, src, rows, rcol);
+    else if (T.layout == 2) tile_walk_dealt<MODE, false, true>(T, rb, g, src, rows, rcol);
+    else if (T.layout == (2 | BSLS_TILE_NT))
+        tile_walk_dealt<MODE, true, true>(T, rb, g, src, rows, rcol);
     else tile_walk<MODE>(T, rb, g, src, rows, rcol);
 }
 

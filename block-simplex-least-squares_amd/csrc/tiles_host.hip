@@ -198,19 +198,34 @@ void dealt_collect(const Plan &p, const double *data, int64_t rb, std::vector<st
                   [](const DealtEnt &a, const DealtEnt &b) { return a.key < b.key; });
 }
 
-// instruction starts of a sorted tile (greedy: <= 64 entries, column span <= 65535)
-void dealt_insts(const std::vector<DealtEnt> &e, std::vector<int64_t> &st) {
+// instruction starts of a sorted tile (greedy: <= 64 entries, column span <= span)
+void dealt_insts(const std::vector<DealtEnt> &e, std::vector<int64_t> &st, uint64_t span) {
     st.clear();
     size_t i = 0;
     while (i < e.size()) {
         st.push_back((int64_t)i);
         const uint64_t base = e[i].key >> 16;
         size_t j = i + 1;
-        while (j < e.size() && j - i < 64 && (e[j].key >> 16) - base <= 65535) ++j;
+        while (j < e.size() && j - i < 64 && (e[j].key >> 16) - base <= span) ++j;
         i = j;
     }
     st.push_back((int64_t)e.size());
 }
+
+int bit_width(int64_t v) {
+    int b = 0;
+    while (v > 0) {
+        ++b;
+        v >>= 1;
+    }
+    return b;
+}
+
+// layout 1 (packed == false) or 2 (3-byte entries, include/bsls_hip.h)
+int64_t build_dealt(int64_t rows, int64_t cols, const int64_t *indptr, const int32_t *indices,
+                    const double *data, int64_t H, int64_t halo, int64_t ngroups,
+                    const int64_t *group_col, int64_t *wave_off_out, uint32_t *ent_out,
+                    int32_t *base_out, double *val_out, int64_t nquads_cap, bool packed);
 
 }  // namespace
 
@@ -220,9 +235,34 @@ extern "C" int64_t bsls_tiles_build_dealt(int64_t rows, int64_t cols, const int6
                                           int64_t *wave_off_out, uint32_t *ent_out,
                                           int32_t *base_out, double *val_out,
                                           int64_t nquads_cap) {
+    return build_dealt(rows, cols, indptr, indices, data, H, halo, ngroups, group_col,
+                       wave_off_out, ent_out, base_out, val_out, nquads_cap, false);
+}
+
+extern "C" int64_t bsls_tiles_build_dealt3(int64_t rows, int64_t cols, const int64_t *indptr,
+                                           const int32_t *indices, const double *data, int64_t H,
+                                           int64_t halo, int64_t ngroups, const int64_t *group_col,
+                                           int64_t *wave_off_out, uint32_t *ent_out,
+                                           int32_t *base_out, double *val_out,
+                                           int64_t nquads_cap) {
+    return build_dealt(rows, cols, indptr, indices, data, H, halo, ngroups, group_col,
+                       wave_off_out, ent_out, base_out, val_out, nquads_cap, true);
+}
+
+namespace {
+
+int64_t build_dealt(int64_t rows, int64_t cols, const int64_t *indptr, const int32_t *indices,
+                    const double *data, int64_t H, int64_t halo, int64_t ngroups,
+                    const int64_t *group_col, int64_t *wave_off_out, uint32_t *ent_out,
+                    int32_t *base_out, double *val_out, int64_t nquads_cap, bool packed) {
     if (rows < 1 || cols < 1 || !indptr || !indices || H < 64 || (halo != 0 && halo != 1) ||
         ngroups < 1 || !group_col || H + halo + 1 > 65536)
         return BSLS_E_ARG;
+    // packed: 24-bit entries, local row (rbits, the dummy row H + halo
+    // included) above the column offset (cbits = 24 - rbits)
+    const int rbits = bit_width(H + halo), cbits = 24 - rbits;
+    if (packed && cbits < 6) return BSLS_E_ARG;
+    const uint64_t span = packed ? ((1ull << cbits) - 1) : 65535ull;
     Plan p;
     p.rows = rows;
     p.cols = cols;
@@ -255,7 +295,7 @@ extern "C" int64_t bsls_tiles_build_dealt(int64_t rows, int64_t cols, const int6
         std::vector<int64_t> st;
         dealt_collect(p, nullptr, rb, e);
         for (int64_t g = 0; g < ngroups; ++g) {
-            dealt_insts(e[(size_t)g], st);
+            dealt_insts(e[(size_t)g], st, span);
             const int64_t ni = (int64_t)st.size() - 1;
             qs[rb * ngroups + g] = (ni + 63) / 64;
         }
@@ -267,18 +307,26 @@ extern "C" int64_t bsls_tiles_build_dealt(int64_t rows, int64_t cols, const int6
     if (!ent_out || !base_out || nquads_cap < nquads || (data && !val_out)) return BSLS_E_ARG;
     wave_off_out[0] = 0;
     for (int64_t t = 0; t < ntiles; ++t) wave_off_out[t + 1] = wave_off_out[t] + qs[t];
-    const uint32_t dummy = (uint32_t)(H + halo) << 16;
-    // pass 2: fill
+    const int rshift = packed ? cbits : 16;
+    const uint32_t dummy = (uint32_t)(H + halo) << rshift;
+    // pass 2: fill (packed: each tile in the 4-per-lane form first, then 3
+    // uint32 per lane: e0 | e1 << 24, e1 >> 8 | e2 << 16, e2 >> 16 | e3 << 8)
     parallel_blocks(p.nrb, [&](int64_t rb) {
         std::vector<std::vector<DealtEnt>> e;
         std::vector<int64_t> st;
+        std::vector<uint32_t> tmp;
         dealt_collect(p, data, rb, e);
         for (int64_t g = 0; g < ngroups; ++g) {
             const auto &E = e[(size_t)g];
-            dealt_insts(E, st);
+            dealt_insts(E, st, span);
             const int64_t t = rb * ngroups + g, q0 = wave_off_out[t];
             const int64_t nslot = (wave_off_out[t + 1] - q0) * 64;   // instructions incl. padding
             const int64_t ni = (int64_t)st.size() - 1;
+            uint32_t *eo = ent_out + 4 * q0 * 1024;
+            if (packed) {
+                tmp.assign((size_t)(4 * (wave_off_out[t + 1] - q0) * 1024), 0u);
+                eo = tmp.data();
+            }
             for (int64_t k = 0; k < nslot; ++k) {
                 const int64_t w = k % 16, j = (k / 16) % 4, q = q0 + k / 64;
                 const int64_t qi = (q * 16 + w) * 64;           // uint4 index of lane 0
@@ -292,18 +340,32 @@ extern "C" int64_t bsls_tiles_build_dealt(int64_t rows, int64_t cols, const int6
                 base_out[(q * 16 + w) * 4 + j] = (int32_t)base;
                 for (int64_t l = 0; l < 64; ++l) {
                     const int64_t u = 4 * (qi + l) + j;
+                    const int64_t ul = u - 4 * q0 * 1024;       // within the tile
                     if (a + l < b) {
                         const DealtEnt &d = E[(size_t)(a + l)];
-                        ent_out[u] = (uint32_t)(d.key & 0xFFFF) << 16 |
-                                     (uint32_t)((d.key >> 16) - base);
+                        eo[ul] = (uint32_t)(d.key & 0xFFFF) << rshift |
+                                 (uint32_t)((d.key >> 16) - base);
                         if (data) val_out[u] = d.v;
                     } else {
-                        ent_out[u] = dummy;
+                        eo[ul] = dummy;
                         if (data) val_out[u] = 0.0;
                     }
+                }
+            }
+            if (packed) {
+                const int64_t nl = (wave_off_out[t + 1] - q0) * 1024;   // lanes of the tile
+                uint32_t *po = ent_out + 3 * q0 * 1024;
+                for (int64_t i = 0; i < nl; ++i) {
+                    const uint32_t e0 = tmp[4 * i], e1 = tmp[4 * i + 1], e2 = tmp[4 * i + 2],
+                                   e3 = tmp[4 * i + 3];
+                    po[3 * i] = e0 | (e1 << 24);
+                    po[3 * i + 1] = (e1 >> 8) | (e2 << 16);
+                    po[3 * i + 2] = (e2 >> 16) | (e3 << 8);
                 }
             }
         }
     });
     return nquads;
 }
+
+}  // namespace

@@ -287,7 +287,7 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
         v = [int(a) for a in plan.split(',')]
         H, G = v[0], v[1]
         return H, G, (v[2] if len(v) > 2 else (1 if G > 8 else 0))
-    if layout == 1:
+    if layout in (1, 2):
         # dealt image: one round of workgroups (one per CU); K1 with as many
         # column groups, up to 8, as keep its row blocks within the LDS -- a
         # narrower group puts more of a tile's entries on each gathered line,
@@ -372,7 +372,7 @@ def tiles_matvec(img, x, colv=None, group_sums=False):
     T = _native.TILE_THREADS
     gc = img['group_col']
     x = np.asarray(x, dtype=np.float64)
-    if img.get('layout', 0) == 1:
+    if img.get('layout', 0) in (1, 2):
         return _dealt_matvec(img, x, colv, group_sums)
     nslots = -(-(H + halo) // T)
     out = np.zeros(R)
@@ -415,6 +415,19 @@ def _dealt_matvec(img, x, colv=None, group_sums=False):
     R, H, halo, G = img['rows'], img['H'], img['halo'], img['ngroups']
     gc, wo = img['group_col'], img['wave_off']
     ent = img['ent'].astype(np.int64)
+    cb = 16
+    if img.get('layout', 1) == 2:
+        # 3-byte entries: unpack every lane's 3 words into the 4-per-lane form
+        cb = 24 - int(H + halo).bit_length()
+        nl = int(wo[-1]) * 1024
+        w = ent[:3 * nl].reshape(-1, 3)
+        u = np.empty((nl, 4), dtype=np.int64)
+        u[:, 0] = w[:, 0] & 0xFFFFFF
+        u[:, 1] = (w[:, 0] >> 24) | ((w[:, 1] & 0xFFFF) << 8)
+        u[:, 2] = (w[:, 1] >> 16) | ((w[:, 2] & 0xFF) << 16)
+        u[:, 3] = w[:, 2] >> 8
+        ent = u.reshape(-1)
+    cmask = (1 << cb) - 1
     parts = []
     for g in range(G):
         acc = np.zeros(R)
@@ -430,8 +443,8 @@ def _dealt_matvec(img, x, colv=None, group_sums=False):
                     u = ((q * 16 + w) * 64 + lanes) * 4
                     for j in range(4):
                         e = ent[u + j]
-                        lr = e >> 16
-                        col = gc[g] + int(img['base'][(q * 16 + w) * 4 + j]) + (e & 0xFFFF)
+                        lr = e >> cb
+                        col = gc[g] + int(img['base'][(q * 16 + w) * 4 + j]) + (e & cmask)
                         xv = x[np.minimum(col, x.size - 1)]
                         if img['val'] is not None:
                             term = img['val'][u + j] * xv
@@ -476,8 +489,8 @@ class DeviceTiles:
         gc = np.round(np.linspace(0, C, G + 1)).astype(np.int64)
         if np.any(np.diff(gc) < 1):
             raise ValueError('more column groups than columns')
-        if layout == 1:
-            img = _native.tiles_build_dealt(M, H, halo, gc, values=values)
+        if layout in (1, 2):
+            img = _native.tiles_build_dealt(M, H, halo, gc, values=values, packed=layout == 2)
         else:
             img = _native.tiles_build(M, H, halo, gc, values=values)
         img.update(rows=R, cols=C, H=H, halo=halo, ngroups=G, order=order, group_col=gc,
@@ -489,13 +502,14 @@ class DeviceTiles:
                   'ent': torch.from_numpy(img['ent'].view(np.int32)).cuda()}
         if img['val'] is not None:
             self.t['val'] = torch.from_numpy(img['val']).cuda()
-        if layout == 1:
+        if layout in (1, 2):
             self.t['base'] = torch.from_numpy(img['base']).cuda()
         S = _native.Tiles()
         # dealt images larger than the Infinity Cache stream their entries
         # non-temporally (csrc/tiles.hpp tq_load)
-        S.layout = layout | (_native.TILE_NT if layout == 1 and self_bytes(img) > NT_BYTES else 0)
-        S.base = self.t['base'].data_ptr() if layout == 1 else None
+        S.layout = layout | (_native.TILE_NT if layout in (1, 2) and self_bytes(img) > NT_BYTES
+                             else 0)
+        S.base = self.t['base'].data_ptr() if layout in (1, 2) else None
         S.rows, S.cols, S.H, S.halo = R, C, H, halo
         S.nrb, S.ngroups, S.order, S.nquads = img['nrb'], G, order, img['nquads']
         S.group_col = self.t['group_col'].data_ptr()
@@ -678,17 +692,19 @@ class BBEngine:
         self.scaled = colv is not None
         # tile layouts (K1, K2): the dealt images (column-sorted gathers, LDS
         # atomic sums: the same sums to rounding, not run-to-run bit-identical;
-        # C5 K1 1334 -> 374 us, K2 984 -> 503 us) unless `deterministic`, which
-        # keeps the thread streams (every row summed in CSR order: K2
-        # bit-identical to SciPy with one group).  BSLS_TILE_LAYOUT="a,at" overrides.
+        # C5 K1 1334 -> 374 us, K2 984 -> 503 us), with 3-byte entries (layout
+        # 2: C5 K1 359 -> 331, K2 358 -> 345 us against 4-byte layout 1)
+        # unless `deterministic`, which keeps the thread streams (every row
+        # summed in CSR order: K2 bit-identical to SciPy with one group).
+        # BSLS_TILE_LAYOUT="a,at" overrides.
         if tile_layouts is None:
             env = os.environ.get('BSLS_TILE_LAYOUT')
             tile_layouts = (tuple(int(v) for v in env.split(',')) if env
-                            else ((0, 0) if deterministic else (1, 1)))
+                            else ((0, 0) if deterministic else (2, 2)))
         self.tile_layouts = tile_layouts
         # per matrix: panels or streamed tiles (spmv_format)
-        self.fmt_A = spmv_format(A, fmt, dealt=tile_layouts[0] == 1)
-        self.fmt_AT = spmv_format(AT, fmt, dealt=tile_layouts[1] == 1)
+        self.fmt_A = spmv_format(A, fmt, dealt=tile_layouts[0] in (1, 2))
+        self.fmt_AT = spmv_format(AT, fmt, dealt=tile_layouts[1] in (1, 2))
         self.A_pan = self.AT_pan = self.A_til = self.AT_til = None
         if self.fmt_A == 'panels':
             prow, groups = k1_plan(self.m)

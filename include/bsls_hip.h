@@ -225,7 +225,8 @@ typedef struct bsls_tiles {
     const int64_t *wave_off;        /* layout 0: nrb * ngroups * 16 + 1 (in quads); 1: see above */
     const uint32_t *ent;
     const double *val;              /* 4 * nquads, or NULL (scaled incidence) */
-    int64_t layout;                 /* 0: thread streams (CSR order per row), 1: dealt;
+    int64_t layout;                 /* 0: thread streams (CSR order per row), 1: dealt,
+                                       2: dealt with 3-byte entries;
                                        | BSLS_TILE_NT: dealt, entries by non-temporal loads */
     const int32_t *base;            /* layout 1: 4 * nquads / 64 instruction bases */
 } bsls_tiles;
@@ -248,6 +249,16 @@ int64_t bsls_tiles_build_dealt(int64_t rows, int64_t cols, const int64_t *indptr
                                int64_t halo, int64_t ngroups, const int64_t *group_col,
                                int64_t *wave_off_out, uint32_t *ent_out, int32_t *base_out,
                                double *val_out, int64_t nquads_cap);
+/* Layout 2: layout 1 with 3-byte entries (local row << cbits | column - base,
+ * cbits = 24 - bit_width(H + halo), instructions split where their columns
+ * would span more than 2^cbits - 1); lane l of quad-step q, wave w holds its
+ * four entries in ent[3 ((q * 16 + w) * 64 + l) + 0..2] as e0 | e1 << 24,
+ * e1 >> 8 | e2 << 16, e2 >> 16 | e3 << 8 (ent_out: 3 * count uint32). */
+int64_t bsls_tiles_build_dealt3(int64_t rows, int64_t cols, const int64_t *indptr,
+                                const int32_t *indices, const double *data, int64_t H,
+                                int64_t halo, int64_t ngroups, const int64_t *group_col,
+                                int64_t *wave_off_out, uint32_t *ent_out, int32_t *base_out,
+                                double *val_out, int64_t nquads_cap);
 
 typedef struct bsls_bb_problem {
     int64_t m, n, nz, nblocks;      /* rows, x length, z length (n - nblocks), blocks */

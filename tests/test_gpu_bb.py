@@ -79,7 +79,11 @@ FORMATS = {'panels': dict(fmt='panels'),
            'tiles': dict(fmt='tiles'),
            'tiles-det': dict(fmt='tiles', deterministic=True),
            'tiles-groups': dict(fmt='tiles', tile_plans=((1024, 4, 0), (1536, 2, 0))),
-           'tiles-mixed': dict(fmt='tiles', tile_layouts=(1, 0))}
+           'tiles-mixed': dict(fmt='tiles', tile_layouts=(1, 0)),
+           'tiles-dealt16': dict(fmt='tiles', tile_layouts=(1, 1)),
+           'tiles-dealt12': dict(fmt='tiles', tile_layouts=(2, 2)),
+           'tiles-dealt12-groups': dict(fmt='tiles', tile_layouts=(2, 2),
+                                        tile_plans=((1024, 4, 0), (1536, 2, 0)))}
 # formats whose K2 sums each row in CSR order (one group, thread streams)
 K2_EXACT = ('panels', 'tiles-det', 'tiles-mixed')
 # formats with a fixed summation order everywhere (bit-reproducible runs)

@@ -41,10 +41,10 @@ def test_c5_takes_the_tile_kernels(c5):
 
 
 def test_c5_k2_vs_scipy(c5):
-    """The default (dealt) K2: LDS atomic sums, equal to SciPy to rounding."""
+    """The default (dealt, 3-byte entries) K2: LDS atomic sums, equal to SciPy to rounding."""
     import torch
     sh, _, eng = c5
-    assert eng.AT_til.img['layout'] == 1
+    assert eng.AT_til.img['layout'] == 2
     r = np.random.RandomState(5).randn(eng.m)
     eng.r.copy_(torch.from_numpy(r))
     eng.stage(3, 0)

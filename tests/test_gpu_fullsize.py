@@ -31,7 +31,7 @@ def c3(cuda):
     b = add_noise(sh['Ax'], 0.02, seed=SEED)
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 3, 'opt_tol': 1e-30},
                    AT=sh['AT'])
-    assert eng.fmt_A == eng.fmt_AT == 'tiles' and eng.tile_layouts == (1, 1)
+    assert eng.fmt_A == eng.fmt_AT == 'tiles' and eng.tile_layouts == (2, 2)
     return sh, b, eng
 
 

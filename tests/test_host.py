@@ -331,7 +331,7 @@ def test_panel_overflow_is_typed():
     assert issubclass(device.PanelOverflow, ValueError)
 
 
-@pytest.mark.parametrize('layout', [0, 1])
+@pytest.mark.parametrize('layout', [0, 1, 2])
 @pytest.mark.parametrize('halo', [0, 1])
 @pytest.mark.parametrize('values', [True, False])
 def test_tile_images_restate_scipy(layout, halo, values):
@@ -348,8 +348,10 @@ def test_tile_images_restate_scipy(layout, halo, values):
     A.data = rs.randn(A.nnz) if values else np.ones(A.nnz)
     gc = np.round(np.linspace(0, n, 4)).astype(np.int64)
     H = 1500
-    build = _native.tiles_build_dealt if layout else _native.tiles_build
-    img = build(A, H, halo, gc, values=values)
+    if layout:
+        img = _native.tiles_build_dealt(A, H, halo, gc, values=values, packed=layout == 2)
+    else:
+        img = _native.tiles_build(A, H, halo, gc, values=values)
     img.update(rows=m, cols=n, H=H, halo=halo, ngroups=3, order=0, group_col=gc, layout=layout)
     x = rs.randn(n)
     got = device.tiles_matvec(img, x)
@@ -359,5 +361,14 @@ def test_tile_images_restate_scipy(layout, halo, values):
         # every entry once: the non-dummy entries count nnz (+ halo copies)
         e = img['ent'][:4 * img['nquads']].astype(np.int64)
         live = int(np.sum((e >> 16) != H + halo))
+        extra = sum(int(A.indptr[r + 1] - A.indptr[r]) for r in range(H, m, H)) if halo else 0
+        assert live == A.nnz + extra
+    if layout == 2:
+        # 3 words per 4 entries, rows above 24 - bit_width(H + halo) column bits
+        w = img['ent'][:3 * img['nquads']].astype(np.int64).reshape(-1, 3)
+        e = np.stack([w[:, 0] & 0xFFFFFF, (w[:, 0] >> 24) | ((w[:, 1] & 0xFFFF) << 8),
+                      (w[:, 1] >> 16) | ((w[:, 2] & 0xFF) << 16), w[:, 2] >> 8], 1)
+        cb = 24 - int(H + halo).bit_length()
+        live = int(np.sum((e >> cb) != H + halo))
         extra = sum(int(A.indptr[r + 1] - A.indptr[r]) for r in range(H, m, H)) if halo else 0
         assert live == A.nnz + extra
