@@ -507,8 +507,10 @@ class DeviceTiles:
         S = _native.Tiles()
         # dealt images larger than the Infinity Cache stream their entries
         # non-temporally (csrc/tiles.hpp tq_load)
-        S.layout = layout | (_native.TILE_NT if layout in (1, 2) and self_bytes(img) > NT_BYTES
-                             else 0)
+        nt = self_bytes(img) > NT_BYTES
+        if os.environ.get('BSLS_TILE_NT'):          # A/B override of the policy
+            nt = os.environ['BSLS_TILE_NT'] == '1'
+        S.layout = layout | (_native.TILE_NT if layout in (1, 2) and nt else 0)
         S.base = self.t['base'].data_ptr() if layout in (1, 2) else None
         S.rows, S.cols, S.H, S.halo = R, C, H, halo
         S.nrb, S.ngroups, S.order, S.nquads = img['nrb'], G, order, img['nquads']
