@@ -588,6 +588,9 @@ __device__ __forceinline__ void wt_store_f64(const __amdgpu_buffer_rsrc_t &rs, i
         __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, v), rs, off, 0, 16);
 }
 
+#ifndef BSLS_K3_SGPRS
+#define BSLS_K3_SGPRS 80
+#endif
 #ifndef BSLS_DZ_PLAIN
 #define BSLS_DZ_PLAIN 0   // 1: dz through an ordinary store (A/B variant)
 #endif
@@ -596,8 +599,11 @@ __device__ __forceinline__ void wt_store_f64(const __amdgpu_buffer_rsrc_t &rs, i
 // issues every load of all of them -- metadata, then z, g and the column
 // scales -- before the first PAVA.  MERGE (K3_PPW = 2): the two packs' PAVA
 // share the wave after their first passes (pava_v1_wave_pair).
+// (at most 80 SGPRs: 256-thread blocks are admitted 8 per CU only up to 80,
+// MI355X_MICROARCH.md "Residency"; the merged form otherwise takes 83 and 7)
 template <int K3_PPW, bool MERGE>
-__global__ __launch_bounds__(256) void bb_k3(bsls_bb_problem P, int64_t iter,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(BSLS_K3_SGPRS)))
+void bb_k3(bsls_bb_problem P, int64_t iter,
                                              const double *__restrict__ zc,
                                              const double *__restrict__ g,
                                              double *__restrict__ zn,
