@@ -118,6 +118,21 @@ __device__ __forceinline__ double dpp_shr1_d(double v) {
     const int hi = dpp_shr1_i(__double2hiint(v));
     return __hiloint2double(hi, lo);
 }
+// the same shift with bound_ctrl (lane 0 reads 0) and no `old` operand: one
+// v_mov_b32_dpp per dword, no zero-initialised destination (wave_pass only
+// reads the shifted value on lanes >= 1)
+__device__ __forceinline__ int dpp_shr1_bc_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ double dpp_shr1_bc_d(double v) {
+    const int lo = dpp_shr1_bc_i(__double2loint(v));
+    const int hi = dpp_shr1_bc_i(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+// ballot of a bool computed with bitwise operators under the full exec mask
+// (HIP's __ballot(int) after a short-circuit && materialises the predicate
+// through a branch, a v_cndmask and a v_cmp)
+__device__ __forceinline__ uint64_t ballot_b(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -139,11 +154,13 @@ __device__ __forceinline__ WaveRuns wave_runs(double y, int L, uint64_t B, int o
 // pools, else the pooled chains merged and the survivors packed into lanes
 // 0 .. nh-1.  ys / ps / cst: this wave's 64 doubles / 64 ints / 65 ints of LDS.
 __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int *cst) {
+    // (predicates with bitwise operators: no branches, ballots straight from
+    // the compares; the scan counter is wave-uniform)
     const int t = lane_id();
     const bool act = t < s.nh;
-    const double yp = dpp_shr1_d(s.Y);
-    const bool cs = act && (s.BS || !(s.Y <= yp));     // lane 0 is always a block start
-    const uint64_t CS = __ballot(cs);
+    const double yp = dpp_shr1_bc_d(s.Y);
+    const bool cs = act & ((s.BS != 0) | !(s.Y <= yp));   // lane 0 is always a block start
+    const uint64_t CS = ballot_b(cs);
     // chain c of this lane (lanes >= nh: the last chain, unused); the
     // table holds every chain's first run, then nh
     const int c = mbcnt64(CS) - (cs ? 0 : 1);
@@ -155,21 +172,33 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
     const double ylast = shfl_d(s.Y, last);
     // the chain pools iff its first and last values differ (the reference's
     // y[i] != y[j]); every member sees both
-    const bool inpool = act && (yfirst != ylast);
-    const bool pool = cs && inpool;
-    if (!__ballot(pool)) return false;
+    const bool inpool = act & (yfirst != ylast);
+    const bool pool = cs & inpool;
+    if (!ballot_b(pool)) return false;
     const int depth = t - mycs;
     const double pr = s.Y * (double)s.W;
     double num = 0.0 + pr;
     int den = s.W;
     // k = 1 .. the deepest pooled member (a ballot per step instead of a
-    // six-round shuffle max up front: 2-4 steps are typical)
-    for (int k = 1; __ballot(inpool && depth >= k); ++k) {
-        const double np = dpp_shr1_d(num);
-        const int dp = dpp_shr1_i(den);
-        const bool upd = inpool && depth == k;
-        num = upd ? np + pr : num;
-        den = upd ? dp + s.W : den;
+    // six-round shuffle max up front: 2-4 steps are typical).  Every member
+    // at depth >= k steps at k: after step k such a lane holds the left fold
+    // ((0 + pr[t-k]) + pr[t-k+1]) + ... + pr[t] (by induction: lane t - 1,
+    // at depth >= k - 1, held the fold over [t-k, t-1]), so at the end a
+    // member at depth d holds the fold from its chain's first run -- the
+    // reference's order.  The step test is the loop test (one compare per
+    // step, no select on depth == k).  Lanes at depth >= 1 read lane t - 1
+    // >= 0, so the bound_ctrl zero at lane 0 is never used; the shifts run
+    // under the full exec mask (DPP reads of disabled lanes return 0).
+    const int dk = inpool ? depth : 0;
+    for (int k = 1;; ++k) {
+        const bool step = dk >= k;
+        if (!ballot_b(step)) break;
+        const double np = dpp_shr1_bc_d(num);
+        const int dp = dpp_shr1_bc_i(den);
+        if (step) {
+            num = np + pr;
+            den = dp + s.W;
+        }
     }
     const double tn = shfl_d(num, last);
     const int td = shfl_i(den, last);
@@ -178,8 +207,8 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
         s.W = td;
     }
     // pack the surviving runs into lanes 0 .. nh-1
-    const bool surv = act && !(inpool && depth > 0);
-    const uint64_t S = __ballot(surv);
+    const bool surv = act & !(dk > 0);
+    const uint64_t S = ballot_b(surv);
     if (surv) {
         const int idx = mbcnt64(S);
         ys[idx] = s.Y;
