@@ -495,16 +495,27 @@ def roofline_of(kern, traffic_file=None, config=None):
     workload), None when absent."""
     names = [k for k in kern if k != 'formats']
     dom = max(names, key=lambda k: kern[k]['avg_us'])
-    traffic = None
+    per = {}
     if traffic_file and os.path.exists(traffic_file):
         try:
-            traffic = (json.load(open(traffic_file)).get(config, {}).get(dom, {})
-                       .get('hbm_bytes_per_launch'))
+            per = json.load(open(traffic_file)).get(config, {})
         except Exception:
-            traffic = None
+            per = {}
+    # physical rate next to the algorithmic one: the PMC bytes of each kernel
+    # over this run's average launch time (the bytes the images, gathers and
+    # partials really move, C5 images beyond the Infinity Cache)
+    for k in names:
+        tb = per.get(k, {}).get('hbm_bytes_per_launch')
+        if tb:
+            kern[k]['pmc_bytes'] = tb
+            kern[k]['pmc_GB_s'] = tb / (kern[k]['avg_us'] * 1e-6) / 1e9
+    traffic = per.get(dom, {}).get('hbm_bytes_per_launch')
     return {'bound': 'hbm', 'kernel': dom, 'achieved': kern[dom]['GB_s'],
             'peak': HBM_PEAK / 1e9, 'unit': 'GB/s', 'frac': kern[dom]['frac'],
-            'traffic': traffic, 'traffic_source': traffic_file and os.path.basename(traffic_file)}
+            'traffic': traffic, 'traffic_source': traffic_file and os.path.basename(traffic_file),
+            'physical_GB_s': kern[dom].get('pmc_GB_s'),
+            'physical_frac': (kern[dom]['pmc_GB_s'] * 1e9 / HBM_PEAK
+                              if kern[dom].get('pmc_GB_s') else None)}
 
 
 def host_info(threads):
