@@ -109,24 +109,15 @@ __device__ __forceinline__ void pava_v1_wave(double &y, int &w, int L, uint64_t 
 // Checked bit-for-bit against the reference PAVA (oracle) in
 // tests/test_gpu_bb.py::test_k3_wave_pava_bit_exact.
 
-// lane l - 1's value (lane 0: 0), DPP wave_shr:1
+// lane l - 1's value, DPP wave_shr:1 with bound_ctrl (lane 0 reads 0) and
+// no `old` operand: one v_mov_b32_dpp per dword, no zero-initialised
+// destination (wave_pass only uses the shifted value on lanes >= 1)
 __device__ __forceinline__ int dpp_shr1_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false);
+    return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);
 }
 __device__ __forceinline__ double dpp_shr1_d(double v) {
     const int lo = dpp_shr1_i(__double2loint(v));
     const int hi = dpp_shr1_i(__double2hiint(v));
-    return __hiloint2double(hi, lo);
-}
-// the same shift with bound_ctrl (lane 0 reads 0) and no `old` operand: one
-// v_mov_b32_dpp per dword, no zero-initialised destination (wave_pass only
-// reads the shifted value on lanes >= 1)
-__device__ __forceinline__ int dpp_shr1_bc_i(int v) {
-    return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);
-}
-__device__ __forceinline__ double dpp_shr1_bc_d(double v) {
-    const int lo = dpp_shr1_bc_i(__double2loint(v));
-    const int hi = dpp_shr1_bc_i(__double2hiint(v));
     return __hiloint2double(hi, lo);
 }
 // ballot of a bool computed with bitwise operators under the full exec mask
@@ -158,7 +149,7 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
     // the compares; the scan counter is wave-uniform)
     const int t = lane_id();
     const bool act = t < s.nh;
-    const double yp = dpp_shr1_bc_d(s.Y);
+    const double yp = dpp_shr1_d(s.Y);
     const bool cs = act & ((s.BS != 0) | !(s.Y <= yp));   // lane 0 is always a block start
     const uint64_t CS = ballot_b(cs);
     // chain c of this lane (lanes >= nh: the last chain, unused); the
@@ -193,8 +184,8 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
     for (int k = 1;; ++k) {
         const bool step = dk >= k;
         if (!ballot_b(step)) break;
-        const double np = dpp_shr1_bc_d(num);
-        const int dp = dpp_shr1_bc_i(den);
+        const double np = dpp_shr1_d(num);
+        const int dp = dpp_shr1_i(den);
         if (step) {
             num = np + pr;
             den = dp + s.W;
