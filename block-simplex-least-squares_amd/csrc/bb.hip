@@ -437,18 +437,22 @@ __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t it
                                                    unsigned *ticket) {
     __shared__ double red[4];
     if (iter > 0 && P.scal[BSLS_S_STOP] != 0.0) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // grid-stride over at most R_FINISH_GRID workgroups (the launch below):
+    // one workgroup per 256 rows made 3.9k ticket arrivals at m = 1M, ~20 us
+    // for 24 MB in the 8-way rehearsal
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
     double sq[1] = {0.0};
-    if (i < P.m) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.m; i += gs) {
         const double o = P.r[i] + P.target[i];
         P.r[i] = o;
-        sq[0] = o * o;
+        sq[0] += o * o;
     }
     block_sum<1>(sq, red);
     double tot[1];
     if (last_block_sum<1>(sq, part, ticket, tot, red) && threadIdx.x == 0)
         bb_record_f(P, iter, tot[0], iter > 0);
 }
+constexpr int R_FINISH_GRID = 512;
 
 // K2: g = N'(A' r); with ITER also dg = g - g_prev and the BB sums.  The
 // workgroup's 16 panels (x-rows) are summed over every chunk of r; then lane
@@ -1177,7 +1181,8 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
             else launch_k1<false, false, false>(P, iter, w, st);
             break;
         case 2:  // r += target, ||r||^2, stop test
-            bb_r_finish<<<grid_for(P.m, 256), 256, 0, st>>>(P, iter, w.pf, w.tkf);
+            bb_r_finish<<<(grid_for(P.m, 256) < R_FINISH_GRID ? grid_for(P.m, 256) : R_FINISH_GRID),
+                          256, 0, st>>>(P, iter, w.pf, w.tkf);
             break;
         case 3:  // g = N'A'r (+ sums)
             if (iter > 0) launch_k2<true>(P, P.g[zc], P.g[zn], w, st);
