@@ -39,7 +39,12 @@ for _p in (ROOT, PKG):
 
 import numpy as np  # noqa: E402
 
-METRIC = 'BB solver iterations/sec (1M-route block-LSQ) + proj_simplex HBM GB/s'
+# BASELINE.json's metric names the 1M-route problem (C3); the headline `value`
+# here is the north star's 10M-route problem (C5, BASELINE configs[4]), the one
+# its 8-GPU target is quoted on and the one bench.py scales over N GPUs, so the
+# metric text says which; the C3 rate is the line's "c3" entry (N = 1).
+METRIC = ('BB solver iterations/sec (10M-route block-LSQ, BASELINE configs[4]; '
+          '1M-route rate in "c3") + proj_simplex HBM GB/s')
 HBM_PEAK = 8.0e12   # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -243,10 +248,23 @@ def bench_xspace(sh, b, rounds=40, reps=5):
         ok = ok and bool(np.isfinite(s[_native.XS_F]))
     torch.cuda.synchronize()
     ms = sum(ev[2 * k].elapsed_time(ev[2 * k + 1]) for k in range(reps))
+    A = sh['A']
+    m, n, nnz, p = A.shape[0], A.shape[1], A.nnz, len(sizes)
+    # SURVEY 8(d)-style general-CSR bytes of a round (csrc/xbb.hip): residual
+    # 12 nnz + 4 (m+1) + 8 n + 16 m, gradient 12 nnz + 4 (n+1) + 8 m + 8 n, the
+    # finish's four vectors 32 n; a STEP round adds the step (x_new, g_new in,
+    # x, g, x_new out: 40 n) and the projection 16 n + 4 (p+1), a BACKTRACK
+    # round its blend (24 n)
+    nr = rounds * reps
+    common = 24 * nnz + 4 * (m + n + 2) + 24 * m + 16 * n + 32 * n
+    byt = nr * common + (nr - bts) * (40 * n + 16 * n + 4 * (p + 1)) + bts * 24 * n
     return {'operator': 'panels' if obj.lsq is not None else 'csr',
-            'rounds': rounds * reps, 'us_per_round': ms * 1e3 / (rounds * reps),
-            'rounds_per_s': rounds * reps / (ms * 1e-3), 'iterations_per_s': its / (ms * 1e-3),
-            'backtracks': bts, 'finite': ok}
+            'rounds': nr, 'us_per_round': ms * 1e3 / nr,
+            'rounds_per_s': nr / (ms * 1e-3), 'iterations_per_s': its / (ms * 1e-3),
+            'backtracks': bts, 'finite': ok,
+            'roofline': {'bound': 'hbm', 'alg_bytes_per_round': byt / nr,
+                         'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK / 1e9,
+                         'unit': 'GB/s', 'frac': byt / (ms * 1e-3) / HBM_PEAK}}
 
 
 def bench_dore(sh, b, iters=30):
@@ -320,10 +338,20 @@ def bench_md(sh, b, iters=30):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
     x = md.x.cpu().numpy()
+    A = sh['A']
+    m, n, nnz, p = A.shape[0], A.shape[1], A.nnz, len(sh['block_sizes'])
+    # general-CSR bytes per iteration: residual 12 nnz + 4 (m+1) + 8 n + 16 m,
+    # gradient 12 nnz + 4 (n+1) + 8 m + 8 n, the update (x, g in, x out) 24 n +
+    # 4 (p+1)
+    byt = 24 * nnz + 4 * (m + n + 2) + 24 * m + 16 * n + 24 * n + 4 * (p + 1)
+    us = ms * 1e3 / iters
     return {'operator': 'panels' if md.lsq is not None else 'csr', 'scale': 0.01,
             'iterations': iters,
-            'us_per_iter': ms * 1e3 / iters, 'iterations_per_s': iters / (ms * 1e-3),
-            'finite': bool(np.all(np.isfinite(x)))}
+            'us_per_iter': us, 'iterations_per_s': iters / (ms * 1e-3),
+            'finite': bool(np.all(np.isfinite(x))),
+            'roofline': {'bound': 'hbm', 'alg_bytes_per_iter': byt,
+                         'achieved': byt / (us * 1e-6) / 1e9, 'peak': HBM_PEAK / 1e9,
+                         'unit': 'GB/s', 'frac': byt / (us * 1e-6) / HBM_PEAK}}
 
 
 def bench_iso(reps=3, batch=16):
@@ -484,9 +512,24 @@ def kernel_table(eng, it0, reps, world, m, n, nz, p, nnz):
         us = ev[0].elapsed_time(ev[1]) * 1e3 / reps
         kern[nm] = {'avg_us': us, 'alg_bytes': kb[nm], 'GB_s': kb[nm] / (us * 1e-6) / 1e9,
                     'frac': kb[nm] / (us * 1e-6) / HBM_PEAK, 'format_bytes': fb[nm],
-                    'format_GB_s': fb[nm] / (us * 1e-6) / 1e9}
+                    'format_GB_s': fb[nm] / (us * 1e-6) / 1e9,
+                    'format_frac': fb[nm] / (us * 1e-6) / HBM_PEAK,
+                    'rocprof_kernels': rocprof_names(eng, nm, world)}
     kern['formats'] = {'K1': eng.fmt_A, 'K2': eng.fmt_AT}
     return kern
+
+
+def rocprof_names(eng, nm, world):
+    """The kernel names (rocprofv3 'Kernel_Name' prefixes) one stage launch of
+    `nm` runs: the rows of profiles/*_kernel_stats.csv its avg_us is the sum
+    of."""
+    if nm == 'K3_pava_clip_z2x':
+        return ['bb_k3']
+    if nm == 'K2_spmvT_Nt_dots':
+        return ['bb_k2t' if eng.AT_til is not None else 'bb_k2']
+    if eng.A_til is not None:
+        return ['bb_k1t'] + (['bb_k1_sum'] if eng.A_til.img['ngroups'] > 1 else [])
+    return ['bb_k1']
 
 
 def roofline_of(kern, traffic_file=None, config=None):
@@ -510,12 +553,18 @@ def roofline_of(kern, traffic_file=None, config=None):
             kern[k]['pmc_bytes'] = tb
             kern[k]['pmc_GB_s'] = tb / (kern[k]['avg_us'] * 1e-6) / 1e9
     traffic = per.get(dom, {}).get('hbm_bytes_per_launch')
-    return {'bound': 'hbm', 'kernel': dom, 'achieved': kern[dom]['GB_s'],
+    return {'bound': 'hbm', 'kernel': dom, 'rocprof_kernels': kern[dom].get('rocprof_kernels'),
+            'avg_us': kern[dom]['avg_us'], 'alg_bytes': kern[dom]['alg_bytes'],
+            'achieved': kern[dom]['GB_s'],
             'peak': HBM_PEAK / 1e9, 'unit': 'GB/s', 'frac': kern[dom]['frac'],
+            'format_bytes': kern[dom]['format_bytes'], 'format_frac': kern[dom]['format_frac'],
             'traffic': traffic, 'traffic_source': traffic_file and os.path.basename(traffic_file),
             'physical_GB_s': kern[dom].get('pmc_GB_s'),
             'physical_frac': (kern[dom]['pmc_GB_s'] * 1e9 / HBM_PEAK
-                              if kern[dom].get('pmc_GB_s') else None)}
+                              if kern[dom].get('pmc_GB_s') else None),
+            'note': 'frac = SURVEY 8(d) general-CSR bytes / avg_us / 8 TB/s; format_frac = '
+                    'the bytes the compressed images stream; physical_frac = PMC '
+                    'FETCH+WRITE bytes (traffic) / avg_us'}
 
 
 def host_info(threads):
@@ -533,6 +582,16 @@ def host_info(threads):
             'OPENBLAS_NUM_THREADS': os.environ.get('OPENBLAS_NUM_THREADS')}
 
 
+LEGS = ('main', 'c3', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'cpu')
+
+
+def traffic_file():
+    """The newest PMC traffic summary under profiles/ (tools/traffic.py)."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'traffic_r*.json')))
+    return fs[-1] if fs else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -540,17 +599,24 @@ def main():
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--workload', default='C5', choices=['C5', 'C3'])
     ap.add_argument('--parts', type=int, default=1,
-                    help='row parts of the pipelined residual all-reduce (N > 1); 1 = one K1 '
-                         'launch then one all-reduce: rehearsed on one GPU (--rehearse-shard 8), '
-                         '4 parts cost 457 us per iteration against 207 for 1 -- a part of K1 '
-                         'is a quarter of the grid, the GPU is not filled')
+                    help='row parts of the pipelined residual all-reduce (N > 1)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-extras', action='store_true', help='skip the C3 / C2 / x-space / MD legs')
+    ap.add_argument('--no-extras', action='store_true', help='only the headline workload')
+    ap.add_argument('--legs', default='all',
+                    help='comma list of %s (N = 1; default all): one rocprofv3 run per leg '
+                         'keeps each workload\'s kernel rows apart' % ','.join(LEGS))
     ap.add_argument('--profile-iters', type=int, default=20)
     ap.add_argument('--rehearse-shard', type=int, default=0,
                     help='one GPU, one process: time rank 0 of an N-way C5 partition through '
                          'the sharded (RCCL) driver -- per-rank cost without the fabric')
     args = ap.parse_args()
+    legs = set(LEGS) if args.legs == 'all' else set(args.legs.split(','))
+    if legs - set(LEGS):
+        raise SystemExit('unknown legs %s' % sorted(legs - set(LEGS)))
+    if args.no_extras:
+        legs = {'main'}
+    if args.no_cpu_baseline:
+        legs.discard('cpu')
 
     import torch
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -558,6 +624,8 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    if world > 1 or args.rehearse_shard:
+        legs = {'main'}
     # (modulo: the gloo rehearsal puts several ranks on one GPU)
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -574,105 +642,128 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    tfile = traffic_file()
+    out = {} if rank == 0 else None
     wl = args.workload
-    sh, b = build_problem(wl, world, rank, dist, shard_of=args.rehearse_shard or None)
-    log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
-        % (wl, rank, world, sh['n'], sh['p'], sh['m'], sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
-    eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(args.rehearse_shard))
-    log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
-    el = time_run(run, args.steps, args.warmup, dist)
-    it_s = args.steps / el
-    finite = bool(np.isfinite(eng.scalars()[4]))
-    log('%d iterations in %.3f s: %.1f it/s' % (args.steps, el, it_s))
-    m, n_g, nz_g, p_g, nnz_g = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
-    kern = {}
-    if args.profile_iters > 0 and rank == 0:
-        kern = kernel_table(eng, 1 + args.warmup + args.steps, args.profile_iters, world,
-                            m, n_g, nz_g, p_g, nnz_g)
-        log('kernel table done')
-    if dist:
-        dist.barrier()
-
-    out = None
-    if rank == 0:
-        n_tot, p_tot = sh['n_total'], sh['p_total']
-        nnz_tot = 16 * n_tot
-        ib = survey_iter_bytes(m, n_tot, n_tot - p_tot, nnz_tot)
-        tfile = os.path.join(ROOT, 'profiles', 'traffic_r02.json')
-        out = {
-            'metric': METRIC, 'value': it_s,
-            'unit': 'BB iterations/s of the whole job (%s: %d routes / %d blocks / %d links)'
-                    % (wl, n_tot, p_tot, m),
-            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': '%s: BB (z-space, PAVA projection) on %d routes / %d blocks / '
-                                   '%d links / %d nnz, column-sharded over %d GPU(s)'
-                                   % (wl, n_tot, p_tot, m, nnz_tot, world),
-                       'routes': n_tot, 'blocks': p_tot, 'links': m, 'nnz': nnz_tot,
-                       'routes_rank0': n_g, 'nnz_rank0': nnz_g,
-                       'parallelism': 'column-shard x%d' % world,
-                       'residual_allreduce_parts': args.parts if world > 1 else None},
-            'roofline': roofline_of(kern, tfile, wl) if kern else None,
-            'iteration_roofline': {'survey_bytes_per_iter': ib, 'achieved_GB_s': ib * it_s / 1e9,
-                                   'frac': ib * it_s / HBM_PEAK,
-                                   'note': 'whole job over all GPUs; peak is one GPU'},
-            'kernels': kern, 'finite': finite,
-        }
-    # --- N = 1 extras: the BASELINE metric's C3 problem and the other legs ---------
-    if args.rehearse_shard and out is not None:
-        out['config']['rehearsal'] = ('rank 0 of a %d-way C5 partition on one GPU through the '
-                                      'sharded driver (RCCL with one rank: no fabric)'
-                                      % args.rehearse_shard)
-    if world == 1 and not args.no_extras and not args.rehearse_shard:
+    if 'main' in legs:
+        sh, b = build_problem(wl, world, rank, dist, shard_of=args.rehearse_shard or None)
+        log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
+            % (wl, rank, world, sh['n'], sh['p'], sh['m'],
+               sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
+        eng, run = build_engine(sh, b, world, dist, args.parts,
+                                sharded=bool(args.rehearse_shard))
+        log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
+        el = time_run(run, args.steps, args.warmup, dist)
+        it_s = args.steps / el
+        finite = bool(np.isfinite(eng.scalars()[4]))
+        log('%d iterations in %.3f s: %.1f it/s' % (args.steps, el, it_s))
+        m, n_g, nz_g, p_g, nnz_g = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
+        kern = {}
+        if args.profile_iters > 0 and rank == 0:
+            kern = kernel_table(eng, 1 + args.warmup + args.steps, args.profile_iters, world,
+                                m, n_g, nz_g, p_g, nnz_g)
+            log('kernel table done')
+        if dist:
+            dist.barrier()
+        if rank == 0:
+            n_tot, p_tot = sh['n_total'], sh['p_total']
+            nnz_tot = 16 * n_tot
+            ib = survey_iter_bytes(m, n_tot, n_tot - p_tot, nnz_tot)
+            key = ('%s_x%d' % (wl, args.rehearse_shard)) if args.rehearse_shard else wl
+            out.update({
+                'metric': METRIC, 'value': it_s,
+                'unit': 'BB iterations/s of the whole job (%s: %d routes / %d blocks / %d links)'
+                        % (wl, n_tot, p_tot, m),
+                'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+                'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
+                'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
+                'config': {'workload': '%s: BB (z-space, PAVA projection) on %d routes / %d '
+                                       'blocks / %d links / %d nnz, column-sharded over %d GPU(s)'
+                                       % (wl, n_tot, p_tot, m, nnz_tot, world),
+                           'routes': n_tot, 'blocks': p_tot, 'links': m, 'nnz': nnz_tot,
+                           'routes_rank0': n_g, 'nnz_rank0': nnz_g,
+                           'parallelism': 'column-shard x%d' % world,
+                           'residual_allreduce_parts': args.parts if world > 1 else None},
+                'roofline': roofline_of(kern, tfile, key) if kern else None,
+                'iteration_roofline': {'survey_bytes_per_iter': ib,
+                                       'achieved_GB_s': ib * it_s / 1e9,
+                                       'frac': ib * it_s / HBM_PEAK,
+                                       'note': 'whole job over all GPUs; peak is one GPU'},
+                'kernels': kern, 'finite': finite,
+                'profiles': 'profiles/r03_%s_kernel_stats.csv' % key,
+            })
+            if args.rehearse_shard:
+                out['config']['rehearsal'] = ('rank 0 of a %d-way C5 partition on one GPU through '
+                                              'the sharded driver (RCCL with one rank: no fabric)'
+                                              % args.rehearse_shard)
         del eng, run
         torch.cuda.empty_cache()
-        sh3, b3 = build_problem('C3', 1, 0, None)
-        eng3, run3 = build_engine(sh3, b3, 1, None, 1)
-        el3 = time_run(run3, max(args.steps, 50), args.warmup, None)
-        its3 = max(args.steps, 50) / el3
-        c = sh3['A']
-        kern3 = kernel_table(eng3, 1 + args.warmup + max(args.steps, 50), 50, 1,
-                             eng3.m, eng3.n, eng3.nz, eng3.layout.p, c.nnz)
-        ib3 = survey_iter_bytes(eng3.m, eng3.n, eng3.nz, c.nnz)
-        log('C3: %.1f it/s' % its3)
-        out['c3'] = {'value': its3, 'unit': 'BB iterations/s (C3: 1M routes / 50k blocks / '
-                                            '100k links / 16M nnz, 1 GPU)',
-                     'ms_per_step': el3 / max(args.steps, 50) * 1e3, 'kernels': kern3,
-                     'roofline': roofline_of(kern3, os.path.join(ROOT, 'profiles',
-                                                                 'traffic_r02.json'), 'C3'),
-                     'iteration_roofline': {'survey_bytes_per_iter': ib3,
-                                            'achieved_GB_s': ib3 * its3 / 1e9,
-                                            'frac': ib3 * its3 / HBM_PEAK}}
-        del eng3, run3
-        out['c3_stored_values'] = bench_stored_values(sh3, b3, max(args.steps, 50), args.warmup)
-        torch.cuda.empty_cache()
-        out['proj_simplex'] = bench_proj()
-        log('C2 projection done')
-        out['isotonic'] = bench_iso()
-        out['xspace_bb'] = bench_xspace(sh3, b3)
-        out['mirror_descent'] = bench_md(sh3, b3)
-        out['dore'] = bench_dore(sh3, b3)
-        log('extras done')
-        if not args.no_cpu_baseline:
-            cps, cit, cel = cpu_baseline_bb(sh3['A'], b3, sh3['block_sizes'])
-            aps, ait, ael = cpu_baseline_bb_omp(sh3['A'], b3, sh3['block_sizes'], HOST_THREADS)
-            out['cpu_baseline'] = {
-                'value': cps, 'unit': 'BB it/s (C3)', 'cores': 1, 'kind': 'port',
-                'sample': '%d BB iterations (%.1f s) of the C3 problem: oracle restatement of '
-                          'BB.py over SciPy csr_matvec + C PAVA' % (cit, cel),
-                'host': host_info(1),
-                'all_cores': {'value': aps, 'unit': 'BB it/s (C3)', 'cores': HOST_THREADS,
-                              'kind': 'port',
-                              'sample': '%d BB iterations (%.1f s) of the C3 problem: the BB '
-                                        'loop in C + OpenMP (oracle/bsls_cpu_bb.c)' % (ait, ael),
-                              'host': host_info(HOST_THREADS)}}
-            log('CPU baseline done')
+    # --- N = 1 legs: the BASELINE metric's C3 problem and the other paths -----------
+    if world == 1 and not args.rehearse_shard and legs - {'main'}:
+        extras(args, legs, out, tfile)
     if out is not None:
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def extras(args, legs, out, tfile):
+    import torch
+    steps3 = max(args.steps, 50)
+    sh3 = b3 = None
+    if legs & {'c3', 'c3sv', 'xspace', 'md', 'dore', 'lbfgs', 'cpu'}:
+        sh3, b3 = build_problem('C3', 1, 0, None)
+    if 'c3' in legs:
+        eng3, run3 = build_engine(sh3, b3, 1, None, 1)
+        el3 = time_run(run3, steps3, args.warmup, None)
+        its3 = steps3 / el3
+        c = sh3['A']
+        kern3 = kernel_table(eng3, 1 + args.warmup + steps3, 50, 1,
+                             eng3.m, eng3.n, eng3.nz, eng3.layout.p, c.nnz)
+        ib3 = survey_iter_bytes(eng3.m, eng3.n, eng3.nz, c.nnz)
+        log('C3: %.1f it/s' % its3)
+        out['c3'] = {'value': its3, 'unit': 'BB iterations/s (C3: 1M routes / 50k blocks / '
+                                            '100k links / 16M nnz, 1 GPU)',
+                     'ms_per_step': el3 / steps3 * 1e3, 'kernels': kern3,
+                     'roofline': roofline_of(kern3, tfile, 'C3'),
+                     'iteration_roofline': {'survey_bytes_per_iter': ib3,
+                                            'achieved_GB_s': ib3 * its3 / 1e9,
+                                            'frac': ib3 * its3 / HBM_PEAK},
+                     'profiles': 'profiles/r03_C3_kernel_stats.csv'}
+        del eng3, run3
+        torch.cuda.empty_cache()
+    if 'c3sv' in legs:
+        out['c3_stored_values'] = bench_stored_values(sh3, b3, steps3, args.warmup)
+        torch.cuda.empty_cache()
+    if 'proj' in legs:
+        out['proj_simplex'] = bench_proj()
+        log('C2 projection done')
+    if 'iso' in legs:
+        out['isotonic'] = bench_iso()
+    if 'xspace' in legs:
+        out['xspace_bb'] = bench_xspace(sh3, b3)
+    if 'md' in legs:
+        out['mirror_descent'] = bench_md(sh3, b3)
+    if 'dore' in legs:
+        out['dore'] = bench_dore(sh3, b3)
+    if 'lbfgs' in legs and 'bench_lbfgs' in globals():
+        out['lbfgs'] = bench_lbfgs(sh3, b3)
+    log('extras done')
+    if 'cpu' in legs:
+        cps, cit, cel = cpu_baseline_bb(sh3['A'], b3, sh3['block_sizes'])
+        aps, ait, ael = cpu_baseline_bb_omp(sh3['A'], b3, sh3['block_sizes'], HOST_THREADS)
+        out['cpu_baseline'] = {
+            'value': cps, 'unit': 'BB it/s (C3)', 'cores': 1, 'kind': 'port',
+            'sample': '%d BB iterations (%.1f s) of the C3 problem: oracle restatement of '
+                      'BB.py over SciPy csr_matvec + C PAVA' % (cit, cel),
+            'host': host_info(1),
+            'all_cores': {'value': aps, 'unit': 'BB it/s (C3)', 'cores': HOST_THREADS,
+                          'kind': 'port',
+                          'sample': '%d BB iterations (%.1f s) of the C3 problem: the BB '
+                                    'loop in C + OpenMP (oracle/bsls_cpu_bb.c)' % (ait, ael),
+                          'host': host_info(HOST_THREADS)}}
+        log('CPU baseline done')
 
 
 if __name__ == '__main__':

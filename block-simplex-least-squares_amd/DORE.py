@@ -106,7 +106,7 @@ def solve_engine(engine, z0, scale, target, record_every=5, log=None, options=No
                 S=torch.zeros(_native.S_COUNT, **dev), S2=torch.zeros(_native.S_COUNT, **dev),
                 dsc=torch.zeros(_native.DORE_COUNT, **dev),
                 part=torch.zeros(L.bsls_dore_work_size(nz, m), dtype=torch.uint8, device='cuda'),
-                tickets=torch.zeros(576, dtype=torch.uint8, device='cuda'))
+                tickets=torch.zeros(L.bsls_ticket_bytes(), dtype=torch.uint8, device='cuda'))
     bufs['S'][_native.S_SUMDG] = 1.0
     bufs['S'][_native.S_DZDG] = -scale      # K3: x - (-scale) g = x + linop_T(err)
     bufs['S'][_native.S_DGDG] = 1.0
@@ -134,6 +134,7 @@ def solve_engine(engine, z0, scale, target, record_every=5, log=None, options=No
             start = log(end - 1, X[end % 3].clone(), time.time() - start)
         it = end
     x = X[i % 3].clone()
-    log(i - 1, x, time.time() - start)
+    # the reference's loop variable after the loop: i - 1, or 0 when it never ran
+    log(max(i - 1, 0), x, time.time() - start)
     e.dore_scalars = bufs['dsc'].cpu().numpy()
     return x

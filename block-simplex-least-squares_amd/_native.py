@@ -150,6 +150,7 @@ _SIGS = {
     'bsls_bb_prologue': (_int, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_iterate': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _vp]),
     'bsls_dore_work_size': (_sz, [_i64, _i64]),
+    'bsls_ticket_bytes': (_sz, []),
     'bsls_dore_iterate': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(DoreState), _i64,
                                  _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),

@@ -29,8 +29,12 @@
 // Sparse row blocks (C5: 1M links, ~0.3 entries per row per panel chunk) take
 // the streamed-tile format instead of the panels for K1 and/or K2 (tiles.hpp;
 // bb_k1t / bb_k2t, chosen per matrix by the host: P.At / P.ATt).
-// Every cross-workgroup sum is reduced in a fixed order by the last-arriving
-// workgroup (bsls_common.hpp last_block_sum), so runs are bit-reproducible.
+// Every cross-workgroup sum of a reduction (the BB sums, ||r||^2) is reduced in
+// a fixed order by the last-arriving workgroup (bsls_common.hpp last_block_sum).
+// The SpMV row sums are fixed-order on the panels and the thread-stream tiles
+// (BBEngine(deterministic=True): runs bit-reproducible); the dealt tiles, the
+// default, add them with LDS atomics, so their rounding varies run to run at
+// the 1e-16 level.
 // Scalars live in device memory (scal[]); the host only polls them.
 #include "pava.hpp"
 #include "pava_long.hpp"
@@ -1155,6 +1159,8 @@ extern "C" int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state
     }
     return BSLS_OK;
 }
+
+extern "C" size_t bsls_ticket_bytes(void) { return (size_t)TICKET_BYTES; }
 
 extern "C" size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz) {
     return bb_layout(nullptr, m, n, nz).bytes;

@@ -33,15 +33,32 @@ def parser():
     p.add_argument('--eq', dest='eq', type=str, default='CP',
                    help='Type of equality constraint (CP or OD)')
     p.add_argument('--noise', dest='noise', type=float, default=None, help='Noise level')
+    p.add_argument('--deterministic', dest='deterministic', action='store_true', default=None,
+                   help='fixed-order SpMV sums (bit-reproducible runs and exit iterations); '
+                        'also BSLS_DETERMINISTIC=1')
     return p
 
 
-def build_engine(A, b, x0, block_sizes, options=None):
+def deterministic_default():
+    """BSLS_DETERMINISTIC=1 selects the fixed-order engine where no explicit
+    choice was made."""
+    import os
+    return os.environ.get('BSLS_DETERMINISTIC', '0') not in ('', '0')
+
+
+def build_engine(A, b, x0, block_sizes, options=None, deterministic=None):
+    """The device engine of solve_in_z's closures.  deterministic=True keeps
+    every SpMV row sum in a fixed order (panels / thread-stream tiles): runs are
+    bit-reproducible, so the exact-zero exit of BB.py:22 and the exit iteration
+    repeat run to run; the default (dealt tiles, LDS atomic row sums) is faster
+    and reproducible to ~1e-16."""
     from device import BBEngine
-    return BBEngine(A, b, block_sizes, options=options, x0=x0)
+    if deterministic is None:
+        deterministic = deterministic_default()
+    return BBEngine(A, b, block_sizes, options=options, x0=x0, deterministic=bool(deterministic))
 
 
-def solve_in_z(A, b, x0, N, block_sizes, method, options=None, engine=None):
+def solve_in_z(A, b, x0, N, block_sizes, method, options=None, engine=None, deterministic=None):
     """python/main.py:41-79 on the device.  N is accepted for signature
     compatibility and never used: the engine applies N / N' as per-block
     differences without materialising it."""
@@ -53,7 +70,7 @@ def solve_in_z(A, b, x0, N, block_sizes, method, options=None, engine=None):
     # (c_extensions.pyx:78 through main.py:64): every block needs >= 2 routes
     assert np.all(block_sizes >= 2)
     z0 = x2z(x0, block_sizes)
-    eng = engine or build_engine(A, b, x0, block_sizes)
+    eng = engine or build_engine(A, b, x0, block_sizes, deterministic=deterministic)
     gd = GradientDescent(z0=z0, method=method, options=options, engine=eng)
     iters, times, states = gd.run()
     import torch
@@ -144,7 +161,8 @@ def main(args=None, plot=False):
     if args.noise:
         delta = np.random.normal(scale=bb * args.noise)
         bb = bb + delta
-    eng = build_engine(AA, bb, x0, block_sizes)
+    eng = build_engine(AA, bb, x0, block_sizes,
+                       deterministic=getattr(args, 'deterministic', None))
     iters, times, states = solve_in_z(AA, bb, x0, N, block_sizes, args.method, engine=eng)
     x_last, error, output = LS_postprocess(states, x0, AA, bb, x_split, scaling=scaling,
                                            block_sizes=block_sizes, N=N, output=output,

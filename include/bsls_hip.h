@@ -376,10 +376,12 @@ typedef struct bsls_dore_state {
     double *S, *S2;        /* BSLS_S_COUNT doubles each */
     double *dsc;           /* BSLS_DORE_COUNT doubles */
     double *part;          /* bsls_dore_work_size(nz, m) bytes: reduction partials */
-    unsigned *tickets;     /* 576 zeroed bytes (nine 64-B ticket words) */
+    unsigned *tickets;     /* bsls_ticket_bytes() zeroed bytes (nine 64-B ticket words) */
     double scale, eps;
 } bsls_dore_state;
 size_t bsls_dore_work_size(int64_t nz, int64_t m);
+/* Bytes of one set of reduction tickets (bsls_dore_state.tickets). */
+size_t bsls_ticket_bytes(void);
 int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state *d, int64_t first_iter,
                       int64_t count, void *stream);
 

@@ -4,8 +4,10 @@
 //
 // TEST INFRASTRUCTURE ONLY: the resulting oracle/_ref/libbsls_ref.so pins the
 // oracle restatement (oracle/bsls_oracle.c) and may serve as bench.py's
-// "reference" CPU baseline in this container.  It never ships and never runs
-// on the GPU box (it is built only where /root/reference exists).
+// "reference" CPU baseline in this container.  It is built only where
+// /root/reference exists and is kept out of git history (.gitignore); like every
+// other built library it travels in the gpurun snapshot, but no GPU-box process
+// loads it (only the CPU pinning tests, tests/test_oracle_pinning.py, do).
 //
 // Wrapped reference symbols (python/c_extensions/):
 //   proj_simplex.h:17,37,50        isotonic_regression.h:13,61,85,95,105,157

@@ -53,6 +53,9 @@ def test_host_only_entry_points(native):
     assert L.bsls_bb_workspace_size(100_000, 1_000_000, 950_000) > 4 * 950_000
     assert L.bsls_spmv_workspace_size(8000) > 8 * 8000
     assert L.bsls_md_workspace_size(50_000) > 0
+    # nine 64-B ticket words (bsls_common.hpp TICKET_BYTES; DORE.py sizes its
+    # ticket buffer from this, not from a literal)
+    assert L.bsls_ticket_bytes() == 9 * 64
 
 
 def _c_layout(tmp_path, struct, fields):
@@ -70,7 +73,8 @@ def _c_layout(tmp_path, struct, fields):
 
 @pytest.mark.parametrize('struct,cls', [('bsls_bb_problem', 'BBProblem'), ('bsls_panels', 'Panels'),
                                         ('bsls_xbb_problem', 'XBBProblem'), ('bsls_csr', 'CSR'),
-                                        ('bsls_tiles', 'Tiles')])
+                                        ('bsls_tiles', 'Tiles'), ('bsls_dore_state', 'DoreState'),
+                                        ('bsls_lsq_op', 'LsqOp')])
 def test_struct_layout_matches_header(native, tmp_path, struct, cls):
     C = getattr(native, cls)
     names = [f[0] for f in C._fields_]

@@ -51,8 +51,9 @@ def _gd_run(G, tag, method, options):
     return eng, gd, iters, states
 
 
+@pytest.mark.parametrize('det', [False, True])
 @pytest.mark.parametrize('vi', [0, 1, 2])
-def test_main_end_to_end(cuda, golden, tmp_path, vi):
+def test_main_end_to_end(cuda, golden, tmp_path, vi, det):
     import bsls_utils
     import main
     G = golden('solvers.npz')
@@ -61,8 +62,14 @@ def test_main_end_to_end(cuda, golden, tmp_path, vi):
     fname = os.path.join(str(tmp_path), 'test_main.mat')
     bsls_utils.generate_data(fname=fname, **kw)
     args = argparse.Namespace(noise=0, file=fname, log='WARN', init=False, eq='CP',
-                              method='BB')
+                              method='BB', deterministic=det)
     iters, times, states, output = main.main(args=args)
+    if det:
+        # the fixed-order engine (main.py --deterministic): a second run repeats
+        # the first bit for bit, exit iteration included
+        iters2, _, states2, _ = main.main(args=args)
+        assert list(iters2) == list(iters)
+        assert all(np.array_equal(a, b2) for a, b2 in zip(states, states2))
     err = np.asarray(output['0.5norm(Ax-b)^2'])
     # tests/fast/test_main.py:31-47
     assert err[-1] < 1e-16, err
@@ -121,14 +128,21 @@ def test_dore_vs_reference(cuda, golden):
         assert rel(s, G['dore_states'][k]) < 1e-6, (k, iters[k])
 
 
-@pytest.mark.parametrize('eps', [-1.0, 1e30])
-def test_dore_device_loop_vs_closures(cuda, eps):
+@pytest.mark.parametrize('eps,record_every,max_iter', [(-1.0, 1, 40), (1e30, 1, 40),
+                                                      (-1.0, 7, 40), ('mid', 7, 40),
+                                                      (-1.0, 1, 0)])
+def test_dore_device_loop_vs_closures(cuda, eps, record_every, max_iter):
     """DORE.solve_engine (every step and branch on the device, what
     GradientDescent('DORE') runs) against DORE.solve over the engine's
     closures (host branch decisions) on a 60k-route problem: every logged
     iterate within 1e-8 (the dot products round in different orders), the
     extrapolated path taken, and the norm-change break (eps = 1e30: stop at
-    iteration 1 with the iterate of iteration 0) at the same iteration."""
+    iteration 1 with the iterate of iteration 0) at the same iteration.
+    record_every = 7 runs solve_engine's chunking (up to 25 iterations
+    enqueued between reads of the stop flag, log points at multiples of 7);
+    eps = 'mid' sets the threshold between two iterations' norm changes so the
+    break falls inside a chunk; max_iter = 0 logs iteration 0 with x0 twice,
+    as the reference does."""
     import torch
     import DORE
     from device import BBEngine
@@ -140,27 +154,46 @@ def test_dore_device_loop_vs_closures(cuda, eps):
     scale = 0.99 / lsv_operator(eng, None)
     tgt = eng.target * scale
     z0 = torch.zeros(eng.nz, dtype=torch.float64, device='cuda')
-    opts = {'max_iter': 40, 'opt_tol': eps}
-    runs = []
-    for fused in (False, True):
+
+    def run(fused, eps_, every):
+        opts = {'max_iter': max_iter, 'opt_tol': eps_}
         rec = []
 
         def log(i, st, dt):
             rec.append((i, st.detach().cpu().numpy().copy()))
             return 0.0
         if fused:
-            DORE.solve_engine(eng, z0, scale, tgt, record_every=1, log=log, options=opts)
+            DORE.solve_engine(eng, z0, scale, tgt, record_every=every, log=log, options=opts)
         else:
             DORE.solve(z0, lambda z: eng.apply_A(z, alpha=scale),
-                       lambda r: eng.apply_AT(r, alpha=scale), tgt, record_every=1,
+                       lambda r: eng.apply_AT(r, alpha=scale), tgt, record_every=every,
                        proj=eng.proj, log=log, options=opts)
-        runs.append(rec)
-    ref, got = runs
+        return rec
+    brk = None
+    if eps == 'mid':
+        # norm_change of iteration k = ||x_k - x_{k-1}||^2, x_k = the state logged
+        # after iteration k - 1 (entry k of a record_every = 1 run, entry 0 = x0);
+        # pick k in 16..21 (inside the chunk [15, 22)) where it drops below every
+        # earlier one and put eps between the two
+        st = [s for _, s in run(False, -1.0, 1)]
+        nc = [float(np.sum((st[k] - st[k - 1]) ** 2)) for k in range(1, len(st))]
+        for k in range(16, 22):
+            lo = min(nc[:k - 1])
+            if nc[k - 1] < 0.5 * lo:
+                brk, eps = k, float(np.sqrt(nc[k - 1] * lo))
+                break
+        assert brk is not None, nc[:25]
+    ref, got = run(False, eps, record_every), run(True, eps, record_every)
     assert [i for i, _ in got] == [i for i, _ in ref]
     for (i, a), (_, bb) in zip(got, ref):
         assert rel(a, bb) < 1e-8, i
-    if eps < 0:
+    if max_iter == 0:
+        assert [i for i, _ in got] == [0, 0]
+    elif brk is not None:
+        assert got[-1][0] == brk
+    elif eps < 0:
         assert eng.dore_scalars[3] != 0.0          # a2: the extrapolated path ran
+        assert got[-1][0] == max_iter - 1
     else:
         assert got[-1][0] == 1
 

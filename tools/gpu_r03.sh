@@ -1,0 +1,67 @@
+#!/bin/bash
+# One GPU-box session (round 3): parity tests, smoke, bench, and one rocprofv3
+# kernel-trace run per workload (profiles/r03_<key>_kernel_stats.csv), so a
+# kernel name's rows never mix workloads.  Every GPU step runs under its own
+# timeout; a crash / timeout / abort ends the script (no further GPU work), an
+# ordinary test failure (pytest rc 1) does not.
+#   STEPS="tests smoke bench prof" tools/gpu_r03.sh
+#   PROF="C5 C3 C2 C4iso md_xs C5x8" (the prof step's workloads)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+STEPS="${STEPS:-tests smoke bench prof}"
+PROF="${PROF:-C5 C3 C2 C4iso md_xs C5x8}"
+TESTS="${TESTS:-tests}"
+
+fatal() {  # timeouts (124/137), aborts (134), faults (139) and other signals end the session
+    if [ "$1" -eq 124 ] || [ "$1" -ge 128 ]; then
+        echo "step failed with rc=$1: stopping GPU work" | tee -a $OUT/status.txt; exit "$1"
+    fi
+    return 0
+}
+
+prof() {  # prof <key> <bench args...>
+    local key=$1; shift
+    rm -rf $OUT/prof_$key
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$key -o run \
+        -- python3 bench.py "$@" > $OUT/prof_$key.log 2>&1
+    local rc=$?
+    echo "prof $key rc=$rc" | tee -a $OUT/status.txt; fatal $rc
+    local f
+    f=$(find $OUT/prof_$key -name '*kernel_stats.csv' | head -n 1)
+    [ -n "$f" ] && cp "$f" $OUT/r03_${key}_kernel_stats.csv
+    return 0
+}
+
+for s in $STEPS; do
+  case "$s" in
+    tests)
+      timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread \
+          > $OUT/gpu_tests.log 2>&1
+      rc=$?; echo "tests rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    bench)
+      timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1
+      rc=$?; echo "bench rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    rehearse)
+      timeout -k 10 400 python bench.py --rehearse-shard 8 --steps 200 --warmup 20 \
+          > $OUT/rehearse8.log 2>&1
+      rc=$?; echo "rehearse rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    prof)
+      for k in $PROF; do
+        case "$k" in
+          C5)    prof C5 --no-extras --steps 100 --warmup 10 ;;
+          C3)    prof C3 --legs c3 --steps 100 --warmup 10 ;;
+          C2)    prof C2 --legs proj ;;
+          C4iso) prof C4iso --legs iso ;;
+          md_xs) prof md_xs --legs xspace,md,dore,lbfgs ;;
+          C5x8)  prof C5_x8 --rehearse-shard 8 --steps 100 --warmup 10 ;;
+        esac
+      done ;;
+  esac
+done
+echo done | tee -a $OUT/status.txt
