@@ -267,6 +267,48 @@ def bench_xspace(sh, b, rounds=40, reps=5):
                          'unit': 'GB/s', 'frac': byt / (ms * 1e-3) / HBM_PEAK}}
 
 
+def bench_lbfgs(sh, b, rounds=40, reps=5, corrections=50):
+    """BATCH.solve_LBFGS (python/BATCH.py:110-214) on the C3
+    matrix with the block simplex projection: the fused device rounds of
+    device.XBBEngine(lbfgs=50) -- BB steps to iteration 5, LBFGS_helper's
+    two-loop recursion from 6 (csrc/xbb.hip xlb_step / xlb_dir: four dot
+    products and one combine pass per direction) -- each rep restarting from
+    x0 with prog_tol < 0 (no early stop).  Reports us per round (one step or
+    one backtracking step, each a full objective) and per accepted iteration."""
+    import torch
+    from algorithm_utils import get_solver_parts
+    from device import XBBEngine
+    import _native
+    sizes = sh['block_sizes']
+    starts = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+    x0 = np.repeat(1.0 / sizes, sizes)
+    _, proj, _, obj = get_solver_parts((sh['A'], b), starts, 1.0, is_sparse=True)
+    eng = XBBEngine(obj, proj, lbfgs=corrections)
+    x0d = torch.from_numpy(x0).cuda()
+    eng.start(x0d, max_iter=10 ** 12, prog_tol=-1.0, hist_cap=1)
+    eng.rounds(rounds)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    its = bts = 0
+    ok = True
+    for k in range(reps):
+        eng.start(x0d, max_iter=10 ** 12, prog_tol=-1.0, hist_cap=1)
+        ev[2 * k].record()
+        eng.rounds(rounds)
+        ev[2 * k + 1].record()
+        s = eng.scalars()
+        its += int(s[_native.XS_ITER]) - 1
+        bts += int(s[_native.XS_BACKTRACKS])
+        ok = ok and bool(np.isfinite(s[_native.XS_F]))
+    torch.cuda.synchronize()
+    ms = sum(ev[2 * k].elapsed_time(ev[2 * k + 1]) for k in range(reps))
+    nr = rounds * reps
+    return {'operator': 'panels' if obj.lsq is not None else 'csr', 'corrections': corrections,
+            'rounds': nr, 'us_per_round': ms * 1e3 / nr,
+            'iterations': its, 'us_per_iter': ms * 1e3 / max(its, 1),
+            'iterations_per_s': its / (ms * 1e-3), 'backtracks': bts, 'finite': ok}
+
+
 def bench_dore(sh, b, iters=30):
     """DORE (python/DORE.py:6-90 through gradient_descent.py:55-67's setup) on
     the C3 problem, the loop gradient_descent runs: DORE.solve_engine, every
@@ -747,7 +789,7 @@ def extras(args, legs, out, tfile):
         out['mirror_descent'] = bench_md(sh3, b3)
     if 'dore' in legs:
         out['dore'] = bench_dore(sh3, b3)
-    if 'lbfgs' in legs and 'bench_lbfgs' in globals():
+    if 'lbfgs' in legs:
         out['lbfgs'] = bench_lbfgs(sh3, b3)
     log('extras done')
     if 'cpu' in legs:

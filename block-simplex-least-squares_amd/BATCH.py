@@ -7,11 +7,11 @@ the closures come from algorithm_utils.get_solver_parts and launch the HIP
 kernels.  `x_init` may be a NumPy array (as the reference's callers pass); the
 result dict holds `x` as a NumPy array, like the reference.
 
-solve_BB on a sparse least-squares objective with a block projection
-(get_solver_parts(..., is_sparse=True)) runs by default on the fused device
-engine (device.XBBEngine: one stage per BB quantity, the line search and the
-stopping test on the device, no host round trip per iteration); pass
-fused=False for the closure-by-closure loop below.
+solve_BB and solve_LBFGS on a sparse least-squares objective with a block
+projection (get_solver_parts(..., is_sparse=True)) run by default on the fused
+device engine (device.XBBEngine: one stage per quantity, the line search and
+the stopping test on the device, no host round trip per iteration); pass
+fused=False for the closure-by-closure loops below.
 """
 import time
 from collections import deque
@@ -135,10 +135,19 @@ def solve_BB(obj, proj, line_search, x_init, f_min=None, opt_tol=1e-6, max_iter=
 
 
 def solve_LBFGS(obj, proj, line_search, x_init, f_min=None, opt_tol=1e-6, max_iter=1000,
-                prog_tol=1e-12, corrections=50):
+                prog_tol=1e-12, corrections=50, fused=True):
     """Projected L-BFGS (BATCH.py:110-193).  As in the reference, the history
     queues hold the one delta_x / delta_g buffer that every iteration
-    overwrites in place, so all stored corrections alias the latest one."""
+    overwrites in place, so all stored corrections alias the latest one.
+    On a sparse least-squares objective with a block projection it runs on the
+    fused device engine (device.XBBEngine(lbfgs=corrections): the BB rounds
+    with LBFGS_helper's recursion in place of the BB step from iteration 6,
+    every decision on the device); fused=False runs the loop below."""
+    if fused and _fusable(obj, proj, line_search) and int(corrections) > 0:
+        from device import XBBEngine
+        eng = XBBEngine(obj, proj, lbfgs=int(corrections))
+        return eng.solve(x_init, f_min=f_min, opt_tol=opt_tol, max_iter=max_iter,
+                         prog_tol=prog_tol)
     torch = _torch()
     q_delta_g = deque()
     q_delta_x = deque()

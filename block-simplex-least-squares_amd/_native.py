@@ -109,7 +109,8 @@ class XBBProblem(ctypes.Structure):
                 ('hist', _vp), ('hist_cap', _i64), ('proj_work', _vp), ('proj_work_bytes', _sz),
                 ('work', _vp), ('work_bytes', _sz), ('max_iter', _i64), ('opt_tol', _dbl),
                 ('prog_tol', _dbl), ('f_min', _dbl), ('has_fmin', _i64),
-                ('lsq', ctypes.POINTER(LsqOp))]
+                ('lsq', ctypes.POINTER(LsqOp)), ('lbfgs', _i64), ('s', _vp), ('y', _vp),
+                ('lb', _vp)]
 
 
 # x-space engine scal[] slots / modes / stop reasons (include/bsls_hip.h)
@@ -135,6 +136,7 @@ _SIGS = {
     'bsls_lsq_residual': (_int, [ctypes.POINTER(LsqOp), _vp, _vp, _vp, _vp, _vp]),
     'bsls_lsq_gradient': (_int, [ctypes.POINTER(LsqOp), _vp, _vp, _vp]),
     'bsls_xbb_workspace_size': (_sz, [_i64, _i64, _i64, _i64]),
+    'bsls_xbb_lbfgs_size': (_sz, [_i64]),
     'bsls_xbb_init': (_int, [ctypes.POINTER(XBBProblem), _vp]),
     'bsls_xbb_rounds': (_int, [ctypes.POINTER(XBBProblem), _i64, _vp]),
     'bsls_md_step': (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _dbl, _vp]),

@@ -5,7 +5,8 @@
 // line_search_np (:113-137), with the stopping rule algorithm_utils.stopping
 // (:158-172) -- every decision on the device.
 //
-// A round (bsls_xbb_rounds) is five launches:
+// A round (bsls_xbb_rounds) is five launches (six for L-BFGS, BATCH.solve_LBFGS:
+// xlb_step / xlb_dir in place of xbb_step, see below):
 //   xbb_step    mode STEP:      x <- x_new, g <- g_new (the accepted point),
 //                               x_new = x + (-t) g        (np.add(x, -t*g, x_new))
 //               mode BACKTRACK: x_new = (1-tt) x + tt x_new, or x_new = x when
@@ -53,13 +54,10 @@ __global__ __launch_bounds__(64) void xbb_init_kernel(double *scal, double *hist
     (void)hist_cap;
 }
 
-__global__ __launch_bounds__(XT) void xbb_step_kernel(double *__restrict__ x,
-                                                      double *__restrict__ g,
-                                                      double *__restrict__ xn,
-                                                      const double *__restrict__ gn, int64_t n,
-                                                      const double *__restrict__ scal) {
-    const int mode = (int)scal[BSLS_XS_MODE];
-    if (mode == BSLS_XM_STOPPED) return;
+__device__ __forceinline__ void xbb_step_body(double *__restrict__ x, double *__restrict__ g,
+                                              double *__restrict__ xn,
+                                              const double *__restrict__ gn, int64_t n,
+                                              const double *__restrict__ scal, int mode) {
     const int64_t stride = (int64_t)gridDim.x * XT;
     int64_t i = (int64_t)blockIdx.x * XT + threadIdx.x;
     if (mode == BSLS_XM_INIT) {
@@ -88,6 +86,104 @@ __global__ __launch_bounds__(XT) void xbb_step_kernel(double *__restrict__ x,
     }
 }
 
+__global__ __launch_bounds__(XT) void xbb_step_kernel(double *__restrict__ x,
+                                                      double *__restrict__ g,
+                                                      double *__restrict__ xn,
+                                                      const double *__restrict__ gn, int64_t n,
+                                                      const double *__restrict__ scal) {
+    const int mode = (int)scal[BSLS_XS_MODE];
+    if (mode == BSLS_XM_STOPPED) return;
+    xbb_step_body(x, g, xn, gn, n, scal, mode);
+}
+
+// ---- L-BFGS (BATCH.solve_LBFGS, python/BATCH.py:110-214) ---------------------
+// lb (doubles): [0, C) the rho ring (rho appended at iteration i' in slot
+// (i' - 2) % C), [C, 2C) alpha (the slot of its rho), [2C, 2C + 4) the
+// coefficients a, b, c of the last direction and its t.
+static size_t lb_doubles(int64_t C) { return (size_t)(2 * C + 8); }
+
+// STEP round of iteration i > 5: the accepted point's deltas s = x_new - x,
+// y = g_new - g (np.add(x_new, -x, delta_x), BATCH.py:197-198), x <- x_new,
+// g <- g_new, and g.s, g.y, s.y, y.y; the last block then runs LBFGS_helper
+// (:196-214) -- every queued correction is the latest (s, y), the queues
+// holding the one delta buffer -- in the coefficients of d = a g + b s + c y:
+//   d = g; for j = 1..m: alpha_j = rho[-j] s.d; d -= alpha_j y
+//   d *= s.y / y.y; for j = 0..m-1: beta = rho[j] y.d; d += s (alpha[-m+j] - beta)
+//   d = -d
+// Any other round: xbb_step (i <= 5 keeps the BB step, :179-181).
+__global__ __launch_bounds__(XT) void xlb_step_kernel(
+    double *__restrict__ x, double *__restrict__ g, double *__restrict__ xn,
+    const double *__restrict__ gn, double *__restrict__ sv, double *__restrict__ yv, int64_t n,
+    const double *__restrict__ scal, double *__restrict__ lb, int64_t C,
+    double *__restrict__ part, unsigned *__restrict__ ticket) {
+    __shared__ double red[4 * XT / WAVE];
+    const int mode = (int)scal[BSLS_XS_MODE];
+    if (mode == BSLS_XM_STOPPED) return;
+    const double it = scal[BSLS_XS_ITER];
+    if (mode != BSLS_XM_STEP || it <= 5.0) {
+        xbb_step_body(x, g, xn, gn, n, scal, mode);
+        return;
+    }
+    const int64_t stride = (int64_t)gridDim.x * XT;
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * XT + threadIdx.x; i < n; i += stride) {
+        const double xv = xn[i], gv = gn[i], xo = x[i], go = g[i];
+        const double s_ = xv - xo, y_ = gv - go;
+        sv[i] = s_;
+        yv[i] = y_;
+        x[i] = xv;
+        g[i] = gv;
+        v[0] += gv * s_;
+        v[1] += gv * y_;
+        v[2] += s_ * y_;
+        v[3] += y_ * y_;
+    }
+    block_reduce<4, 0u>(v, red);
+    double tot[4];
+    if (!last_block_reduce<4, 0u>(v, part, ticket, tot, red)) return;
+    if (threadIdx.x != 0) return;
+    const double gs = tot[0], gy = tot[1], sy = tot[2], yy = tot[3];
+    const int64_t k = (int64_t)it - 1;            // corrections appended (iterations 2..i)
+    const int64_t m = k < C ? k : C;
+    double *rho = lb, *alpha = lb + C, *cf = lb + 2 * C;
+    double a = 1.0, b = 0.0, c = 0.0;
+    for (int64_t j = 1; j <= m; ++j) {            // newest first
+        const int64_t q = (k - j) % C;
+        const double al = rho[q] * (a * gs + c * sy);   // s.d, d = a g + c y
+        alpha[q] = al;
+        c -= al;                                        // d -= alpha y
+    }
+    const double t = sy / yy;
+    a *= t;
+    c *= t;
+    for (int64_t j = 0; j < m; ++j) {             // oldest first
+        const int64_t q = (k - m + j) % C;
+        const double beta = rho[q] * (a * gy + b * sy + c * yy);   // y.d
+        b += alpha[q] - beta;                           // d += s (alpha - beta)
+    }
+    cf[0] = a;
+    cf[1] = b;
+    cf[2] = c;
+    cf[3] = t;
+}
+
+// x_new = x + d, d = -(a g + b s + c y) (d *= -1.0; np.add(x, d, x_new))
+__global__ __launch_bounds__(XT) void xlb_dir_kernel(const double *__restrict__ x,
+                                                     const double *__restrict__ g,
+                                                     const double *__restrict__ sv,
+                                                     const double *__restrict__ yv,
+                                                     double *__restrict__ xn, int64_t n,
+                                                     const double *__restrict__ scal,
+                                                     const double *__restrict__ lb, int64_t C) {
+    if ((int)scal[BSLS_XS_MODE] != BSLS_XM_STEP || scal[BSLS_XS_ITER] <= 5.0) return;
+    const double a = lb[2 * C], b = lb[2 * C + 1], c = lb[2 * C + 2];
+    const int64_t stride = (int64_t)gridDim.x * XT;
+    for (int64_t i = (int64_t)blockIdx.x * XT + threadIdx.x; i < n; i += stride) {
+        const double d = -((a * g[i] + b * sv[i]) + c * yv[i]);
+        xn[i] = x[i] + d;
+    }
+}
+
 // algorithm_utils.stopping (:158-172): every test runs, the last true one names
 // the reason.
 __device__ __forceinline__ int xstop(double i, double max_iter, double f, double f_old,
@@ -105,7 +201,7 @@ __global__ __launch_bounds__(XT) void xbb_finish_kernel(
     const double *__restrict__ gn, int64_t n, double *__restrict__ scal,
     double *__restrict__ hist, int64_t hist_cap, double max_iter, double opt_tol,
     double prog_tol, double f_min, int has_fmin, double *__restrict__ part,
-    unsigned *__restrict__ ticket) {
+    unsigned *__restrict__ ticket, double *__restrict__ lb, int64_t C) {
     __shared__ double red[4 * XT / WAVE];
     const int mode = (int)scal[BSLS_XS_MODE];
     if (mode == BSLS_XM_STOPPED) return;
@@ -194,6 +290,8 @@ __global__ __launch_bounds__(XT) void xbb_finish_kernel(
     scal[BSLS_XS_TT] = 1.0;
     scal[BSLS_XS_REVERT] = 0.0;
     scal[BSLS_XS_ITER] = it;
+    // L-BFGS: q_rho.append(1 / delta_g.T.dot(delta_x)) at iteration it (BATCH.py:174)
+    if (C > 0) lb[((int64_t)it - 2) % C] = 1.0 / tot[1];
     const int64_t k = (int64_t)it - 1;
     if (k < hist_cap) hist[k] = f_new;
     const int r = xstop(it, max_iter, f_new, f, opt_tol, prog_tol, f_min, has_fmin);
@@ -241,6 +339,10 @@ extern "C" size_t bsls_xbb_workspace_size(int64_t m, int64_t n, int64_t A_ntiles
     return xwork(nullptr, A_ntiles).bytes;
 }
 
+extern "C" size_t bsls_xbb_lbfgs_size(int64_t corrections) {
+    return (corrections > 0 ? lb_doubles(corrections) : 0) * sizeof(double);
+}
+
 extern "C" int bsls_xbb_init(const bsls_xbb_problem *p, void *stream) {
     if (!p || !p->scal) return BSLS_E_ARG;
     xbb_init_kernel<<<1, 64, 0, (hipStream_t)stream>>>(p->scal, p->hist, p->hist_cap);
@@ -253,6 +355,7 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
         !p->r || !p->scal || !p->neg_b || !p->starts || count < 0)
         return BSLS_E_ARG;
     if (!p->lsq && (p->A.rows != p->m || p->AT.rows != p->n)) return BSLS_E_ARG;
+    if (p->lbfgs < 0 || (p->lbfgs > 0 && (!p->s || !p->y || !p->lb))) return BSLS_E_ARG;
     XWork w = xwork(p->work, p->A.ntiles);
     if (!p->work || p->work_bytes < w.bytes) return BSLS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
@@ -260,7 +363,15 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
     const int64_t fw = ((p->n >> 1) + XT * XU - 1) / (XT * XU);
     const int gf = (int)(fw < 1 ? 1 : (fw > XGRID ? XGRID : fw));
     for (int64_t c = 0; c < count; ++c) {
-        xbb_step_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal);
+        if (p->lbfgs > 0) {
+            xlb_step_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->s, p->y, p->n, p->scal,
+                                               p->lb, p->lbfgs, w.part, w.ticket);
+            BSLS_LAUNCH_CHECK();
+            xlb_dir_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->s, p->y, p->xn, p->n, p->scal, p->lb,
+                                              p->lbfgs);
+        } else {
+            xbb_step_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal);
+        }
         BSLS_LAUNCH_CHECK();
         int rc = proj_launch_gated(p->ball != 0, p->xn, p->starts, p->nblocks, p->n, p->max_block,
                                    p->proj_work, p->proj_work_bytes, st, p->scal + BSLS_XS_MODE);
@@ -283,7 +394,7 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
         xbb_finish_kernel<<<gf, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal, p->hist,
                                              p->hist_cap, (double)p->max_iter, p->opt_tol,
                                              p->prog_tol, p->f_min, (int)p->has_fmin, w.part,
-                                             w.ticket);
+                                             w.ticket, p->lb, p->lbfgs);
         BSLS_LAUNCH_CHECK();
     }
     return BSLS_OK;

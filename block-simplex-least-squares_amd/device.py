@@ -1017,7 +1017,11 @@ class XBBEngine:
     (csrc/xbb.hip, bsls_xbb_rounds); the host polls the mode every `poll`
     rounds."""
 
-    def __init__(self, obj, proj, A_dev=None):
+    def __init__(self, obj, proj, A_dev=None, lbfgs=0):
+        """lbfgs = C > 0: BATCH.solve_LBFGS (python/BATCH.py:110-214) with C
+        corrections -- the BB step of iterations i > 5 replaced by
+        LBFGS_helper's two-loop recursion on the device (csrc/xbb.hip
+        xlb_step / xlb_dir)."""
         torch = _torch()
         L = _native.lib()
         self.obj, self.proj = obj, proj
@@ -1052,6 +1056,15 @@ class XBBEngine:
         P.work, P.work_bytes = self.work.data_ptr(), self.work.numel()
         lsq = getattr(obj, 'lsq', None)
         P.lsq = ctypes.pointer(lsq.op) if lsq is not None else None
+        self.lbfgs = int(lbfgs)
+        if self.lbfgs < 0:
+            raise ValueError('corrections must be >= 0')
+        if self.lbfgs:
+            self.s = torch.zeros(n, **dev)
+            self.y = torch.zeros(n, **dev)
+            self.lb = torch.zeros(max(1, L.bsls_xbb_lbfgs_size(self.lbfgs) // 8), **dev)
+            P.lbfgs, P.s, P.y, P.lb = (self.lbfgs, self.s.data_ptr(), self.y.data_ptr(),
+                                       self.lb.data_ptr())
         self.P = P
 
     def start(self, x_init, f_min=None, opt_tol=1e-6, max_iter=2000, prog_tol=1e-12,

@@ -474,9 +474,21 @@ typedef struct bsls_xbb_problem {
     double opt_tol, prog_tol, f_min;
     int64_t has_fmin;
     const bsls_lsq_op *lsq;         /* panel operator for both products, or NULL (A / AT CSR) */
+    /* L-BFGS (BATCH.solve_LBFGS, python/BATCH.py:110-214): lbfgs = corrections
+     * C > 0 replaces the BB step of iterations i > 5 by the two-loop recursion
+     * of LBFGS_helper (:196-214) over the history queues; i <= 5 keep the BB
+     * step (:179-181).  As in the reference, the queues hold the one delta_x /
+     * delta_g buffer that every iteration overwrites, so every stored
+     * correction is the latest (s, y) with its own rho: the recursion runs in
+     * the coefficients of d = a g + b s + c y (four dot products per
+     * iteration, one pass; then x_new = x + d, one pass).  0: BB. */
+    int64_t lbfgs;
+    double *s, *y;                  /* n each: delta_x, delta_g of the last accepted step */
+    double *lb;                     /* bsls_xbb_lbfgs_size(lbfgs) doubles: rho ring, alpha, coefficients */
 } bsls_xbb_problem;
 
 size_t bsls_xbb_workspace_size(int64_t m, int64_t n, int64_t A_ntiles, int64_t AT_ntiles);
+size_t bsls_xbb_lbfgs_size(int64_t corrections);
 /* x must hold x_init; resets scal (mode INIT) and the reduction tickets. */
 int bsls_xbb_init(const bsls_xbb_problem *p, void *stream);
 /* Enqueue `count` rounds (the first one after init evaluates obj(x_init)). */

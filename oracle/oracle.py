@@ -451,6 +451,66 @@ def batch_solve_bb(obj, proj, line_search, x_init, f_min=None, opt_tol=1e-6, max
     return {'f': f, 'x': x, 'stop': stop, 'iterations': i, 'progress': np.array(progress)}
 
 
+def batch_solve_lbfgs(obj, proj, line_search, x_init, f_min=None, opt_tol=1e-6, max_iter=1000,
+                      prog_tol=1e-12, corrections=50):
+    """BATCH.py:110-193 with LBFGS_helper (:196-214), vector operations in the
+    reference's order; the history queues hold the one delta_x / delta_g
+    buffer (updated in place every iteration), as the reference's do."""
+    from collections import deque
+    q_dg, q_dx, q_rho = deque(), deque(), deque()
+    n = x_init.shape[0]
+    x = np.copy(x_init)
+    g = np.zeros(n)
+    d = np.zeros(n)
+    alpha = np.zeros(corrections)
+    delta_x, delta_g = np.zeros(n), np.zeros(n)
+    g_new, x_new = np.zeros(n), np.zeros(n)
+    f_old = np.inf
+    i = 1
+    f = obj(x, g)
+    progress = [f]
+    while True:
+        flag, stop = batch_stopping(i, max_iter, f, f_old, opt_tol, prog_tol, f_min)
+        if flag:
+            break
+        if i == 1:
+            np.add(x, -g, x_new)
+        else:
+            q_dg.append(delta_g)
+            q_dx.append(delta_x)
+            q_rho.append(1 / delta_g.T.dot(delta_x))
+            if i > corrections + 1:
+                q_dg.popleft()
+                q_dx.popleft()
+                q_rho.popleft()
+            if i <= 5:
+                d = -(delta_x.T.dot(delta_g) / delta_g.T.dot(delta_g)) * g
+            else:
+                m = len(q_dg)
+                np.copyto(d, g)
+                for j in range(1, m + 1):
+                    alpha[-j] = q_rho[-j] * q_dx[-j].T.dot(d)
+                    d -= alpha[-j] * q_dg[-j]
+                t = q_dx[-1].T.dot(q_dg[-1]) / q_dg[-1].T.dot(q_dg[-1])
+                d *= t
+                for j in range(m):
+                    beta = q_rho[j] * q_dg[j].T.dot(d)
+                    d += q_dx[j] * (alpha[-m + j] - beta)
+                d *= -1.0
+            np.add(x, d, x_new)
+        proj(x_new)
+        f_new = obj(x_new, g_new)
+        f_new = line_search(x, f, g, x_new, f_new, g_new, i)
+        f_old, f = f, f_new
+        np.add(x_new, -x, delta_x)
+        np.add(g_new, -g, delta_g)
+        np.copyto(x, x_new)
+        np.copyto(g, g_new)
+        i += 1
+        progress.append(f)
+    return {'f': f, 'x': x, 'stop': stop, 'iterations': i, 'progress': np.array(progress)}
+
+
 def batch_solve_md(obj, block_starts, step_size, x_init, f_min=None, opt_tol=1e-6,
                    max_iter=1000, prog_tol=0.0):
     """BATCH.py:217-250 with normalization (algorithm_utils.py:175-179)."""

@@ -389,6 +389,43 @@ def gen_batch_traces():
     np.savez_compressed(os.path.join(OUT, 'batch.npz'), **out)
 
 
+def gen_lbfgs_traces():
+    """BATCH.solve_LBFGS (python/BATCH.py:110-214) on the sparse x-space
+    problems of gen_batch_traces ('s': 3000 routes / 150 blocks, 2 % noise;
+    'c': 1500 / 60, exact data) with the block simplex projection, stopped at
+    several max_iter (iterations 2-5 take the BB step, LBFGS_helper from 6)
+    and run to its own stop; also corrections = 3 (the queues cap)."""
+    import contextlib
+    import io
+    from algorithm_utils import get_solver_parts
+    import BATCH as batch
+    out = {}
+    cases = [('s', SEED + 11, 3000, 150, 300, 16, 0.02),
+             ('c', SEED + 12, 1500, 60, 200, 8, 0.0)]
+    for tag, seed, n, p, m, pc, noise in cases:
+        A, b, xs, sizes = sparse_problem(seed, n, p, m, per_col=pc, noise=noise)
+        starts = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+        x_init = np.repeat(1.0 / sizes, sizes)
+        step_size, proj, line_search, obj = get_solver_parts((A, b), starts, 1.0,
+                                                            is_sparse=True)
+        runs = [(k, 50) for k in (2, 3, 6, 7, 10, 15, 40, 2000)] + [(30, 3)]
+        for k, corr in runs:
+            with contextlib.redirect_stdout(io.StringIO()):
+                sol = batch.solve_LBFGS(obj, proj, line_search, x_init.copy(), max_iter=k,
+                                        corrections=corr)
+            key = '%s_lb%d' % (tag, k) + ('' if corr == 50 else '_c%d' % corr)
+            out[key + '_x'] = sol['x']
+            out[key + '_f'] = np.array(sol['f'])
+            out[key + '_it'] = np.array(sol['iterations'])
+            out[key + '_stop'] = np.array(sol['stop'])
+            out[key + '_prog'] = np.array([q[1] for q in sol['progress']])
+        out['%s_A_data' % tag], out['%s_A_indices' % tag] = A.data, A.indices
+        out['%s_A_indptr' % tag], out['%s_A_shape' % tag] = A.indptr, np.array(A.shape)
+        out['%s_b' % tag], out['%s_starts' % tag] = b, starts
+        out['%s_x_init' % tag] = x_init
+    np.savez_compressed(os.path.join(OUT, 'lbfgs.npz'), **out)
+
+
 def gen_plugin_traces():
     """GradientDescent dispatch (python/gradient_descent.py:47-69) over the
     z-space closures of main.solve_in_z (python/main.py:47-65): every exit of
@@ -487,11 +524,15 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == 'plugins':
         gen_plugin_traces()
         return
+    if len(sys.argv) > 1 and sys.argv[1] == 'lbfgs':
+        gen_lbfgs_traces()
+        return
     gen_projection_cases()
     gen_isotonic_cases()
     gen_xz_quad()
     gen_solver_traces()
     gen_batch_traces()
+    gen_lbfgs_traces()
     gen_plugin_traces()
     for f in sorted(os.listdir(OUT)):
         if f.endswith('.npz'):

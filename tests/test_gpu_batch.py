@@ -154,3 +154,73 @@ def test_fused_engine_larger_problem_matches_closure_loop(cuda, orc):
         prog = np.array([q[1] for q in sol['progress']])
         assert prog.shape == r['progress'].shape
         assert np.max(np.abs(prog - r["progress"]) / np.abs(r["progress"])) < 1e-8
+
+
+LBFGS_RUNS = [(k, 50) for k in (2, 3, 6, 7, 10, 15, 40, 2000)] + [(30, 3)]
+
+
+def _lbfgs_problem(golden, tag):
+    d = golden('lbfgs.npz')
+    A = sps.csr_matrix((d['%s_A_data' % tag], d['%s_A_indices' % tag], d['%s_A_indptr' % tag]),
+                       shape=tuple(d['%s_A_shape' % tag]))
+    return d, A, d['%s_b' % tag], d['%s_starts' % tag], d['%s_x_init' % tag]
+
+
+@pytest.mark.parametrize('fused,panels', [(True, False), (False, False), (True, True)])
+@pytest.mark.parametrize('tag', ['s', 'c'])
+def test_solve_lbfgs_vs_reference(cuda, golden, monkeypatch, tag, fused, panels):
+    """BATCH.solve_LBFGS (python/BATCH.py:110-214) on the sparse x-space
+    problems, against the reference's own runs (tests/golden/lbfgs.npz):
+    the fused device rounds (LBFGS_helper's recursion in d's coefficients,
+    csrc/xbb.hip) and the closure loop, BB steps for i <= 5, L-BFGS from 6,
+    the queues' cap (corrections 3) -- iterates within 1e-6, the objective
+    trace within 1e-6, the same exit (max_iter at the same iteration, or the
+    revert's |f_old - f| < prog_tol at the same f)."""
+    import BATCH
+    from algorithm_utils import SparseLSQ, get_solver_parts
+    monkeypatch.setattr(SparseLSQ, 'PANEL_MIN_NNZ', 0 if panels else 1 << 62)
+    d, A, b, starts, x0 = _lbfgs_problem(golden, tag)
+    step, proj, ls, obj = get_solver_parts((A, b), starts, 1.0, is_sparse=True)
+    for k, corr in LBFGS_RUNS:
+        key = '%s_lb%d' % (tag, k) + ('' if corr == 50 else '_c%d' % corr)
+        sol = BATCH.solve_LBFGS(obj, proj, ls, x0.copy(), max_iter=k, corrections=corr,
+                                fused=fused)
+        ref_it = int(d[key + '_it'])
+        ref_f = float(d[key + '_f'])
+        if str(d[key + '_stop']) == 'max_iter':
+            assert sol['iterations'] == ref_it and sol['stop'] == 'max_iter', (key, sol['stop'])
+            assert rel(sol['x'], d[key + '_x']) < 1e-6, key
+            prog = np.array([q[1] for q in sol['progress']])
+            ref = d[key + '_prog']
+            assert prog.shape == ref.shape, key
+            assert np.max(np.abs(prog - ref) / np.maximum(np.abs(ref), 1e-3)) < 1e-6, key
+        else:
+            assert sol['stop'].endswith('< prog_tol'), (key, sol['stop'])
+            assert abs(sol['f'] - ref_f) <= 1e-9 * max(abs(ref_f), 1.0), (key, sol['f'], ref_f)
+            assert rel(sol['x'], d[key + '_x']) < 1e-5, key
+
+
+def test_lbfgs_c3_size_vs_oracle(cuda, orc):
+    """The fused L-BFGS rounds on the C3 matrix (1M routes / 50k blocks /
+    100k links / 16M nnz, 2 % noise) against the oracle's restatement of
+    BATCH.solve_LBFGS over SciPy (oracle.batch_solve_lbfgs): iterates within
+    1e-6 and the objective trace within 1e-8 at 12 iterations (BB steps to 5,
+    L-BFGS from 6)."""
+    import BATCH
+    from algorithm_utils import get_solver_parts
+    from synthetic import make_shard, add_noise, CONFIGS, SEED
+    c = CONFIGS['C3']
+    sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+    b = add_noise(sh['Ax'], 0.02, seed=SEED)
+    sizes = sh['block_sizes']
+    starts = np.concatenate(([0], np.cumsum(sizes)[:-1]))
+    x0 = np.repeat(1.0 / sizes, sizes)
+    step, proj, ls, obj = get_solver_parts((sh['A'], b), starts, 1.0, is_sparse=True)
+    a = BATCH.solve_LBFGS(obj, proj, ls, x0.copy(), max_iter=12)
+    o_obj, o_proj, o_ls = orc.sparse_parts(sh['A'], b, starts)
+    r = orc.batch_solve_lbfgs(o_obj, o_proj, o_ls, x0.copy(), max_iter=12)
+    assert a['iterations'] == r['iterations'] == 12 and r['stop'] == 'max_iter'
+    assert rel(a['x'], r['x']) < 1e-6
+    prog = np.array([q[1] for q in a['progress']])
+    assert prog.shape == r['progress'].shape
+    assert np.max(np.abs(prog - r['progress']) / np.abs(r['progress'])) < 1e-8

@@ -342,6 +342,34 @@ def test_golden_batch_solve_bb(orc, golden, tag, lasso):
         assert exact(sol['progress'], d['%s_bb%d_prog' % (tag, k)])
 
 
+LBFGS_RUNS = [(k, 50) for k in (2, 3, 6, 7, 10, 15, 40, 2000)] + [(30, 3)]
+
+
+def _lbfgs_key(tag, k, corr):
+    return '%s_lb%d' % (tag, k) + ('' if corr == 50 else '_c%d' % corr)
+
+
+@pytest.mark.parametrize('tag', ['s', 'c'])
+def test_golden_batch_solve_lbfgs(orc, golden, tag):
+    """BATCH.solve_LBFGS over get_solver_parts(is_sparse=True)
+    (python/BATCH.py:110-214, fixtures tests/golden/lbfgs.npz): the
+    restatement's vector recursion reproduces the reference bit for bit,
+    BB steps (i <= 5), LBFGS_helper (i >= 6), the queues' cap (corrections 3)
+    and both exits (max_iter, the revert's |f_old - f| = 0)."""
+    d = golden('lbfgs.npz')
+    A = sps.csr_matrix((d['%s_A_data' % tag], d['%s_A_indices' % tag], d['%s_A_indptr' % tag]),
+                       shape=tuple(d['%s_A_shape' % tag]))
+    obj, proj, ls = orc.sparse_parts(A, d['%s_b' % tag], d['%s_starts' % tag])
+    for k, corr in LBFGS_RUNS:
+        key = _lbfgs_key(tag, k, corr)
+        sol = orc.batch_solve_lbfgs(obj, proj, ls, d['%s_x_init' % tag].copy(), max_iter=k,
+                                    corrections=corr)
+        assert exact(sol['x'], d[key + '_x']), key
+        assert sol['iterations'] == int(d[key + '_it'])
+        assert sol['stop'] == str(d[key + '_stop'])
+        assert exact(sol['progress'], d[key + '_prog'])
+
+
 @pytest.mark.parametrize('tag', ['s', 'c'])
 def test_golden_batch_solve_md(orc, golden, tag):
     """BATCH.solve_MD (python/BATCH.py:217-250), decreasing_step_size(i, 1, 1e8)."""
