@@ -267,13 +267,15 @@ def bench_xspace(sh, b, rounds=40, reps=5):
                          'unit': 'GB/s', 'frac': byt / (ms * 1e-3) / HBM_PEAK}}
 
 
-def bench_lbfgs(sh, b, rounds=40, reps=5, corrections=50):
+def bench_lbfgs(sh, b, rounds=16, reps=10, corrections=50):
     """BATCH.solve_LBFGS (python/BATCH.py:110-214) on the C3
     matrix with the block simplex projection: the fused device rounds of
     device.XBBEngine(lbfgs=50) -- BB steps to iteration 5, LBFGS_helper's
     two-loop recursion from 6 (csrc/xbb.hip xlb_step / xlb_dir: four dot
     products and one combine pass per direction) -- each rep restarting from
-    x0 with prog_tol < 0 (no early stop).  Reports us per round (one step or
+    x0 with prog_tol < 0 (no early stop), `rounds` short of where the run
+    converges (a revert makes delta_x = 0 and rho = 1/0, which the reference's
+    own prog_tol test stops on).  Reports us per round (one step or
     one backtracking step, each a full objective) and per accepted iteration."""
     import torch
     from algorithm_utils import get_solver_parts
@@ -307,6 +309,30 @@ def bench_lbfgs(sh, b, rounds=40, reps=5, corrections=50):
             'rounds': nr, 'us_per_round': ms * 1e3 / nr,
             'iterations': its, 'us_per_iter': ms * 1e3 / max(its, 1),
             'iterations_per_s': its / (ms * 1e-3), 'backtracks': bts, 'finite': ok}
+
+
+def bench_c1():
+    """BASELINE configs[0]: main.py --method BB --device cpu on the
+    tests/fast/test_main.py problem (bsls_utils.generate_data() defaults, the
+    reference tests' seed): the host path of the drop-in (SciPy closures + the
+    host c_extensions library, include/bsls_cpu.h), end to end from the .mat
+    file through LS_postprocess.  Plumbing, not a GPU number."""
+    import argparse
+    import tempfile
+    import bsls_utils
+    import main as bmain
+    np.random.seed(237423433)
+    with tempfile.TemporaryDirectory() as d:
+        fname = os.path.join(d, 'test_main.mat')
+        bsls_utils.generate_data(fname=fname)
+        args = argparse.Namespace(noise=0, file=fname, log='WARN', init=False, eq='CP',
+                                  method='BB', device='cpu')
+        t0 = time.perf_counter()
+        iters, times, states, output = bmain.main(args=args)
+        el = time.perf_counter() - t0
+    err = np.asarray(output['0.5norm(Ax-b)^2'])
+    return {'device': 'cpu', 'iterations': int(iters[-1]), 'seconds': el,
+            'final_0.5norm(Ax-b)^2': float(err[-1]), 'converged_below_1e-16': bool(err[-1] < 1e-16)}
 
 
 def bench_dore(sh, b, iters=30):
@@ -506,7 +532,8 @@ def build_engine(sh, b, world, dist, parts, sharded=False):
     eng.target.copy_(eng.r - torch.from_numpy(b).cuda())
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
     drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
-                    all_reduce_async=torch_all_reduce_async())
+                    all_reduce_async=torch_all_reduce_async(),
+                    rank=dist.get_rank() if dist else 0)
     drv.prologue()
     return eng, drv.iterate
 
@@ -624,7 +651,7 @@ def host_info(threads):
             'OPENBLAS_NUM_THREADS': os.environ.get('OPENBLAS_NUM_THREADS')}
 
 
-LEGS = ('main', 'c3', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'cpu')
+LEGS = ('main', 'c3', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'c1', 'cpu')
 
 
 def traffic_file():
@@ -791,6 +818,8 @@ def extras(args, legs, out, tfile):
         out['dore'] = bench_dore(sh3, b3)
     if 'lbfgs' in legs:
         out['lbfgs'] = bench_lbfgs(sh3, b3)
+    if 'c1' in legs:
+        out['c1_cpu_path'] = bench_c1()
     log('extras done')
     if 'cpu' in legs:
         cps, cit, cel = cpu_baseline_bb(sh3['A'], b3, sh3['block_sizes'])

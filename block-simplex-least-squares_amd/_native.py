@@ -73,7 +73,7 @@ class BBProblem(ctypes.Structure):
                 ('z', _vp * 2), ('g', _vp * 2), ('x', _vp), ('r', _vp), ('scal', _vp),
                 ('work', _vp),
                 ('max_zblock', _i64), ('max_iter', _i64), ('opt_tol', _dbl),
-                ('early_exit', _i32), ('reserved', _i32),
+                ('early_exit', _i32), ('shard_role', _i32),
                 ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz),
                 ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp)]
 
@@ -174,6 +174,72 @@ _SIGS = {
     'bsls_version': (ctypes.c_char_p, []),
     'bsls_device_arch': (_int, [ctypes.c_char_p, _int]),
 }
+
+
+# ---- the host path (include/bsls_cpu.h, lib/libbsls_cpu.so) -------------------
+# Selected explicitly only (BSLS_DEVICE=cpu, or set_device('cpu'); main.py
+# --device cpu): BASELINE configs[0], the reference's CPU c_extensions path.
+# Nothing falls back to it -- lib() still raises without a HIP device.
+CPU_LIB_PATH = os.path.join(HERE, 'lib', 'libbsls_cpu.so')
+CPU_HEADER = os.path.join(os.path.dirname(HERE), 'include', 'bsls_cpu.h')
+_device = None
+
+_CPU_SIGS = {
+    'bsls_cpu_proj_simplex': (_int, [_vp, _i64, _i64]),
+    'bsls_cpu_proj_multi_simplex': (_int, [_vp, _vp, _i64, _i64, _int]),
+    'bsls_cpu_proj_multi_ball': (_int, [_vp, _vp, _i64, _i64, _int]),
+    'bsls_cpu_isotonic_multi': (_int, [_int, _vp, _vp, _i64, _i64, _vp, _int, _int]),
+    'bsls_cpu_quad_obj': (_dbl, [_vp, _vp, _vp, _vp, _i64]),
+    'bsls_cpu_line_search': (_dbl, [_vp, _dbl, _vp, _vp, _dbl, _vp, _vp, _vp, _i64]),
+    'bsls_cpu_x2z': (_int, [_vp, _vp, _vp, _i64, _i64]),
+    'bsls_cpu_z2x': (_int, [_vp, _vp, _vp, _i64, _i64]),
+    'bsls_cpu_version': (ctypes.c_char_p, []),
+}
+_cpu = None
+
+
+def set_device(name):
+    """'hip' (the default: every entry point on the MI355X) or 'cpu' (the
+    host path of the c_extensions drop-in and the solvers' closures)."""
+    global _device
+    if name not in ('hip', 'cpu', None):
+        raise ValueError("device must be 'hip' or 'cpu'")
+    _device = name
+
+
+def device_mode():
+    if _device is not None:
+        return _device
+    d = os.environ.get('BSLS_DEVICE', 'hip').lower()
+    return 'cpu' if d == 'cpu' else 'hip'
+
+
+def cpu_threads():
+    return int(os.environ.get('BSLS_CPU_THREADS') or os.environ.get('OMP_NUM_THREADS')
+               or os.cpu_count() or 1)
+
+
+def cpu_lib():
+    """The host library (built with the HIP one by build())."""
+    global _cpu
+    if _cpu is None:
+        if not os.path.exists(CPU_LIB_PATH):
+            raise RuntimeError('bsls: %s is missing -- run __graft_entry__.build()'
+                               % CPU_LIB_PATH)
+        L = ctypes.CDLL(CPU_LIB_PATH)
+        for name, (res, args) in _CPU_SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _cpu = L
+    return _cpu
+
+
+def declared_cpu_symbols():
+    import re
+    text = open(CPU_HEADER).read()
+    return sorted(set(re.findall(r'^\s*(?:double|int|const char \*)\s*(bsls_cpu_\w+)\s*\(',
+                                 text, re.M)))
 
 
 def build(force=False):

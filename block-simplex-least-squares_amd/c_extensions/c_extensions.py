@@ -16,12 +16,16 @@ Same function names, argument meaning, asserts and in-place behaviour:
 Inputs may be NumPy arrays (staged to HBM and back over PCIe for each call) or
 float64 ``torch`` tensors already on the GPU (projected in place, no copies) --
 the fused solver path uses the latter.  There is no CPU fallback: without the
-HIP library or a HIP device every function raises RuntimeError.
+HIP library or a HIP device every function raises RuntimeError.  The host path
+(include/bsls_cpu.h, c_extensions/_cpu.py: the reference's own CPU path,
+BASELINE configs[0]) runs NumPy inputs only when selected explicitly
+(BSLS_DEVICE=cpu or _native.set_device('cpu')).
 """
 import numpy as np
 
 import _native
 from _native import check, ptr, stream_handle
+from c_extensions import _cpu
 
 __all__ = ['proj_simplex_c', 'proj_multi_simplex_c', 'proj_multi_ball_c',
            'isotonic_regression_c', 'isotonic_regression_multi_c',
@@ -61,6 +65,12 @@ def _check_y(y, name='y'):
         raise ValueError('Buffer has wrong number of dimensions (expected 1, got %d)' % y.ndim)
     if y.dtype != np.float64:
         raise ValueError("Buffer dtype mismatch, expected 'double_t' but got '%s'" % y.dtype)
+
+
+def _cpu_sel(*arrays):
+    """The explicitly selected host path, for NumPy inputs (device tensors stay
+    on the device)."""
+    return _native.device_mode() == 'cpu' and not any(_is_tensor(a) for a in arrays)
 
 
 def _host_blocks(blocks):
@@ -152,6 +162,8 @@ def proj_simplex_c(y, start, end):
     assert start >= 0 and start < n and end > 0 and end <= n
     if start >= end:
         return
+    if _cpu_sel(y):
+        return _cpu.proj_simplex(y, start, end)
     st = _Staged(y)
     L = _native.lib()
     sub = st.dev[:end]
@@ -169,6 +181,8 @@ def proj_multi_simplex_c(y, blocks):
     _check_blocks_typed(blocks)
     bh = _host_blocks(blocks)
     _assert_multi(bh, y.shape[0])
+    if _cpu_sel(y, blocks):
+        return _cpu.proj_multi(False, y, bh)
     _run_proj('bsls_proj_multi_simplex', y, bh, y.shape[0])
 
 
@@ -178,6 +192,8 @@ def proj_multi_ball_c(y, blocks):
     _check_blocks_typed(blocks)
     bh = _host_blocks(blocks)
     _assert_multi(bh, y.shape[0])
+    if _cpu_sel(y, blocks):
+        return _cpu.proj_multi(True, y, bh)
     _run_proj('bsls_proj_multi_ball', y, bh, y.shape[0])
 
 
@@ -206,6 +222,8 @@ def _weights(weight, n, first):
 
 
 def _run_iso(variant, y, blocks_h, n, weight, update, name):
+    if _cpu_sel(y, weight):
+        return _cpu.isotonic(variant, y, blocks_h, n, weight, update)
     torch = _torch()
     L = _native.lib()
     st = _Staged(y)
@@ -291,6 +309,8 @@ def quad_obj_c(x, Q, c, g):
     writes g in place (when g is C-contiguous float64, like the reference)."""
     for name, a in (('x', x), ('Q', Q), ('c', c), ('g', g)):
         _check_y(a, name)
+    if _cpu_sel(x, Q, c, g):
+        return _cpu.quad_obj(x, Q, c, g)
     torch = _torch()
     L = _native.lib()
     n = x.shape[0]
@@ -310,6 +330,8 @@ def line_search_quad_obj_c(x, f, g, x_new, f_new, g_new, Q, c):
     last value there, as it does on valid memory in the reference)."""
     for name, a in (('x', x), ('g', g), ('x_new', x_new), ('g_new', g_new), ('Q', Q), ('c', c)):
         _check_y(a, name)
+    if _cpu_sel(x, g, x_new, g_new, Q, c):
+        return _cpu.line_search(x, f, g, x_new, f_new, g_new, Q, c)
     torch = _torch()
     L = _native.lib()
     n = x.shape[0]
@@ -343,6 +365,8 @@ def x2z_c(x, z, blocks):
     nz = n - len(bh)
     if z.shape[0] < nz:
         raise IndexError('Out of bounds on buffer access (axis 0)')
+    if _cpu_sel(x, z):
+        return _cpu.x2z(x, z, bh, nz)
     L = _native.lib()
     sx = _Staged(x)
     torch = _torch()
@@ -364,6 +388,8 @@ def z2x_c(x, z, blocks):
     nz = n - len(bh)
     if z.shape[0] < nz:
         raise IndexError('Out of bounds on buffer access (axis 0)')
+    if _cpu_sel(x, z):
+        return _cpu.z2x(x, z, bh)
     L = _native.lib()
     torch = _torch()
     sz = _Staged(z)

@@ -111,6 +111,16 @@ __device__ __forceinline__ void bb_record_f(const bsls_bb_problem &P, int64_t it
     }
 }
 
+// A column-sharded rank other than the one adding target (shard_role 2)
+// writes r = 0 for its rows once the run has stopped: its K1 no longer forms a
+// partial, and the all-reduce must leave the final residual (held by the
+// shard_role 1 rank, whose r is not touched) as it was.
+__device__ __forceinline__ void k1_stopped_rows(const bsls_bb_problem &P, int64_t r0, int64_t r1,
+                                                int64_t t0, int64_t stride) {
+    if (P.shard_role != 2) return;
+    for (int64_t row = r0 + t0; row < r1; row += stride) P.r[row] = 0.0;
+}
+
 // K1's finish for row block rb (rows [r0, r1)), run by one workgroup: r =
 // the G partials of each row summed in group order (from rpart, or from LDS
 // `local` when the block had one group) + target; its share of ||r||^2 goes
@@ -178,10 +188,17 @@ __global__ __launch_bounds__(1024) void bb_k1(bsls_bb_problem P, int64_t iter, u
                                               double *part, unsigned *ticket, int64_t rb_base) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int row_last;
-    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_panels &M = P.A;
     const int64_t G = M.ngroups;
     const int64_t g = blockIdx.x % G, rb = rb_base + blockIdx.x / G;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
+        if (g == 0) {
+            const int64_t r0 = rb * PANEL_WAVES * M.prow;
+            const int64_t r1 = (r0 + PANEL_WAVES * M.prow < P.m) ? r0 + PANEL_WAVES * M.prow : P.m;
+            k1_stopped_rows(P, r0, r1, threadIdx.x, blockDim.x);
+        }
+        return;
+    }
     const int wv = threadIdx.x / WAVE, lane = lane_id();
     const int64_t panel = rb * PANEL_WAVES + wv;
     double s[4] = {0.0, 0.0, 0.0, 0.0};
@@ -231,7 +248,11 @@ __global__ __launch_bounds__(256) void bb_k1_sum(bsls_bb_problem P, int64_t iter
                                                  int64_t r0, int64_t r1, double *part,
                                                  unsigned *ticket) {
     __shared__ double red[4];
-    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
+        k1_stopped_rows(P, r0, r1, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                        (int64_t)gridDim.x * blockDim.x);
+        return;
+    }
     // grid-stride rows: with REDUCE the launch is capped at K1_SUM_GRID
     // workgroups (one per 256 rows made 3.9k arrivals at the ||r||^2 tickets
     // at m = 1M: 12.5 us against 4.6 without the reduction)
@@ -267,11 +288,17 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ double red[16];
     __shared__ int row_last;
-    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_tiles &T = P.At;
     int64_t rb, g;
     tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, g);
     rb += rb_base;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
+        // (several groups with the split finish: bb_k1_sum zeroes the rows)
+        if (g == 0 && (T.ngroups == 1 || !BSLS_K1_SPLIT))
+            k1_stopped_rows(P, rb * T.H, (rb * T.H + T.H < P.m) ? rb * T.H + T.H : P.m,
+                            threadIdx.x, blockDim.x);
+        return;
+    }
     const int HR = (int)tile_lds_doubles(T, false);
     for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;
     __syncthreads();
@@ -316,13 +343,17 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
 // product; the rows' scales sit in LDS beside the sums); MODE 3: scaled
 // incidence with several groups (no bit pattern to keep): w_i = colv_i *
 // sum r, one product per row after the group sums, and the whole LDS for rows.
-template <int MODE, bool ITER>
+// FUSE (stage 8, column-sharded): the finishing workgroup of row block rb also
+// sums r_i^2 over the rows [rb m / nrb, (rb + 1) m / nrb) of r (already the
+// all-reduced residual), and the last one records f and runs the stopping
+// test of iteration iter - 1 before it stores this iteration's sums.
+template <int MODE, bool ITER, bool FUSE = false>
 __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
                                                const double *__restrict__ gp,
                                                double *__restrict__ gout, double *part,
-                                               unsigned *ticket, unsigned *tk2rb) {
+                                               unsigned *ticket, unsigned *tk2rb, int64_t iter) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    __shared__ double red[4 * 16];
+    __shared__ double red[5 * 16];
     __shared__ int row_last;
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_tiles &T = P.ATt;
@@ -373,7 +404,10 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
             __syncthreads();
         }
     }
-    double sums[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int NS = FUSE ? 5 : 4;
+    double sums[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) sums[q] = 0.0;
     if (fin) {
         // K2E rows per thread per batch: every z index, then every operand of
         // the batch in flight at once (two round trips per batch instead of
@@ -423,15 +457,23 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
         }
     }
     if (!ITER || !fin) return;
-    block_sum<4>(sums, red);
-    double tot[4];
+    if constexpr (FUSE) {
+        const int64_t q0 = rb * P.m / T.nrb, q1 = (rb + 1) * P.m / T.nrb;
+        for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
+            const double v = P.r[i];
+            sums[4] += v * v;
+        }
+    }
+    block_sum<NS>(sums, red);
+    double tot[NS];
     // one slot per row block, summed in row-block order: with several groups
     // the finishing workgroup of a block varies from run to run, so its
     // blockIdx must not decide where the block's sums enter the reduction
-    const bool last = (G == 1) ? last_block_sum<4>(sums, part, ticket, tot, red)
-                               : last_of_sum<4>(sums, part, (unsigned)rb, (unsigned)T.nrb, ticket,
-                                                tot, red);
+    const bool last = (G == 1) ? last_block_sum<NS>(sums, part, ticket, tot, red)
+                               : last_of_sum<NS>(sums, part, (unsigned)rb, (unsigned)T.nrb, ticket,
+                                                 tot, red);
     if (last && threadIdx.x == 0) {
+        if constexpr (FUSE) bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
@@ -441,7 +483,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
 
 // Multi-GPU stage 2: r (already all-reduced) += target, ||r||^2, stop test.
 __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t iter, double *part,
-                                                   unsigned *ticket) {
+                                                   unsigned *ticket, int add_target) {
     __shared__ double red[4];
     if (iter > 0 && P.scal[BSLS_S_STOP] != 0.0) return;
     // grid-stride over at most R_FINISH_GRID workgroups (the launch below):
@@ -450,8 +492,11 @@ __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t it
     const int64_t gs = (int64_t)gridDim.x * blockDim.x;
     double sq[1] = {0.0};
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.m; i += gs) {
-        const double o = P.r[i] + P.target[i];
-        P.r[i] = o;
+        double o = P.r[i];
+        if (add_target) {
+            o += P.target[i];
+            P.r[i] = o;
+        }
         sq[0] += o * o;
     }
     block_sum<1>(sq, red);
@@ -470,11 +515,11 @@ constexpr int R_FINISH_GRID = 512;
 // no faster).  The ITER epilogue reads g_prev and dz = z - z_prev (K3 wrote
 // dz from the z's it holds, bit-identical to the subtraction here): 15.2 MB
 // that no walk overlaps, where z and z_prev were 22.8 MB.
-template <int MODE, bool ITER>
+template <int MODE, bool ITER, bool FUSE = false>
 __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *__restrict__ dzv,
                                               const double *__restrict__ gp,
                                               double *__restrict__ gout, double *part,
-                                              unsigned *ticket) {
+                                              unsigned *ticket, int64_t iter) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
     const bsls_panels &M = P.AT;
@@ -505,7 +550,10 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
         nx[q] = (lane < 63) ? dn : wrap;
     }
     __syncthreads();   // the chunk table becomes the reduction scratch below
-    double sums[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int NS = FUSE ? 5 : 4;
+    double sums[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) sums[q] = 0.0;
     // epilogue operands: unconditional loads at clamped indices, all in flight
     int32_t j[4];
     double gpj[4], dzj[4];
@@ -541,9 +589,18 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
         }
     }
     if (!ITER) return;
-    block_sum<4>(sums, lds);
-    double tot[4];
-    if (last_block_sum<4>(sums, part, ticket, tot, lds) && threadIdx.x == 0) {
+    if constexpr (FUSE) {   // stage 8: this workgroup's slice of ||r||^2 (see bb_k2t)
+        const int64_t q0 = (int64_t)blockIdx.x * P.m / gridDim.x;
+        const int64_t q1 = ((int64_t)blockIdx.x + 1) * P.m / gridDim.x;
+        for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
+            const double v = P.r[i];
+            sums[4] += v * v;
+        }
+    }
+    block_sum<NS>(sums, lds);
+    double tot[NS];
+    if (last_block_sum<NS>(sums, part, ticket, tot, lds) && threadIdx.x == 0) {
+        if constexpr (FUSE) bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
@@ -851,34 +908,35 @@ static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, h
     }
 }
 
-template <int MODE, bool ITER>
+template <int MODE, bool ITER, bool FUSE>
 static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *gout,
-                           const BBWork &w, hipStream_t st) {
-    allow_lds(bb_k2<MODE, ITER>);
-    bb_k2<MODE, ITER><<<grid_for(P.AT.npanels, PANEL_WAVES), 1024, panel_lds_bytes(P.AT), st>>>(
-        P, w.dz, gp, gout, w.p2, w.tk2);
+                           const BBWork &w, hipStream_t st, int64_t iter) {
+    allow_lds(bb_k2<MODE, ITER, FUSE>);
+    bb_k2<MODE, ITER, FUSE><<<grid_for(P.AT.npanels, PANEL_WAVES), 1024, panel_lds_bytes(P.AT),
+                              st>>>(P, w.dz, gp, gout, w.p2, w.tk2, iter);
 }
 
-template <int MODE, bool ITER>
+template <int MODE, bool ITER, bool FUSE>
 static void launch_k2t_mode(const bsls_bb_problem &P, const double *gp, double *gout,
-                            const BBWork &w, hipStream_t st) {
-    allow_lds(bb_k2t<MODE, ITER>);
-    bb_k2t<MODE, ITER><<<(int)(P.ATt.nrb * P.ATt.ngroups), BSLS_TILE_THREADS,
-                         tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(P, w.dz, gp, gout, w.p2,
-                                                                       w.tk2, w.tk2rb);
+                            const BBWork &w, hipStream_t st, int64_t iter) {
+    allow_lds(bb_k2t<MODE, ITER, FUSE>);
+    bb_k2t<MODE, ITER, FUSE><<<(int)(P.ATt.nrb * P.ATt.ngroups), BSLS_TILE_THREADS,
+                               tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(
+        P, w.dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter);
 }
 
-template <bool ITER>
+template <bool ITER, bool FUSE = false>
 static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
-                      const BBWork &w, hipStream_t st) {
+                      const BBWork &w, hipStream_t st, int64_t iter = 0) {
     if (P.ATt.ent) {
-        if (!P.colv) launch_k2t_mode<1, ITER>(P, gp, gout, w, st);
-        else if (P.ATt.ngroups == 1 && P.ATt.layout == 0) launch_k2t_mode<2, ITER>(P, gp, gout, w, st);
-        else launch_k2t_mode<3, ITER>(P, gp, gout, w, st);
+        if (!P.colv) launch_k2t_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter);
+        else if (P.ATt.ngroups == 1 && P.ATt.layout == 0)
+            launch_k2t_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter);
+        else launch_k2t_mode<3, ITER, FUSE>(P, gp, gout, w, st, iter);
     } else if (P.colv) {
-        launch_k2_mode<2, ITER>(P, gp, gout, w, st);
+        launch_k2_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter);
     } else {
-        launch_k2_mode<1, ITER>(P, gp, gout, w, st);
+        launch_k2_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter);
     }
 }
 
@@ -933,6 +991,7 @@ static bool tiles_ok(const bsls_tiles &T, int64_t rows, int64_t cols, int64_t ha
 
 static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
+    if (p->shard_role < 0 || p->shard_role > 2) return BSLS_E_ARG;
     const bool general = p->colv == nullptr;
     if (p->At.ent) {
         if (!tiles_ok(p->At, p->m, p->n, 0, general, false)) return BSLS_E_ARG;
@@ -1187,13 +1246,23 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
             BSLS_CHECK(hipMemsetAsync(P.scal, 0, BSLS_S_COUNT * sizeof(double), st));
             BSLS_CHECK(hipMemsetAsync(P.work, 0, (size_t)((char *)w.p1 - (char *)P.work), st));
             return BSLS_OK;
-        case 1:  // r_partial = A_g x_g
-            if (iter > 0) launch_k1<false, false, true>(P, iter, w, st);
-            else launch_k1<false, false, false>(P, iter, w, st);
+        case 1:  // r_partial = A_g x_g (+ target on the shard_role 1 rank)
+            if (P.shard_role == 1) {
+                if (iter > 0) launch_k1<true, false, true>(P, iter, w, st);
+                else launch_k1<true, false, false>(P, iter, w, st);
+            } else {
+                if (iter > 0) launch_k1<false, false, true>(P, iter, w, st);
+                else launch_k1<false, false, false>(P, iter, w, st);
+            }
             break;
         case 2:  // r += target, ||r||^2, stop test
+        case 9:  // ||r||^2, stop test (r already the residual)
             bb_r_finish<<<(grid_for(P.m, 256) < R_FINISH_GRID ? grid_for(P.m, 256) : R_FINISH_GRID),
-                          256, 0, st>>>(P, iter, w.pf, w.tkf);
+                          256, 0, st>>>(P, iter, w.pf, w.tkf, stage == 2 ? 1 : 0);
+            break;
+        case 8:  // stage 3 with stage 9 of iteration iter - 1 folded in
+            if (iter <= 0) return BSLS_E_ARG;
+            launch_k2<true, true>(P, P.g[zc], P.g[zn], w, st, iter);
             break;
         case 3:  // g = N'A'r (+ sums)
             if (iter > 0) launch_k2<true>(P, P.g[zc], P.g[zn], w, st);
@@ -1238,8 +1307,13 @@ extern "C" int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int
     if (rb0 < 0 || rb1 <= rb0 || rb1 > k1_row_blocks(P)) return BSLS_E_ARG;
     const BBWork w = bb_layout(P);
     hipStream_t st = (hipStream_t)stream;
-    if (iter > 0) launch_k1<false, false, true>(P, iter, w, st, rb0, rb1);
-    else launch_k1<false, false, false>(P, iter, w, st, rb0, rb1);
+    if (P.shard_role == 1) {
+        if (iter > 0) launch_k1<true, false, true>(P, iter, w, st, rb0, rb1);
+        else launch_k1<true, false, false>(P, iter, w, st, rb0, rb1);
+    } else {
+        if (iter > 0) launch_k1<false, false, true>(P, iter, w, st, rb0, rb1);
+        else launch_k1<false, false, false>(P, iter, w, st, rb0, rb1);
+    }
     BSLS_LAUNCH_CHECK();
     return BSLS_OK;
 }

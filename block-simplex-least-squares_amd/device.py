@@ -847,6 +847,14 @@ class BBEngine:
         check(_native.lib().bsls_bb_stage(self.P, int(k), int(it), stream_handle()),
               'bsls_bb_stage %d' % k)
 
+    def set_shard_role(self, role):
+        """bsls_bb_problem.shard_role: 0 the whole problem here, 1 a column
+        shard that adds target to its partial residual, 2 another column shard
+        (distributed.ShardedBB)."""
+        if role not in (0, 1, 2):
+            raise ValueError('shard role must be 0, 1 or 2')
+        self.P.shard_role = int(role)
+
     def row_blocks(self):
         """(K1 row blocks, rows per block): the granule of residual_rows."""
         R = ctypes.c_int64(0)

@@ -7,12 +7,17 @@ blockify() already makes each block's columns contiguous
 blocks = a column slice A_g (m x n_g), its transpose, and its slices of
 z, g, x.  Per BB iteration:
 
-    stage 3   g_g = N_g' A_g' r  and the four local BB sums
+    stage 8   g_g = N_g' A_g' r  and the four local BB sums; folded into it, the
+              previous iteration's ||r||^2, f and stopping test (r is the same
+              all-reduced vector on every rank, so every rank decides alike)
     all-reduce(sum) of the 4 BB sums  (32 bytes)
     stage 4   t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = x0_g + N_g z_g   (local)
-    stage 1   r_g = A_g x_g   (partial residual, length m)
+    stage 1   r_g = A_g x_g, + target on rank 0 (partial residual, length m)
     all-reduce(sum) of r_g  (8 m bytes: the one real exchange of the algorithm)
-    stage 2   r += target, ||r||^2, f, stopping test (redundant on every rank)
+and after the last iteration of a call stage 9 (||r||^2, f, stopping test of
+that iteration).  Once the run has stopped, ranks other than 0 write r = 0 in
+stage 1 and rank 0 leaves its r (the final residual) alone, so the all-reduce
+keeps the final residual intact (csrc/bb.hip k1_stopped_rows).
 
 The collectives go through torch.distributed: backend "nccl" is RCCL over xGMI
 on MI355X; "gloo" runs the same orchestration in CPU tests with a fake stage
@@ -68,8 +73,11 @@ class ShardedBB:
 
     SUMS = slice(5, 9)   # scal[SUMDG..GG]
 
-    def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None):
+    def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None, rank=0):
         self.e = engine
+        # rank 0 adds target to its partial residual; the others zero theirs
+        # once the run has stopped (bsls_bb_problem.shard_role)
+        engine.set_shard_role(1 if rank == 0 else 2)
         self.all_reduce = all_reduce
         self.all_reduce_async = all_reduce_async
         self.parts = int(parts) if all_reduce_async is not None else 1
@@ -99,21 +107,21 @@ class ShardedBB:
         e = self.e
         e.stage(0, 0)
         e.stage(5, 0)            # z[1] = z0 + 1, x = x0 + N z[1]
-        self.residual(0)
-        e.stage(2, 0)            # r(z0 + 1)
+        self.residual(0)         # r(z0 + 1)
         e.stage(3, 0)            # g_prev = grad(z0 + 1) -> g[0]
         e.stage(6, 0)            # x = x0 + N z0
-        self.residual(0)
-        e.stage(2, 0)            # r(z0), f(z0)
+        self.residual(0)         # r(z0)
+        e.stage(9, 0)            # f(z0)
 
     def iterate(self, first, count):
         e = self.e
         for i in range(first, first + count):
-            e.stage(3, i)
+            e.stage(8, i)        # K2 + f / stopping test of iteration i - 1
             self.all_reduce(e.scal[self.SUMS])
             e.stage(4, i)
             self.residual(i)
-            e.stage(2, i)
+        if count > 0:
+            e.stage(9, first + count - 1)   # f / stopping test of the last one
 
 
 def torch_all_reduce(group=None):

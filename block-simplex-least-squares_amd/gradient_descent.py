@@ -62,7 +62,7 @@ class GradientDescent:
         e = self.engine
         if self.method == 'LBFGS':
             f, nabla_f, proj = self._device_closures() if e else (self.f, self.nabla_f, self.proj)
-            z0 = self._z0_device()
+            z0 = self._z0_device() if e else self.z0
             LBFGS.solve(z0 + 1, f, nabla_f, solvers.stopping, log=self.log, proj=proj,
                         options=self.options)
             logging.debug('Took %s time' % str(np.sum(self.times)))
@@ -76,7 +76,21 @@ class GradientDescent:
                          proj=self.proj, options=self.options)
         elif self.method == 'DORE':
             if e is None:
-                raise ValueError("method 'DORE' needs the device engine (main.solve_in_z)")
+                if self.A is None or self.N is None or self.target is None:
+                    raise ValueError("method 'DORE' needs the device engine (main.solve_in_z) "
+                                     "or A, N and target (the host path, main.solve_in_z_cpu)")
+                # the host path (gradient_descent.py:55-67 as the reference runs it)
+                alpha = 0.99
+                lsv = lsv_operator(self.A, self.N)
+                logging.info('Largest singular value: %s' % lsv)
+                A_dore = self.A * alpha / lsv
+                target_dore = self.target * alpha / lsv
+                N = self.N
+                DORE.solve(self.z0, lambda z: A_dore.dot(N.dot(z)),
+                           lambda r: N.T.dot(A_dore.T.dot(r)), target_dore, proj=self.proj,
+                           log=self.log, options=self.options, record_every=100)
+                self.lsv = lsv
+                return self.iters, self.times, self.states
             alpha = 0.99
             lsv = lsv_operator(e, None)
             logging.info('Largest singular value: %s' % lsv)

@@ -33,6 +33,9 @@ def parser():
     p.add_argument('--eq', dest='eq', type=str, default='CP',
                    help='Type of equality constraint (CP or OD)')
     p.add_argument('--noise', dest='noise', type=float, default=None, help='Noise level')
+    p.add_argument('--device', dest='device', choices=['gpu', 'cpu'], default=None,
+                   help='gpu (default: the MI355X engine) or cpu (the reference\'s own path: '
+                        'SciPy closures + the host c_extensions library; also BSLS_DEVICE=cpu)')
     p.add_argument('--deterministic', dest='deterministic', action='store_true', default=None,
                    help='fixed-order SpMV sums (bit-reproducible runs and exit iterations); '
                         'also BSLS_DETERMINISTIC=1')
@@ -78,6 +81,78 @@ def solve_in_z(A, b, x0, N, block_sizes, method, options=None, engine=None, dete
     x = eng.n_apply(zl, with_x0=True).cpu().numpy()   # particular_x0 + N z
     assert np.all(x >= 0), "x shouldn't have negative entries after projection"
     return iters, times, states
+
+
+def solve_in_z_cpu(A, b, x0, N, block_sizes, method, options=None):
+    """python/main.py:41-79 on the host (BASELINE configs[0]): the reference's
+    closures over SciPy csr_matvec, proj = the host c_extensions library's
+    isotonic_regression_multi (include/bsls_cpu.h) + clip, the solver loops of
+    BB.py / LBFGS.py / DORE.py over them."""
+    import numpy.linalg as la
+    from bsls_utils import particular_x0
+    from c_extensions import _cpu
+    if block_sizes is not None and len(block_sizes) == A.shape[1]:
+        logging.error('Trivial example: nblocks == nroutes, exiting solver')
+        sys.exit()
+    block_sizes = np.asarray(block_sizes)
+    assert np.all(block_sizes >= 2)
+    z0 = x2z(x0, block_sizes)
+    target = A.dot(x0) - b
+    AT = A.T.tocsr()
+    NT = N.T.tocsr()
+    f = lambda z: 0.5 * la.norm(A.dot(N.dot(z)) + target) ** 2
+    nabla_f = lambda z: NT.dot(AT.dot(A.dot(N.dot(z)) + target))
+    cum_blocks = np.concatenate(([0], np.cumsum(block_sizes - 1)))
+
+    def proj(x):
+        _cpu.isotonic(1, x, cum_blocks[:-1], x.shape[0], None, 1)
+        return np.maximum(np.minimum(x, 1.), 0.)
+    kw = dict(A=A, N=N, target=target) if method == 'DORE' else {}
+    gd = GradientDescent(z0=z0, f=f, nabla_f=nabla_f, proj=proj, method=method, options=options,
+                         **kw)
+    iters, times, states = gd.run()
+    x = particular_x0(block_sizes) + N.dot(states[-1])
+    assert np.all(x >= 0), "x shouldn't have negative entries after projection"
+    return iters, times, states
+
+
+def LS_postprocess_cpu(states, x0, A, b, x_true, scaling=None, block_sizes=None, output=None,
+                       N=None, is_x=False):
+    """python/main.py:81-136 on the host (NumPy / SciPy)."""
+    import numpy.linalg as la
+    if x_true is None:
+        return [], [], output
+    if scaling is None:
+        scaling = np.ones(x_true.shape)
+    if output is None:
+        output = {}
+    d = len(states)
+    if not is_x and N.size > 0:
+        x_hat = N.dot(np.array(states).T) + np.tile(x0, (d, 1)).T
+    else:
+        x_hat = np.array(states).T
+    x_last = x_hat[:, -1]
+    n = x_hat.shape[1]
+    output['AA'] = A.shape
+    output['x_hat'] = x_hat.shape
+    output['blocks'] = block_sizes.shape if block_sizes is not None else None
+    starting_error = 0.5 * la.norm(A.dot(x0) - b) ** 2
+    opt_error = 0.5 * la.norm(A.dot(x_true) - b) ** 2
+    diff = A.dot(x_hat) - np.tile(b, (d, 1)).T
+    error = 0.5 * np.diag(diff.T.dot(diff))
+    output['0.5norm(Ax-b)^2'], output['0.5norm(Ax_init-b)^2'] = error, starting_error
+    output['0.5norm(Ax*-b)^2'] = opt_error
+    x_true_block = np.tile(x_true, (n, 1))
+    x_diff = x_true_block - x_hat.T
+    scaling_block = np.tile(scaling, (n, 1))
+    x_diff_scaled = scaling_block * x_diff
+    x_true_scaled = scaling_block * x_true_block
+    output['max|f * (x-x_true)|'] = np.max(x_diff_scaled, axis=1)
+    output['incorrect x entries'] = np.bincount(np.where(x_diff > 1e-3)[0])
+    output['percent flow allocated incorrectly'] = (np.sum(np.abs(x_diff_scaled), axis=1)
+                                                    / np.sum(x_true_scaled, axis=1))
+    output['max|f * (x_init-x_true)|'] = np.max(scaling * np.abs(x_true - x0))
+    return x_last, error, output
 
 
 def LS_postprocess(states, x0, A, b, x_true, scaling=None, block_sizes=None, output=None, N=None,
@@ -161,6 +236,15 @@ def main(args=None, plot=False):
     if args.noise:
         delta = np.random.normal(scale=bb * args.noise)
         bb = bb + delta
+    device = getattr(args, 'device', None)
+    if device is None:
+        import _native
+        device = 'cpu' if _native.device_mode() == 'cpu' else 'gpu'
+    if device == 'cpu':
+        iters, times, states = solve_in_z_cpu(AA, bb, x0, N, block_sizes, args.method)
+        x_last, error, output = LS_postprocess_cpu(states, x0, AA, bb, x_split, scaling=scaling,
+                                                   block_sizes=block_sizes, N=N, output=output)
+        return iters, times, states, output
     eng = build_engine(AA, bb, x0, block_sizes,
                        deterministic=getattr(args, 'deterministic', None))
     iters, times, states = solve_in_z(AA, bb, x0, N, block_sizes, args.method, engine=eng)

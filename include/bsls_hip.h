@@ -292,7 +292,11 @@ typedef struct bsls_bb_problem {
     int64_t max_iter;               /* options['max_iter'] */
     double opt_tol;                 /* options['opt_tol'] */
     int32_t early_exit;             /* 0 disables every early exit (fixed-count timing) */
-    int32_t reserved;
+    int32_t shard_role;             /* 0: the whole problem on one GCD; column-sharded
+                                     * (bsls_bb_stage 1 is this rank's partial residual):
+                                     * 1 = the rank that adds target to its partial, 2 = the
+                                     * others, whose stage 1 writes r = 0 once the run has
+                                     * stopped (so the all-reduce leaves the final r as it was) */
     /* Tile images replacing the panels when their ent is not NULL (then A / AT
      * are not read): At for K1 (halo 0; ngroups partials in rpart), ATt for K2
      * (halo 1; with ngroups > 1 the partial row sums go through wpart,
@@ -328,7 +332,8 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
 /* The building blocks, for multi-GPU column sharding where RCCL all-reduces sit
  * between them (A_g = the rank's block-aligned column slice):
  *   0  reset scal[] and the reduction tickets
- *   1  r = A_g x_g            (partial residual; all-reduce r afterwards)
+ *   1  r = A_g x_g            (partial residual; all-reduce r afterwards); with
+ *      shard_role 1 r = A_g x_g + target (the sum over ranks is the residual)
  *   2  r += target, ||r||^2, f, stopping test of iteration `iter` (iter 0: none)
  *   3  g = N'A'r -> g[iter & 1]; iter > 0 also dg and the four BB sums into
  *      scal[SUMDG..GG] (all-reduce those four afterwards)
@@ -336,8 +341,15 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  *   5  z[1] = z[0] + 1, x = N z[1]           (prologue)
  *   6  x = N z[0]                             (prologue)
  *   7  single GCD: r = A x + target, ||r||^2, f, stopping test (= 1 then 2 fused)
+ *   8  stage 3 (iter >= 1) with stage 9 of iteration iter - 1 folded into it:
+ *      every workgroup also sums its slice of r^2, and the last one records f
+ *      and runs the stopping test of iter - 1 (with the all-reduced g.g of
+ *      iter - 1) before it stores iteration iter's four sums
+ *   9  ||r||^2, f, stopping test of iteration `iter` (r already the residual)
  * One iteration i >= 1 = 3, [allreduce sums], 4, 1, [allreduce r], 2; on one GCD
- * bsls_bb_iterate runs 3, 4, 7. */
+ * bsls_bb_iterate runs 3, 4, 7.  The column-sharded driver (distributed.py,
+ * shard_role 1 / 2) runs 8, [allreduce sums], 4, 1, [allreduce r] per
+ * iteration and 9 after the last one. */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 /* Stage 1 restricted to K1's row blocks [rb0, rb1) (rows rb0 * R .. rb1 * R - 1,
  * R = *rows_per_block from bsls_bb_row_blocks, which returns the block count):

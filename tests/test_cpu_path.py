@@ -1,0 +1,203 @@
+"""The host path of the drop-in (include/bsls_cpu.h, lib/libbsls_cpu.so;
+c_extensions with BSLS_DEVICE=cpu; main.py --device cpu): BASELINE configs[0],
+the reference's CPU c_extensions path on the tests/fast problems.  CPU tests:
+the library against the reference's own golden vectors (bit for bit) and
+main.main on the tests/fast/test_main.py problems against the reference's runs
+(tests/golden/solvers.npz) -- same logged iterations, same states bit for bit
+(the closures are the reference's SciPy products and the projections are
+bit-identical), 0.5||Ax - b||^2 < 1e-16 (tests/fast/test_main.py:31-47)."""
+import argparse
+import os
+
+import numpy as np
+import pytest
+
+SEED = 237423433
+
+
+@pytest.fixture
+def cpu_mode():
+    import _native
+    _native.set_device('cpu')
+    yield _native
+    _native.set_device(None)
+
+
+def exact(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+def test_cpu_library_exports_every_declared_symbol(cpu_mode):
+    L = cpu_mode.cpu_lib()
+    syms = cpu_mode.declared_cpu_symbols()
+    assert len(syms) >= 9
+    for s in syms:
+        assert hasattr(L, s), s
+
+
+def test_no_silent_cpu_path():
+    """Without the explicit selection the package never runs on the CPU."""
+    import _native
+    assert _native.device_mode() == 'hip' or os.environ.get('BSLS_DEVICE') == 'cpu'
+
+
+@pytest.mark.parametrize('threads', ['1', '4'])
+def test_projections_vs_golden(cpu_mode, golden, monkeypatch, threads):
+    from c_extensions import c_extensions as cx
+    monkeypatch.setenv('BSLS_CPU_THREADS', threads)
+    d = golden('proj_simplex.npz')
+    for ci in range(int(d['ncases'])):
+        y, b = d['c%d_y' % ci], d['c%d_blocks' % ci]
+        a = y.copy()
+        cx.proj_multi_simplex_c(a, b)
+        assert exact(a, d['c%d_simplex' % ci]), ci
+        a = y.copy()
+        cx.proj_multi_ball_c(a, b)
+        assert exact(a, d['c%d_ball' % ci]), ci
+    a = d['single_y'].copy()
+    cx.proj_simplex_c(a, 10, 40)
+    assert exact(a, d['single_out'])
+
+
+@pytest.mark.parametrize('threads', ['1', '4'])
+def test_isotonic_vs_golden(cpu_mode, golden, monkeypatch, threads):
+    from c_extensions import c_extensions as cx
+    monkeypatch.setenv('BSLS_CPU_THREADS', threads)
+    d = golden('isotonic.npz')
+    fns = {'v1': cx.isotonic_regression_multi_c, 'v3': cx.isotonic_regression_multi_c_3}
+    for ci in range(int(d['ncases'])):
+        y, b = d['c%d_y' % ci], d['c%d_blocks' % ci]
+        for tag, fn in fns.items():
+            for upd in (1, 0):
+                a = y.copy()
+                w = np.ones(y.shape[0], dtype=np.int32)      # int32: updated in place
+                fn(a, b, w, upd)
+                assert exact(a, d['c%d_%s_u%d' % (ci, tag, upd)]), (ci, tag, upd)
+                assert np.array_equal(w, d['c%d_%s_u%d_w' % (ci, tag, upd)]), (ci, tag, upd)
+        a = y.copy()
+        cx.isotonic_regression_multi_c_2(a, b)
+        assert exact(a, d['c%d_v2' % ci]), ci
+    a = np.array([4., 5., 1., 6., 8., 7.])
+    cx.isotonic_regression_c(a, 0, 6)
+    assert exact(a, d['kat_single'])
+
+
+def test_buffer_semantics(cpu_mode):
+    """c_extensions.pyx: a non-contiguous y is projected into a copy (the caller
+    sees no change); weight=None leaves no trace; an int64 weight is copied;
+    the asserts fire before anything runs."""
+    from c_extensions import c_extensions as cx
+    y = np.arange(20, dtype=np.float64)[::2].copy()
+    base = np.zeros(40)
+    view = base[::2]
+    view[:] = np.linspace(-1, 2, 20)
+    before = base.copy()
+    cx.proj_multi_simplex_c(view, np.array([0, 5], dtype=np.int64))
+    assert np.array_equal(base, before)
+    w64 = np.ones(10, dtype=np.int64)
+    cx.isotonic_regression_multi_c(y[::-1].copy(), np.array([0], dtype=np.int64), w64)
+    assert np.all(w64 == 1)
+    with pytest.raises(AssertionError):
+        cx.proj_multi_simplex_c(y.copy(), np.array([0, 0], dtype=np.int64))
+    with pytest.raises(ValueError):
+        cx.proj_multi_simplex_c(y.astype(np.float32), np.array([0], dtype=np.int64))
+    with pytest.raises(ValueError):
+        cx.isotonic_regression_multi_c(y.copy(), np.array([0], dtype=np.int64),
+                                       np.zeros(10, dtype=np.int32))
+
+
+def test_xz_quad_vs_golden(cpu_mode, golden):
+    from c_extensions import c_extensions as cx
+    d = golden('xz_quad.npz')
+    for ci in range(int(d['nxz'])):
+        x, b = d['c%d_x' % ci], d['c%d_blocks' % ci]
+        nz = d['c%d_z' % ci].shape[0]
+        z = np.zeros(nz)
+        cx.x2z_c(x, z, b)
+        assert exact(z, d['c%d_z' % ci]), ci
+        x2 = np.zeros(x.shape[0])
+        cx.z2x_c(x2, z, b)
+        assert exact(x2, d['c%d_xback' % ci]), ci
+    for qi in range(int(d['nquad'])):
+        g = np.zeros(d['q%d_x' % qi].shape[0])
+        f = cx.quad_obj_c(d['q%d_x' % qi], d['q%d_Q' % qi].flatten(), d['q%d_c' % qi], g)
+        assert f == float(d['q%d_f' % qi]) and exact(g, d['q%d_g' % qi]), qi
+
+
+@pytest.mark.parametrize('vi', [0, 1, 2])
+def test_main_cpu_path_vs_reference(golden, tmp_path, vi):
+    """BASELINE configs[0]: main.py --method BB --device cpu on the
+    tests/fast/test_main.py problems: the same run as the reference's."""
+    import bsls_utils
+    import main
+    G = golden('solvers.npz')
+    kw = [{}, {'alpha': 0.5}, {'A_sparse': 0.05}][vi]
+    np.random.seed(SEED)
+    fname = os.path.join(str(tmp_path), 'test_main.mat')
+    bsls_utils.generate_data(fname=fname, **kw)
+    args = argparse.Namespace(noise=0, file=fname, log='WARN', init=False, eq='CP',
+                              method='BB', device='cpu')
+    iters, times, states, output = main.main(args=args)
+    err = np.asarray(output['0.5norm(Ax-b)^2'])
+    assert err[-1] < 1e-16, err                         # tests/fast/test_main.py:31-47
+    assert list(iters) == list(G['main%d_iters' % vi])
+    for k, s in enumerate(states):
+        assert exact(s, G['main%d_states' % vi][k]), k
+    assert exact(err, G['main%d_err' % vi])
+    assert float(output['0.5norm(Ax_init-b)^2']) == float(G['main%d_err0' % vi])
+
+
+_DORE_CHILD = r"""
+import sys, numpy as np, scipy.sparse as sps
+sys.path[:0] = [%r, %r]
+from bsls_utils import particular_x0, block_sizes_to_N
+from main import solve_in_z_cpu
+G = np.load(%r)
+A = sps.csr_matrix((G['dore_A_data'], G['dore_A_indices'], G['dore_A_indptr']),
+                   shape=tuple(G['dore_A_shape']))
+sizes = G['dore_block_sizes']
+iters, _, states = solve_in_z_cpu(A, G['dore_b'], particular_x0(sizes), block_sizes_to_N(sizes),
+                                  sizes, 'DORE', options={'max_iter': 300, 'verbose': 0,
+                                                          'opt_tol': 1e-30})
+assert list(iters) == list(G['dore_iters']), (iters, G['dore_iters'])
+for k, s in enumerate(states):
+    ref = G['dore_states'][k]
+    assert np.max(np.abs(s - ref)) <= 1e-10 * max(1.0, np.max(np.abs(ref))), k
+print('ok')
+"""
+
+
+def test_dore_cpu_path():
+    """GradientDescent('DORE') on the host path (no engine) against the
+    reference's run (tests/golden/solvers.npz dore_*).  In a fresh process:
+    ARPACK's starting vector comes from a generator whose state persists
+    across calls in a process, and the fixture is the first call's."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = _DORE_CHILD % (root, os.path.join(root, 'block-simplex-least-squares_amd'),
+                          os.path.join(here, 'golden', 'solvers.npz'))
+    out = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().endswith('ok'), out.stderr[-2000:]
+
+
+def test_lbfgs_cpu_path(golden):
+    """GradientDescent('LBFGS') on the host path (no engine): the reference's
+    run (tests/golden/plugins.npz lbfgs_*), bit for bit."""
+    import scipy.sparse as sps
+    from bsls_utils import particular_x0, block_sizes_to_N
+    from main import solve_in_z_cpu
+    P = golden('plugins.npz')
+    A = sps.csr_matrix((P['lbfgs_A_data'], P['lbfgs_A_indices'], P['lbfgs_A_indptr']),
+                       shape=tuple(P['lbfgs_A_shape']))
+    sizes = P['lbfgs_block_sizes']
+    x0 = particular_x0(sizes)
+    iters, _, states = solve_in_z_cpu(A, P['lbfgs_b'], x0, block_sizes_to_N(sizes), sizes,
+                                      'LBFGS', options={'max_iter': 5, 'verbose': 0,
+                                                        'opt_tol': 1e-30})
+    assert list(iters) == list(P['lbfgs_iters'])
+    for k, s in enumerate(states):
+        assert exact(s, P['lbfgs_states'][k]), k

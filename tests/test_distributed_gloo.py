@@ -35,6 +35,10 @@ class FakeStages:
         self.x = np.zeros(self.n)
         self.r = torch.zeros(A.shape[0], dtype=torch.float64)
         self.scal = torch.zeros(16, dtype=torch.float64)
+        self.role = 0
+
+    def set_shard_role(self, role):
+        self.role = role
 
     def Nz(self, z):
         out = np.empty(self.n)
@@ -55,9 +59,32 @@ class FakeStages:
     def row_blocks(self):
         return -(-self.A.shape[0] // self.ROWS), self.ROWS
 
+    def _partial(self, it, r0, r1):
+        """stage 1 on rows [r0, r1): A_g x_g (+ target with role 1); once
+        stopped, role 2 writes 0 and role 1 keeps r (bsls_bb_problem.shard_role)."""
+        if it > 0 and float(self.scal[0]) != 0:
+            if self.role == 2:
+                self.r[r0:r1] = 0.0
+            return
+        v = self.A[r0:r1].dot(self.x)
+        if self.role == 1:
+            v = v + self.target[r0:r1]
+        self.r[r0:r1] = torch.from_numpy(v)
+
     def residual_rows(self, it, rb0, rb1):
-        r0, r1 = rb0 * self.ROWS, min(rb1 * self.ROWS, self.A.shape[0])
-        self.r[r0:r1] = torch.from_numpy(self.A[r0:r1].dot(self.x))
+        self._partial(it, rb0 * self.ROWS, min(rb1 * self.ROWS, self.A.shape[0]))
+
+    def _record(self, it):
+        """||r||^2, f and the stopping test of iteration it (stage 9)."""
+        s = self.scal
+        if it > 0 and float(s[0]) != 0:
+            return
+        rr = float(self.r.dot(self.r))
+        s[4], s[9] = 0.5 * np.sqrt(rr) ** 2, rr
+        if it > 0:
+            s[1], s[2] = it, it & 1
+            if it >= self.max_iter:
+                s[0] = 2
 
     def stage(self, k, it):
         s = self.scal
@@ -65,16 +92,12 @@ class FakeStages:
         if k == 0:
             s.zero_()
         elif k == 1:
-            self.r[:] = torch.from_numpy(self.A.dot(self.x))
-        elif k == 2:
-            self.r += torch.from_numpy(self.target)
-            rr = float(self.r.dot(self.r))
-            s[4], s[9] = 0.5 * np.sqrt(rr) ** 2, rr
-            if it > 0:
-                s[1], s[2] = it, it & 1
-                if it >= self.max_iter:
-                    s[0] = 2
-        elif k == 3:
+            self._partial(it, 0, self.A.shape[0])
+        elif k == 9:
+            self._record(it)
+        elif k in (3, 8):
+            if it > 0 and float(s[0]) != 0:
+                return
             g = self.Ntw(self.AT.dot(self.r.numpy()))
             if it == 0:
                 self.g[0][:] = g
@@ -82,8 +105,12 @@ class FakeStages:
             self.g[zn][:] = g
             dg = g - self.g[zc]
             dz = self.z[zc] - self.z[zn]
+            if k == 8:
+                self._record(it - 1)     # before this iteration's sums land
             s[5], s[6], s[7], s[8] = dg.sum(), dz.dot(dg), dg.dot(dg), g.dot(g)
         elif k == 4:
+            if float(s[0]) != 0:
+                return
             t = float(s[6]) / float(s[7])
             y = self.z[zc] - t * self.g[zn]
             self.orc.isotonic_regression_multi_c(y, self.zst)
@@ -109,7 +136,7 @@ class _Done:
         pass
 
 
-def _run(rank, world, iters, out_q, parts=1):
+def _run(rank, world, iters, out_q, parts=1, stop_at=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, PKG)
     from oracle import oracle as orc
@@ -133,30 +160,37 @@ def _run(rank, world, iters, out_q, parts=1):
     part = torch.from_numpy(A_g.dot(x0))
     red(part)
     target = part.numpy() - b
-    eng = FakeStages(A_g, A_g.T.tocsr(), sz_g, target, orc, iters)
-    drv = ShardedBB(eng, red, parts=parts, all_reduce_async=red_async)
+    eng = FakeStages(A_g, A_g.T.tocsr(), sz_g, target, orc, stop_at or iters)
+    drv = ShardedBB(eng, red, parts=parts, all_reduce_async=red_async, rank=rank)
     drv.prologue()
     traj = {}
     for i in range(1, iters + 1):
         drv.iterate(i, 1)
         traj[i] = eng.z[i & 1].copy()
-    out_q.put((rank, {k: v for k, v in traj.items() if k in (1, 5, iters)}))
+    res = {k: v for k, v in traj.items() if k in (1, 5, iters)}
+    if stop_at:
+        res['r'] = eng.r.numpy().copy()
+        res['scal'] = eng.scal.numpy().copy()
+    out_q.put((rank, res))
     if world > 1:
         dist.destroy_process_group()
 
 
-def _spawn(world, iters, parts=1):
+def _spawn(world, iters, parts=1, stop_at=None):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
-    os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000) + 7 * parts)
+    os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000) + 7 * parts + (stop_at or 0))
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_run, args=(r, world, iters, q, parts)) for r in range(world)]
+    procs = [ctx.Process(target=_run, args=(r, world, iters, q, parts, stop_at))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if stop_at:
+        return res
     return {i: np.concatenate([res[r][i] for r in range(world)]) for i in res[0]}
 
 
@@ -185,6 +219,20 @@ def test_two_rank_overlapped_residual_matches_single(orc):
     for i in one:
         d = np.max(np.abs(one[i] - three[i])) / max(1.0, np.max(np.abs(one[i])))
         assert d < 1e-10, (i, d)
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_stop_keeps_final_residual(orc):
+    """Iterations enqueued past the stop (max_iter 5, 9 enqueued) leave r the
+    final residual on both ranks -- rank 0 keeps its r, rank 1 writes 0 before
+    each all-reduce -- and the stop is reported at iteration 5 on both."""
+    one = _spawn(1, 9, stop_at=5)
+    two = _spawn(2, 9, stop_at=5)
+    r1 = one[0]['r']
+    for rank in (0, 1):
+        assert two[rank]['scal'][0] == 2 and two[rank]['scal'][1] == 5
+        d = np.max(np.abs(two[rank]['r'] - r1)) / max(1.0, np.max(np.abs(r1)))
+        assert d < 1e-10, (rank, d)
 
 
 def test_row_parts():

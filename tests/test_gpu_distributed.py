@@ -39,7 +39,7 @@ def _partitioned(rank, world):
     return sh, add_noise(full['Ax'], 0.02, seed=33), full
 
 
-def _run(rank, world, backend, port, out_q, fmt=None, parts=1):
+def _run(rank, world, backend, port, out_q, fmt=None, parts=1, max_iter=10 ** 9):
     for p in (ROOT, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -73,28 +73,32 @@ def _run(rank, world, backend, port, out_q, fmt=None, parts=1):
     part = torch.from_numpy(A_g.dot(x0)).cuda()
     dist.all_reduce(part)
     target = part - torch.from_numpy(b).cuda()
-    eng = BBEngine(A_g, None, sz_g, options={'max_iter': 10 ** 9, 'opt_tol': 1e-30},
-                   early_exit=False, target=target, fmt=fmt)
+    eng = BBEngine(A_g, None, sz_g, options={'max_iter': max_iter, 'opt_tol': 1e-30},
+                   early_exit=max_iter < 10 ** 9, target=target, fmt=fmt)
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
     drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
-                    all_reduce_async=torch_all_reduce_async())
+                    all_reduce_async=torch_all_reduce_async(), rank=rank)
     drv.prologue()
     traj = {}
     for i in range(1, ITERS + 1):
         drv.iterate(i, 1)
         if i in CHECK:
-            traj[i] = eng.current_z(i & 1).cpu().numpy().copy()
+            zb = int(eng.scalars()[2]) if max_iter < 10 ** 9 else (i & 1)
+            traj[i] = eng.current_z(zb).cpu().numpy().copy()
+    if max_iter < 10 ** 9:
+        traj['r'] = eng.r.cpu().numpy().copy()
+        traj['scal'] = eng.scalars().copy()
     out_q.put((rank, traj))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _spawn(world, backend, fmt=None, parts=1):
+def _spawn(world, backend, fmt=None, parts=1, max_iter=10 ** 9, raw=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29700 + (os.getpid() % 500) + world + 3 * parts
-    procs = [ctx.Process(target=_run, args=(r, world, backend, port, q, fmt, parts))
+    port = 29700 + (os.getpid() % 500) + world + 3 * parts + (max_iter % 7)
+    procs = [ctx.Process(target=_run, args=(r, world, backend, port, q, fmt, parts, max_iter))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -102,6 +106,8 @@ def _spawn(world, backend, fmt=None, parts=1):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if raw:
+        return res
     return {i: np.concatenate([res[r][i] for r in range(world)]) for i in CHECK}
 
 
@@ -142,3 +148,26 @@ def test_sharded_bb_tiles_overlapped_two_ranks(cuda, orc):
 @pytest.mark.timeout(400)
 def test_sharded_bb_tiles_overlapped_rccl(cuda, orc):
     _check(_spawn(1, 'nccl', fmt='tiles', parts=3), orc, partitioned=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_sharded_stop_keeps_final_residual(cuda, orc):
+    """max_iter = 7 with early exits on: iterations 8..30 enqueued past the stop
+    change nothing -- every rank reports the stop at iteration 7 with the z of
+    iteration 7, and r stays the residual of iteration 7 on every rank (rank 0
+    keeps its r, the others write 0 before each all-reduce), not world x r."""
+    res = _spawn(2, 'gloo', max_iter=7, raw=True)
+    sh, b = _problem()
+    ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], 7, record_every=1)
+    z = np.concatenate([res[r][30] for r in range(2)])
+    assert np.max(np.abs(z - ref[7])) <= 1e-6 * max(1.0, np.max(np.abs(ref[7])))
+    for r in range(2):
+        s = res[r]['scal']
+        assert s[0] == 2 and s[1] == 7, s[:3]          # STOP_MAXITER at iteration 7
+    # the residual of z_7: A (x0 + N z_7) - b
+    from bsls_utils import particular_x0, block_sizes_to_N
+    sizes = sh['block_sizes']
+    r7 = sh['A'].dot(particular_x0(sizes) + block_sizes_to_N(sizes).dot(ref[7])) - b
+    for r in range(2):
+        assert np.max(np.abs(res[r]['r'] - r7)) <= 1e-9 * max(1.0, np.max(np.abs(r7)))

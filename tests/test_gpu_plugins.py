@@ -176,9 +176,9 @@ def test_dore_device_loop_vs_closures(cuda, eps, record_every, max_iter):
         # pick the last k >= 9 that is not the first iteration of a chunk
         # (chunks [1, 8), [8, 15), [15, 22), ... with record_every = 7) where it
         # drops below every earlier one, and put eps between the two
-        st = [s for _, s in run(False, -1.0, 1)]
+        st = [s for _, s in run(False, -1.0, 1)][:-1]      # (the final log repeats the last)
         nc = [float(np.sum((st[k] - st[k - 1]) ** 2)) for k in range(1, len(st))]
-        for k in range(len(nc), 8, -1):
+        for k in range(min(len(nc), max_iter - 1), 8, -1):
             lo = min(nc[:k - 1])
             if (k - 1) % 7 and nc[k - 1] < 0.99 * lo:
                 brk, eps = k, float(np.sqrt(nc[k - 1] * lo))

@@ -47,6 +47,13 @@ for s in $STEPS; do
     bench)
       timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1
       rc=$?; echo "bench rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    alltests)
+      timeout -k 10 900 python -u -m pytest $TESTS -m gpu -q --timeout 300 --timeout-method thread \
+          > $OUT/gpu_tests.log 2>&1
+      rc=$?; echo "alltests rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    legs)
+      timeout -k 10 600 python bench.py --legs "${LEGS:-lbfgs}" > $OUT/bench_legs.log 2>&1
+      rc=$?; echo "legs rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
     rehearse)
       timeout -k 10 400 python bench.py --rehearse-shard 8 --steps 200 --warmup 20 \
           > $OUT/rehearse8.log 2>&1
