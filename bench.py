@@ -133,18 +133,37 @@ def sps_csr(A):
     return sps.csr_matrix(A)
 
 
-def bench_stored_values(sh, b, steps, warmup):
-    """The C3 BB loop on the general-CSR images (values stored, 8 B per entry:
-    what a matrix that is not a scaled incidence runs) -- BBEngine(general=True)."""
+def bench_stored_values(sh, b, steps, warmup, codec=None):
+    """The C3 BB loop on the general images (values stored: what a matrix that
+    is not a scaled incidence runs) -- BBEngine(general=True).  The values
+    travel in the narrowest type that holds every one of them exactly (the C3
+    flows are integers < 1000: _Float16, 2 B per entry; BSLS_TILE_VAL16);
+    codec='f64' forces the 8-B doubles, what arbitrary real values need."""
     import torch
     from device import BBEngine
-    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 10 ** 12, 'opt_tol': 1e-30},
-                   early_exit=False, AT=sh['AT'], general=True)
+    old = os.environ.get('BSLS_VAL_CODEC')
+    if codec:
+        os.environ['BSLS_VAL_CODEC'] = codec
+    try:
+        eng = BBEngine(sh['A'], b, sh['block_sizes'],
+                       options={'max_iter': 10 ** 12, 'opt_tol': 1e-30},
+                       early_exit=False, AT=sh['AT'], general=True)
+    finally:
+        if old is None:
+            os.environ.pop('BSLS_VAL_CODEC', None)
+        else:
+            os.environ['BSLS_VAL_CODEC'] = old
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
     eng.prologue()
     el = time_run(eng.iterate, steps, warmup, None)
-    return {'value': steps / el, 'unit': 'BB iterations/s (C3, values stored)',
-            'ms_per_step': el / steps * 1e3, 'formats': {'K1': eng.fmt_A, 'K2': eng.fmt_AT}}
+    m, n, nz, p, nnz = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
+    ib = survey_iter_bytes(m, n, nz, nnz)
+    its = steps / el
+    return {'value': its, 'unit': 'BB iterations/s (C3, values stored)',
+            'ms_per_step': el / steps * 1e3, 'formats': {'K1': eng.fmt_A, 'K2': eng.fmt_AT},
+            'value_codec': getattr(eng.A_til, 'val_codec', 'f64') if eng.A_til else 'f64',
+            'iteration_roofline': {'survey_bytes_per_iter': ib, 'achieved_GB_s': ib * its / 1e9,
+                                   'frac': ib * its / HBM_PEAK}}
 
 
 def bench_proj(reps=30, batch=16):
@@ -423,10 +442,14 @@ def bench_md(sh, b, iters=30):
 
 
 def bench_iso(reps=3, batch=16):
-    """Standalone PAVA (bsls_isotonic_multi, variant 1 -- the isotonic_regression
-    path of main.py's proj, isotonic_regression.h:85-92) on the C3/C4 z layout:
-    950k entries in 50k blocks, inputs like K3's (z - t g); `batch` launches
-    back to back on distinct copies between two events.  Bytes 16 n + 4 (p+1)."""
+    """Standalone PAVA (variant 1 -- the isotonic_regression path of main.py's
+    proj, isotonic_regression.h:85-92) on the C3/C4 z layout: 950k entries in
+    50k blocks, inputs like K3's (z - t g); `batch` calls back to back on
+    distinct copies between two events.  The call is the planned one
+    (bsls_isotonic_packs over the layout's pack plan, made once and cached the
+    way c_extensions and BBEngine.proj cache it); `unplanned_avg_us` is
+    bsls_isotonic_multi, which plans on the device every call.  Bytes 16 n +
+    4 (p+1)."""
     import torch
     import _native
     from _native import ptr, stream_handle, check
@@ -444,25 +467,32 @@ def bench_iso(reps=3, batch=16):
     status = torch.zeros(4, dtype=torch.int32, device='cuda')
     ys = [y0.clone() for _ in range(batch)]
 
-    def iso(t):
+    from device import iso_plan
+    plan = iso_plan(zs, nz)
+
+    def iso_unplanned(t):
         check(L.bsls_isotonic_multi(1, ptr(t), ptr(st), zs.size, nz, None, 1, mb, ptr(ws),
                                     ws.numel(), ptr(status), stream_handle()), 'iso')
-    for t in ys[:2]:
-        iso(t)
-    out = []
-    for _ in range(reps):
-        for t in ys:
-            t.copy_(y0)
-        torch.cuda.synchronize()
-        torch.cuda._sleep(int(2e8))
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for t in ys:
-            iso(t)
-        e1.record()
-        torch.cuda.synchronize()
-        out.append(e0.elapsed_time(e1) / batch * 1e3)
-    us = sorted(out)[len(out) // 2]
+
+    def timed(fn):
+        for t in ys[:2]:
+            fn(t)
+        out = []
+        for _ in range(reps):
+            for t in ys:
+                t.copy_(y0)
+            torch.cuda.synchronize()
+            torch.cuda._sleep(int(2e8))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for t in ys:
+                fn(t)
+            e1.record()
+            torch.cuda.synchronize()
+            out.append(e0.elapsed_time(e1) / batch * 1e3)
+        return sorted(out)[len(out) // 2]
+    us_un = timed(iso_unplanned)
+    us = timed(plan.apply)
     from oracle import oracle as orc
     yc = y0.cpu().numpy().copy()
     t0 = time.perf_counter()
@@ -470,8 +500,10 @@ def bench_iso(reps=3, batch=16):
     cpu_s = time.perf_counter() - t0
     ok = bool(np.array_equal(yc.view(np.int64), ys[0].cpu().numpy().view(np.int64)))
     byt = 16 * nz + 4 * (zs.size + 1)
-    return {'n': nz, 'blocks': int(zs.size), 'avg_us': us, 'alg_bytes': byt,
-            'GB_s': byt / (us * 1e-6) / 1e9, 'frac_hbm_peak': byt / (us * 1e-6) / HBM_PEAK,
+    return {'n': nz, 'blocks': int(zs.size), 'packs': plan.npacks, 'avg_us': us,
+            'alg_bytes': byt, 'GB_s': byt / (us * 1e-6) / 1e9,
+            'frac_hbm_peak': byt / (us * 1e-6) / HBM_PEAK, 'unplanned_avg_us': us_un,
+            'rocprof_kernels': ['iso_packs_kernel'],
             'cpu_oracle_ms_1thread': cpu_s * 1e3, 'bit_exact_vs_oracle': ok}
 
 
@@ -804,6 +836,8 @@ def extras(args, legs, out, tfile):
         torch.cuda.empty_cache()
     if 'c3sv' in legs:
         out['c3_stored_values'] = bench_stored_values(sh3, b3, steps3, args.warmup)
+        torch.cuda.empty_cache()
+        out['c3_stored_values_f64'] = bench_stored_values(sh3, b3, steps3, args.warmup, 'f64')
         torch.cuda.empty_cache()
     if 'proj' in legs:
         out['proj_simplex'] = bench_proj()

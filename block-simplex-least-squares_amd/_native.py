@@ -53,6 +53,7 @@ TILE_THREADS = 1024       # BSLS_TILE_THREADS
 TILE_MAXSLOTS = 20        # BSLS_TILE_MAXSLOTS
 TILE_LDS_BYTES = 163840 - 512   # dynamic LDS a tile kernel may take (bb.hip PANEL_LDS_MAX)
 TILE_NT = 0x100                  # bsls_tiles.layout flag BSLS_TILE_NT
+TILE_VAL32, TILE_VAL16 = 0x200, 0x400   # BSLS_TILE_VAL32 / VAL16
 
 
 class Tiles(ctypes.Structure):
@@ -128,6 +129,8 @@ _SIGS = {
     'bsls_isotonic_workspace_size': (_sz, [_i64]),
     'bsls_isotonic_multi': (_int, [_int, _vp, _vp, _i64, _i64, _vp, _int, _i64, _vp, _sz, _vp,
                                    _vp]),
+    'bsls_isotonic_pack_plan': (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64]),
+    'bsls_isotonic_packs': (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _sz, _vp]),
     'bsls_x2z': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     'bsls_z2x': (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     'bsls_n_apply': (_int, [_vp, _vp, _vp, _i64, _i64, _int, _vp]),
@@ -303,6 +306,27 @@ def stream_handle(stream=None):
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def pack_plan(starts, n):
+    """Host pack plan of a block layout (bsls_isotonic_pack_plan, no GPU):
+    dict(start, mask, len, longs) NumPy arrays -- runs of whole consecutive
+    blocks with <= 64 elements, or one longer block (listed in longs)."""
+    import numpy as np
+    st = np.ascontiguousarray(starts, dtype=np.int64)
+    L = load()
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data)
+    nl = ctypes.c_int64(0)
+    np_ = L.bsls_isotonic_pack_plan(vp(st), st.shape[0], int(n), None, None, None, None,
+                                    ctypes.byref(nl), 0)
+    if np_ < 0:
+        raise ValueError('pack plan: invalid block starts')
+    out = dict(start=np.zeros(np_, np.int64), mask=np.zeros(np_, np.int64),
+               len=np.zeros(np_, np.int32), longs=np.zeros(max(nl.value, 1), np.int32))
+    L.bsls_isotonic_pack_plan(vp(st), st.shape[0], int(n), vp(out['start']), vp(out['mask']),
+                              vp(out['len']), vp(out['longs']), ctypes.byref(nl), np_)
+    out['longs'] = out['longs'][:nl.value]
+    return out
 
 
 def plan_tiles(indptr, nzt=2048, rmax=1024, ends=None):

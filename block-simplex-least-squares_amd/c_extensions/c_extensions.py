@@ -226,6 +226,14 @@ def _run_iso(variant, y, blocks_h, n, weight, update, name):
         return _cpu.isotonic(variant, y, blocks_h, n, weight, update)
     torch = _torch()
     L = _native.lib()
+    if variant == 1 and weight is None and update:
+        # main.py's call (fresh unit run lengths, expanded): the layout's pack
+        # plan, made once and cached by content (device.iso_plan), one launch
+        from device import iso_plan
+        st = _Staged(y)
+        iso_plan(np.asarray(blocks_h, dtype=np.int64), n).apply(st.dev)
+        st.commit()
+        return
     st = _Staged(y)
     dev = st.dev[:n]
     wdev, wback = (None, None) if variant == 2 else _weights(weight, n, int(blocks_h[0]))

@@ -982,9 +982,10 @@ static bool tiles_ok(const bsls_tiles &T, int64_t rows, int64_t cols, int64_t ha
     if (T.order != 0 && !(T.order == 1 && T.ngroups % 8 == 0)) return false;
     if (tile_lds_doubles(T, colv_lds) * 8 > (size_t)PANEL_LDS_MAX) return false;
     if (!T.group_col || !T.wave_off || !T.ent) return false;
-    const int64_t lay = T.layout & ~BSLS_TILE_NT;
+    const int64_t lay = T.layout & ~(int64_t)(BSLS_TILE_NT | BSLS_TILE_VAL32 | BSLS_TILE_VAL16);
     if (T.layout != 0 && !((lay == 1 || lay == 2) && T.base && T.H + T.halo < 65536))
         return false;
+    if ((T.layout & BSLS_TILE_VAL32) && (T.layout & BSLS_TILE_VAL16)) return false;
     if (lay == 2 && T.H + T.halo >= (1 << 18)) return false;   // >= 6 column bits
     return need_val ? T.val != nullptr : true;
 }

@@ -235,9 +235,140 @@ __global__ __launch_bounds__(LONG_T) void iso_long_kernel(double *__restrict__ y
     }
 }
 
+// ---- planned packs (bsls_isotonic_pack_plan / bsls_isotonic_packs) ----------
+// The packs are planned once per block layout (host, bsls_isotonic_pack_plan:
+// runs of whole consecutive blocks with <= 64 elements, or one longer block),
+// so a call is one launch whose waves read their pack's (start, mask, length)
+// in one round trip and then y -- as K3 does -- instead of the window plan's
+// three dependent rounds (window bounds, block starts, the starts of every
+// block of the window).  Wave w takes packs w and w + W (W = waves in the
+// grid); with MERGE their passes after the first are shared
+// (pava_v1_wave_pair), which pays once the grid runs several rounds of waves.
+template <int PPW, bool MERGE>
+__global__ __launch_bounds__(256) void iso_packs_kernel(double *__restrict__ y,
+                                                        const int64_t *__restrict__ pk_start,
+                                                        const int64_t *__restrict__ pk_mask,
+                                                        const int32_t *__restrict__ pk_len,
+                                                        int64_t npacks) {
+    const int l = lane_id();
+    const int wv = threadIdx.x / WAVE;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int64_t w0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);
+    __shared__ double pv_y[4][64];
+    __shared__ int pv_p[4][128];
+    __shared__ int pv_c[4][65];
+    int64_t s0[PPW];
+    int L[PPW];
+    uint64_t B[PPW];
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+        const int64_t pk = w0 + q * nw;
+        const int64_t pc = pk < npacks ? pk : npacks - 1;
+        s0[q] = pk_start[pc];
+        B[q] = (uint64_t)pk_mask[pc];
+        L[q] = pk < npacks ? pk_len[pc] : 0;
+    }
+    double v[PPW];
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) v[q] = (l < L[q] && L[q] <= WAVE) ? y[s0[q] + l] : 0.0;
+    if (MERGE && PPW == 2 && L[0] > 0 && L[0] <= WAVE && L[PPW - 1] > 0 && L[PPW - 1] <= WAVE) {
+        pava_v1_wave_pair(v[0], L[0], B[0], v[PPW - 1], L[PPW - 1], B[PPW - 1], pv_y[wv], pv_p[wv],
+                          pv_c[wv]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < PPW; ++q)
+            if (L[q] > 0 && L[q] <= WAVE) pava_v1_wave_c(v[q], L[q], B[q], pv_y[wv], pv_p[wv], pv_c[wv]);
+    }
+#pragma unroll
+    for (int q = 0; q < PPW; ++q)
+        if (l < L[q] && L[q] <= WAVE) y[s0[q] + l] = v[q];
+}
+
+// one workgroup per long block of the plan (> 64 elements), grid-strided
+__global__ __launch_bounds__(LONG_T) void iso_long_planned(double *__restrict__ y,
+                                                           const int64_t *__restrict__ pk_start,
+                                                           const int32_t *__restrict__ pk_len,
+                                                           const int32_t *__restrict__ longs,
+                                                           int64_t nlong, IsoWork w) {
+    __shared__ int64_t sh[LONG_T / 64 + 1];
+    __shared__ int flag;
+    for (int64_t idx = blockIdx.x; idx < nlong; idx += gridDim.x) {
+        const int64_t q = longs[idx];
+        const int64_t s = pk_start[q], k = pk_len[q];
+        pava_v1_long(y + s, k, w.Y0 + s, w.Y1 + s, w.W0 + s, w.W1 + s, w.CH + s, sh, &flag);
+    }
+}
+
 }  // namespace bsls
 
 using namespace bsls;
+
+extern "C" int64_t bsls_isotonic_pack_plan(const int64_t *starts, int64_t nblocks, int64_t n,
+                                           int64_t *pk_start, int64_t *pk_mask, int32_t *pk_len,
+                                           int32_t *long_packs, int64_t *nlong, int64_t cap) {
+    if (!starts || nblocks <= 0 || n <= 0 || starts[0] < 0 || starts[nblocks - 1] >= n)
+        return BSLS_E_ARG;
+    for (int64_t b = 1; b < nblocks; ++b)
+        if (starts[b] <= starts[b - 1]) return BSLS_E_ARG;
+    int64_t np = 0, nl = 0, b = 0;
+    auto len_of = [&](int64_t k) { return ((k + 1 < nblocks) ? starts[k + 1] : n) - starts[k]; };
+    while (b < nblocks) {
+        const int64_t k0 = len_of(b);
+        int64_t tot = 0, e = b;
+        uint64_t m = 0;
+        if (k0 > WAVE) {
+            tot = k0;
+            m = 1;
+            e = b + 1;
+            if (long_packs && np < cap) long_packs[nl] = (int32_t)np;
+            ++nl;
+        } else {
+            while (e < nblocks) {
+                const int64_t k = len_of(e);
+                if (k > WAVE || tot + k > WAVE) break;
+                m |= 1ull << tot;
+                tot += k;
+                ++e;
+            }
+        }
+        if (pk_start && np < cap) {
+            pk_start[np] = starts[b];
+            pk_mask[np] = (int64_t)m;
+            pk_len[np] = (int32_t)tot;
+        }
+        ++np;
+        b = e;
+    }
+    if (nlong) *nlong = nl;
+    return np;
+}
+
+extern "C" int bsls_isotonic_packs(double *d_y, const int64_t *d_pk_start, const int64_t *d_pk_mask,
+                                   const int32_t *d_pk_len, int64_t npacks,
+                                   const int32_t *d_long_packs, int64_t nlong, int64_t n,
+                                   void *d_work, size_t work_bytes, void *stream) {
+    if (!d_y || !d_pk_start || !d_pk_mask || !d_pk_len || npacks < 1 || n <= 0 || nlong < 0)
+        return BSLS_E_ARG;
+    if (nlong > 0 && (!d_long_packs || !d_work || work_bytes < bsls_isotonic_workspace_size(n)))
+        return BSLS_E_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    // two packs per wave from 64k packs (several rounds of resident waves), as K3
+    const char *e = getenv("BSLS_K3_MERGE");
+    const bool merge = e ? atoi(e) != 0 : npacks >= 65536;
+    if (merge)
+        iso_packs_kernel<2, true><<<grid_for(npacks, 8), 256, 0, st>>>(d_y, d_pk_start, d_pk_mask,
+                                                                       d_pk_len, npacks);
+    else
+        iso_packs_kernel<1, false><<<grid_for(npacks, 4), 256, 0, st>>>(d_y, d_pk_start, d_pk_mask,
+                                                                        d_pk_len, npacks);
+    BSLS_LAUNCH_CHECK();
+    if (nlong > 0) {
+        iso_long_planned<<<(int)(nlong < 1024 ? nlong : 1024), LONG_T, 0, st>>>(
+            d_y, d_pk_start, d_pk_len, d_long_packs, nlong, iso_layout(d_work, n));
+        BSLS_LAUNCH_CHECK();
+    }
+    return BSLS_OK;
+}
 
 extern "C" size_t bsls_isotonic_workspace_size(int64_t n) {
     return iso_layout(nullptr, n).bytes;

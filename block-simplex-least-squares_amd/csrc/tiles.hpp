@@ -171,7 +171,17 @@ struct TileEnt<true> {
     typedef tile_tri type;
 };
 
-template <int MODE, bool NT, bool PK3 = false, int P = BSLS_TILE_P, int D = BSLS_TILE_D>
+// the stored values (MODE 1) in the image's value type (VT 0: double, 1:
+// float, 2: _Float16 -- BSLS_TILE_VAL32 / VAL16, exact conversions of the
+// doubles): value e of the image as a double
+template <int VT>
+__device__ __forceinline__ double tile_val(const double *__restrict__ val, int64_t e) {
+    if constexpr (VT == 1) return (double)reinterpret_cast<const float *>(val)[e];
+    else if constexpr (VT == 2) return (double)reinterpret_cast<const _Float16 *>(val)[e];
+    else return val[e];
+}
+
+template <int MODE, bool NT, bool PK3 = false, int VT = 0, int P = BSLS_TILE_P, int D = BSLS_TILE_D>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
                                                 const double *rcol) {
@@ -198,7 +208,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
         else return u[j];
     };
     const int4 *Bq = reinterpret_cast<const int4 *>(T.base) + q0 * 16 + wv;
-    const double *V = (MODE == 1) ? T.val + 4 * l0 : nullptr;
+    const int64_t v0 = 4 * l0;   // first value of this lane (MODE 1)
     const double *xb = src + T.group_col[g];
     ent_t ring[P];
     int4 bring[P];
@@ -217,7 +227,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
         o[3] = xb[b.w + (ent(u, 3) & cmask)];
         if (MODE == 1) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = V[q * 4096 + j];
+            for (int j = 0; j < 4; ++j) w[j] = tile_val<VT>(T.val, v0 + q * 4096 + j);
         }
     };
 #pragma unroll
@@ -261,16 +271,32 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
     if (BSLS_TILE_KO == 2) rows[threadIdx.x] += ko;
 }
 
+// the dealt walk with its value type (MODE 1 only: the other modes store none)
+template <int MODE, bool NT, bool PK3>
+__device__ __forceinline__ void tile_walk_dealt_vt(const bsls_tiles &T, int64_t rb, int64_t g,
+                                                   const double *__restrict__ src, double *rows,
+                                                   const double *rcol) {
+    if constexpr (MODE == 1) {
+        if (T.layout & BSLS_TILE_VAL16) tile_walk_dealt<MODE, NT, PK3, 2>(T, rb, g, src, rows, rcol);
+        else if (T.layout & BSLS_TILE_VAL32)
+            tile_walk_dealt<MODE, NT, PK3, 1>(T, rb, g, src, rows, rcol);
+        else tile_walk_dealt<MODE, NT, PK3, 0>(T, rb, g, src, rows, rcol);
+    } else {
+        tile_walk_dealt<MODE, NT, PK3, 0>(T, rb, g, src, rows, rcol);
+    }
+}
+
 // the walk of either layout
 template <int MODE>
 __device__ __forceinline__ void tile_walk_any(const bsls_tiles &T, int64_t rb, int64_t g,
                                               const double *__restrict__ src, double *rows,
                                               const double *rcol) {
-    if (T.layout == 1) tile_walk_dealt<MODE, false>(T, rb, g, src, rows, rcol);
-    else if (T.layout == (1 | BSLS_TILE_NT)) tile_walk_dealt<MODE, true>(T, rb, g, src, rows, rcol);
-    else if (T.layout == 2) tile_walk_dealt<MODE, false, true>(T, rb, g, src, rows, rcol);
-    else if (T.layout == (2 | BSLS_TILE_NT))
-        tile_walk_dealt<MODE, true, true>(T, rb, g, src, rows, rcol);
+    const int64_t lay = T.layout & ~(int64_t)(BSLS_TILE_VAL32 | BSLS_TILE_VAL16);
+    if (lay == 1) tile_walk_dealt_vt<MODE, false, false>(T, rb, g, src, rows, rcol);
+    else if (lay == (1 | BSLS_TILE_NT)) tile_walk_dealt_vt<MODE, true, false>(T, rb, g, src, rows, rcol);
+    else if (lay == 2) tile_walk_dealt_vt<MODE, false, true>(T, rb, g, src, rows, rcol);
+    else if (lay == (2 | BSLS_TILE_NT))
+        tile_walk_dealt_vt<MODE, true, true>(T, rb, g, src, rows, rcol);
     else tile_walk<MODE>(T, rb, g, src, rows, rcol);
 }
 

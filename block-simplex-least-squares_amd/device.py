@@ -467,11 +467,30 @@ def _dealt_matvec(img, x, colv=None, group_sums=False):
 NT_BYTES = 256 << 20
 
 
+def value_codec(val, layout):
+    """(flag, array) for a dealt image's stored values: _Float16 or float when
+    every value (padding zeros included) converts to that type exactly -- the
+    kernels widen them back to the same doubles, so the products do not change
+    (BSLS_TILE_VAL16 / VAL32, include/bsls_hip.h) -- else the doubles.
+    BSLS_VAL_CODEC=f64|f32|f16 forces the choice down to the exact ones."""
+    if val is None or layout not in (1, 2):
+        return 0, val
+    want = os.environ.get('BSLS_VAL_CODEC', 'auto')
+    order = {'auto': ('f16', 'f32'), 'f16': ('f16', 'f32'), 'f32': ('f32',), 'f64': ()}[want]
+    for c in order:
+        dt = np.float16 if c == 'f16' else np.float32
+        with np.errstate(over='ignore', invalid='ignore'):
+            nv = val.astype(dt)
+        if np.array_equal(nv.astype(np.float64), val):
+            return (_native.TILE_VAL16 if c == 'f16' else _native.TILE_VAL32), nv
+    return 0, val
+
+
 def self_bytes(img):
     """Bytes of a tile image's entry stream (+ values)."""
     b = img['ent'].nbytes
     if img.get('val') is not None:
-        b += img['val'].nbytes
+        b += img.get('val_dev', img['val']).nbytes
     return b
 
 
@@ -500,8 +519,11 @@ class DeviceTiles:
         self.t = {'group_col': torch.from_numpy(gc).cuda(),
                   'wave_off': torch.from_numpy(img['wave_off']).cuda(),
                   'ent': torch.from_numpy(img['ent'].view(np.int32)).cuda()}
+        vflag, vdev = value_codec(img['val'], layout)
+        self.val_codec = {0: 'f64', _native.TILE_VAL32: 'f32', _native.TILE_VAL16: 'f16'}[vflag]
         if img['val'] is not None:
-            self.t['val'] = torch.from_numpy(img['val']).cuda()
+            img['val_dev'] = vdev
+            self.t['val'] = torch.from_numpy(vdev).cuda()
         if layout in (1, 2):
             self.t['base'] = torch.from_numpy(img['base']).cuda()
         S = _native.Tiles()
@@ -510,7 +532,7 @@ class DeviceTiles:
         nt = self_bytes(img) > NT_BYTES
         if os.environ.get('BSLS_TILE_NT'):          # A/B override of the policy
             nt = os.environ['BSLS_TILE_NT'] == '1'
-        S.layout = layout | (_native.TILE_NT if layout in (1, 2) and nt else 0)
+        S.layout = layout | (_native.TILE_NT if layout in (1, 2) and nt else 0) | vflag
         S.base = self.t['base'].data_ptr() if layout in (1, 2) else None
         S.rows, S.cols, S.H, S.halo = R, C, H, halo
         S.nrb, S.ngroups, S.order, S.nquads = img['nrb'], G, order, img['nquads']
@@ -604,6 +626,52 @@ def lsq_operator(A, AT=None, general=False):
         return None
 
 
+class IsoPlan:
+    """A block layout's pack plan on the device (bsls_isotonic_pack_plan /
+    bsls_isotonic_packs): isotonic_regression_multi_c's variant-1 call
+    (weight=None, update=1) in one launch, planned once per layout."""
+
+    def __init__(self, starts, n):
+        torch = _torch()
+        L = _native.lib()
+        P = _native.pack_plan(starts, n)
+        self.n = int(n)
+        self.npacks = int(P['start'].shape[0])
+        self.nlong = int(P['longs'].shape[0])
+        self.host = P
+        self.start = torch.from_numpy(P['start']).cuda()
+        self.mask = torch.from_numpy(P['mask']).cuda()
+        self.len = torch.from_numpy(P['len']).cuda()
+        self.longs = torch.from_numpy(P['longs'] if self.nlong else np.zeros(1, np.int32)).cuda()
+        self.work = (torch.zeros(L.bsls_isotonic_workspace_size(self.n), dtype=torch.uint8,
+                                 device='cuda') if self.nlong else None)
+
+    def apply(self, y, stream=None):
+        """PAVA v1 (expanded) of every block of y[:n], in place."""
+        L = _native.lib()
+        check(L.bsls_isotonic_packs(ptr(y), ptr(self.start), ptr(self.mask), ptr(self.len),
+                                    self.npacks, ptr(self.longs), self.nlong, self.n,
+                                    ptr(self.work), self.work.numel() if self.work is not None
+                                    else 0, stream_handle(stream)), 'bsls_isotonic_packs')
+        return y
+
+
+_iso_plans = {}
+
+
+def iso_plan(starts_h, n):
+    """IsoPlan of a host block-start array, cached by content (a few layouts)."""
+    import hashlib
+    st = np.ascontiguousarray(starts_h, dtype=np.int64)
+    key = (hashlib.blake2b(st.tobytes(), digest_size=16).digest(), st.shape[0], int(n))
+    plan = _iso_plans.get(key)
+    if plan is None:
+        if len(_iso_plans) >= 8:
+            _iso_plans.pop(next(iter(_iso_plans)))
+        plan = _iso_plans[key] = IsoPlan(st, n)
+    return plan
+
+
 class BlockLayout:
     """Block structure of x (sizes k_b) and of z (sizes k_b - 1), on device."""
 
@@ -630,34 +698,24 @@ class BlockLayout:
 
     def packs(self):
         """K3 packs (csrc/bb.hip): consecutive whole z-blocks with <= 64 z entries
-        for one wave, or a single longer block.  Host-planned once."""
+        for one wave, or a single longer block.  Host-planned once
+        (bsls_isotonic_pack_plan over the z-block starts; every z-block holds
+        >= 1 entry)."""
         if self._packs is None:
             torch = _torch()
-            kz = self.sizes - 1
-            z0, b0, mask, ln = [], [], [], []
-            b = 0
-            p = self.p
-            zst = self.zstarts_h
-            while b < p:
-                if kz[b] > 64:
-                    z0.append(zst[b]); b0.append(b); mask.append(1); ln.append(int(kz[b]))
-                    b += 1
-                    continue
-                tot, m_, e = 0, 0, b
-                while e < p and kz[e] <= 64 and tot + kz[e] <= 64:
-                    m_ |= 1 << tot
-                    tot += int(kz[e])
-                    e += 1
-                z0.append(zst[b]); b0.append(b); mask.append(m_); ln.append(tot)
-                b = e
-            mask = np.array(mask, dtype=np.uint64).view(np.int64)
+            P = _native.pack_plan(self.zstarts_h, self.nz)
+            b0 = np.searchsorted(self.zstarts_h, P['start']).astype(np.int64)
             self._packs = dict(
-                z0=torch.from_numpy(np.array(z0, dtype=np.int64)).cuda(),
-                b0=torch.from_numpy(np.array(b0, dtype=np.int64)).cuda(),
-                mask=torch.from_numpy(mask).cuda(),
-                len=torch.from_numpy(np.array(ln, dtype=np.int32)).cuda(),
-                n=len(z0))
+                z0=torch.from_numpy(P['start']).cuda(),
+                b0=torch.from_numpy(b0).cuda(),
+                mask=torch.from_numpy(P['mask']).cuda(),
+                len=torch.from_numpy(P['len']).cuda(),
+                n=int(P['start'].shape[0]))
         return self._packs
+
+    def iso_plan(self):
+        """The z-layout's IsoPlan (PAVA v1 over the z-blocks, BBEngine.proj)."""
+        return iso_plan(self.zstarts_h, self.nz)
 
 
 class BBEngine:
@@ -951,13 +1009,7 @@ class BBEngine:
         if self.layout.max_zblock < 1 or np.any(self.layout.sizes < 2):
             raise AssertionError   # the reference's strictly-increasing z-starts assert
         y = z.clone()
-        if not hasattr(self, '_iso_ws'):
-            self._iso_ws = torch.zeros(L.bsls_isotonic_workspace_size(self.nz),
-                                       dtype=torch.uint8, device='cuda')
-        check(L.bsls_isotonic_multi(1, ptr(y), ptr(self.layout.zstarts), self.layout.p, self.nz,
-                                    None, 1, self.layout.max_zblock, ptr(self._iso_ws),
-                                    self._iso_ws.numel(), None, stream_handle()),
-              'bsls_isotonic_multi')
+        self.layout.iso_plan().apply(y)
         return torch.clamp(y, 0.0, 1.0)
 
     def lsv_matvec(self, v):

@@ -61,6 +61,23 @@ int bsls_isotonic_multi(int variant, double *d_y, const int64_t *d_starts, int64
                         int64_t n, int32_t *d_weight, int expand, int64_t max_block,
                         void *d_work, size_t work_bytes, int32_t *d_status, void *stream);
 
+/* The same variant-1 call (weight=None, update=1 -- main.py's) on a pack plan
+ * made once per block layout: bsls_isotonic_pack_plan (host memory, no GPU)
+ * splits the blocks into packs of whole consecutive blocks with <= 64 elements
+ * (pk_start: first element, pk_mask: block-start bits relative to it, pk_len:
+ * elements) or one longer block (listed in long_packs); call it with
+ * pk_start == NULL for the count (returns npacks, *nlong set), then to fill
+ * arrays of that size.  bsls_isotonic_packs runs one launch over the device
+ * copies (+ one for the long blocks, with the isotonic workspace); the result
+ * is bit-identical to bsls_isotonic_multi.  Elements before the first block
+ * are untouched. */
+int64_t bsls_isotonic_pack_plan(const int64_t *starts, int64_t nblocks, int64_t n,
+                                int64_t *pk_start, int64_t *pk_mask, int32_t *pk_len,
+                                int32_t *long_packs, int64_t *nlong, int64_t cap);
+int bsls_isotonic_packs(double *d_y, const int64_t *d_pk_start, const int64_t *d_pk_mask,
+                        const int32_t *d_pk_len, int64_t npacks, const int32_t *d_long_packs,
+                        int64_t nlong, int64_t n, void *d_work, size_t work_bytes, void *stream);
+
 /* ---- z <-> x change of variables --------------------------------------------
  * Replaces x2z_c / z2x_c (c_extensions.pyx:195-248); d_starts[0] must be 0. */
 int bsls_x2z(const double *d_x, double *d_z, const int64_t *d_starts, int64_t nblocks,
@@ -201,6 +218,12 @@ typedef struct bsls_panels {
  * x + 8 j, nrb' = the row blocks of the launch). */
 #define BSLS_TILE_THREADS 1024
 #define BSLS_TILE_NT 0x100
+/* layouts 1 / 2 with stored values: val holds them as float (VAL32) or
+ * _Float16 (VAL16) instead of double -- only when every value converts to that
+ * type exactly (checked by the host builder), so the products are the same
+ * doubles; 4 or 2 bytes per value instead of 8. */
+#define BSLS_TILE_VAL32 0x200
+#define BSLS_TILE_VAL16 0x400
 #define BSLS_TILE_MAXSLOTS 20       /* LDS: (nslots + 1) * 1024 doubles (x2 with colv) */
 /* layout 1 ("dealt"; bsls_tiles_build_dealt): the entries of tile (rb, g) are
  * sorted by column and dealt to the workgroup in that order, so the 64 gathers
@@ -227,7 +250,8 @@ typedef struct bsls_tiles {
     const double *val;              /* 4 * nquads, or NULL (scaled incidence) */
     int64_t layout;                 /* 0: thread streams (CSR order per row), 1: dealt,
                                        2: dealt with 3-byte entries;
-                                       | BSLS_TILE_NT: dealt, entries by non-temporal loads */
+                                       | BSLS_TILE_NT: dealt, entries by non-temporal loads;
+                                       | BSLS_TILE_VAL32 / VAL16: dealt, narrow exact values */
     const int32_t *base;            /* layout 1: 4 * nquads / 64 instruction bases */
 } bsls_tiles;
 

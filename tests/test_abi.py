@@ -90,6 +90,8 @@ def test_panel_limits_match_header(native):
     assert '#define BSLS_PANEL_WAVES %d' % native.PANEL_WAVES in hdr
     assert '#define BSLS_TILE_THREADS %d' % native.TILE_THREADS in hdr
     assert '#define BSLS_TILE_NT 0x%x' % native.TILE_NT in hdr
+    assert '#define BSLS_TILE_VAL32 0x%x' % native.TILE_VAL32 in hdr
+    assert '#define BSLS_TILE_VAL16 0x%x' % native.TILE_VAL16 in hdr
 
 
 def test_tile_planner(native):
@@ -116,3 +118,37 @@ def test_invalid_arguments_rejected_without_launch(native):
     assert L.bsls_isotonic_multi(4, None, None, 1, 1, None, 1, 1, None, 0, None, None) == \
         native.BSLS_E_ARG
     assert L.bsls_bb_prologue(None, None) == native.BSLS_E_ARG
+
+
+def test_isotonic_pack_plan(native):
+    """bsls_isotonic_pack_plan (host only): packs tile [starts[0], n) in order,
+    each a run of whole blocks with <= 64 elements (mask bit i = a block starts
+    at element i of the pack) or one longer block (listed in longs), greedy as
+    K3's packs."""
+    import numpy as np
+    rs = np.random.RandomState(3)
+    sizes = rs.randint(1, 50, size=3000)
+    sizes[[5, 700, 2999]] = [65, 400, 64]
+    first = 7
+    starts = first + np.concatenate(([0], np.cumsum(sizes)[:-1]))
+    n = int(first + sizes.sum())
+    P = native.pack_plan(starts, n)
+    assert P['start'][0] == first
+    ends = P['start'] + P['len']
+    assert np.array_equal(P['start'][1:], ends[:-1]) and ends[-1] == n
+    blk = 0
+    for q in range(P['start'].shape[0]):
+        m, L = int(P['mask'][q]) & 0xFFFFFFFFFFFFFFFF, int(P['len'][q])
+        nb = bin(m).count('1')
+        assert m & 1
+        assert np.array_equal(starts[blk:blk + nb] - P['start'][q],
+                              [i for i in range(64) if (m >> i) & 1])
+        if L > 64:
+            assert nb == 1 and q in set(P['longs'].tolist())
+        else:
+            # greedy: the next block would not have fitted
+            nxt = sizes[blk + nb] if blk + nb < sizes.size else 0
+            assert blk + nb == sizes.size or L + nxt > 64 or nxt > 64
+        blk += nb
+    assert blk == sizes.size
+    assert sorted(P['longs'].tolist()) == [q for q in range(P['len'].size) if P['len'][q] > 64]
