@@ -76,7 +76,8 @@ class BBProblem(ctypes.Structure):
                 ('max_zblock', _i64), ('max_iter', _i64), ('opt_tol', _dbl),
                 ('early_exit', _i32), ('shard_role', _i32),
                 ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz),
-                ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp)]
+                ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp),
+                ('colv_n', _vp), ('colv_codec', _i64)]
 
 
 class DoreState(ctypes.Structure):

@@ -84,6 +84,24 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
 
 static BBWork bb_layout(const bsls_bb_problem &P) { return bb_layout(P.work, P.m, P.n, P.nz); }
 
+// column scale i (bsls_bb_problem.colv_codec: exact narrow copies read instead
+// of the doubles)
+__device__ __forceinline__ double colv_at(const bsls_bb_problem &P, int64_t i) {
+    if (P.colv_codec == 2) return (double)reinterpret_cast<const _Float16 *>(P.colv_n)[i];
+    if (P.colv_codec == 1) return (double)reinterpret_cast<const float *>(P.colv_n)[i];
+    return P.colv[i];
+}
+
+// the same with the codec known at compile time (the hot kernels are
+// instantiated per codec: a runtime switch among three loads inside K2's
+// batched epilogue kept its loads from being in flight together)
+template <int CV>
+__device__ __forceinline__ double colv_t(const bsls_bb_problem &P, int64_t i) {
+    if constexpr (CV == 2) return (double)reinterpret_cast<const _Float16 *>(P.colv_n)[i];
+    else if constexpr (CV == 1) return (double)reinterpret_cast<const float *>(P.colv_n)[i];
+    else return P.colv[i];
+}
+
 __device__ __forceinline__ void bb_stop_check(const bsls_bb_problem &P, int64_t iter, double fx) {
     double *s = P.scal;
     int reason = 0;
@@ -347,7 +365,7 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
 // sums r_i^2 over the rows [rb m / nrb, (rb + 1) m / nrb) of r (already the
 // all-reduced residual), and the last one records f and runs the stopping
 // test of iteration iter - 1 before it stores this iteration's sums.
-template <int MODE, bool ITER, bool FUSE = false>
+template <int MODE, bool ITER, bool FUSE = false, int CV = 0>
 __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
                                                const double *__restrict__ gp,
                                                double *__restrict__ gout, double *part,
@@ -366,7 +384,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     const int64_t nloc = (i0 + T.H + 1 <= P.n) ? T.H + 1 : P.n - i0;   // rows incl. the halo
     for (int i = threadIdx.x; i < HR; i += blockDim.x) {
         rows[i] = 0.0;
-        if (MODE == 2) rc[i] = (i < nloc) ? P.colv[i0 + i] : 0.0;
+        if (MODE == 2) rc[i] = (i < nloc) ? colv_t<CV>(P, i0 + i) : 0.0;
     }
     __syncthreads();
     tile_walk_any<(MODE == 3 ? 0 : MODE)>(T, rb, g, P.r, rows, rc);
@@ -399,7 +417,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
                 for (int64_t c = 0; c < G; ++c)
                     o += __hip_atomic_load(&P.wpart[(c * T.nrb + rb) * (T.H + 1) + i],
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                rows[i] = (MODE == 3) ? P.colv[i0 + i] * o : o;
+                rows[i] = (MODE == 3) ? colv_t<CV>(P, i0 + i) * o : o;
             }
             __syncthreads();
         }
@@ -424,8 +442,8 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
                 jq[q] = (i < iend) ? P.xz[i0 + i] : -1;
                 ca[q] = cb[q] = 1.0;
                 if (scale_epi && i < iend) {
-                    ca[q] = P.colv[i0 + i];
-                    cb[q] = (i + 1 < nloc) ? P.colv[i0 + i + 1] : 0.0;
+                    ca[q] = colv_t<CV>(P, i0 + i);
+                    cb[q] = (i + 1 < nloc) ? colv_t<CV>(P, i0 + i + 1) : 0.0;
                 }
             }
 #pragma unroll
@@ -535,7 +553,7 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
         for (int q = 0; q < 4; ++q) {
             const int64_t i = i0 + 64 * q + lane;        // halo row included
             const bool ok = live && 64 * q + lane <= M.prow && i < P.n;
-            const double v = P.colv[ok ? i : 0];
+            const double v = colv_at(P, ok ? i : 0);
             sc[q] = ok ? v : 0.0;
         }
     }
@@ -611,7 +629,7 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
 // x entry i of N z; for a scaled incidence K1 gathers colv[i] * x_i instead,
 // the product SciPy's csr_matvec forms for every entry of column i.
 __device__ __forceinline__ void x_put(const bsls_bb_problem &P, int64_t i, double v) {
-    P.x[i] = P.colv ? P.colv[i] * v : v;
+    P.x[i] = P.colv ? colv_at(P, i) * v : v;
 }
 
 __device__ __forceinline__ int64_t zend(const bsls_bb_problem &P, int64_t b) {
@@ -669,7 +687,7 @@ __device__ __forceinline__ void wt_store_f64(const __amdgpu_buffer_rsrc_t &rs, i
 // share the wave after their first passes (pava_v1_wave_pair).
 // (at most 80 SGPRs: 256-thread blocks are admitted 8 per CU only up to 80,
 // MI355X_MICROARCH.md "Residency"; the merged form otherwise takes 83 and 7)
-template <int K3_PPW, bool MERGE>
+template <int K3_PPW, bool MERGE, int CV = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(BSLS_K3_SGPRS)))
 void bb_k3(bsls_bb_problem P, int64_t iter,
                                              const double *__restrict__ zc,
@@ -709,8 +727,8 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
         if (P.colv) {
             // the column scales of this lane's x entries, loaded before the
             // PAVA so their round trip overlaps it (x_put's products)
-            cv[q] = act ? P.colv[xi] : 1.0;
-            cv2[q] = (act && bend) ? P.colv[xi + 1] : 1.0;
+            cv[q] = act ? colv_t<CV>(P, xi) : 1.0;
+            cv2[q] = (act && bend) ? colv_t<CV>(P, xi + 1) : 1.0;
         }
         zv[q] = act ? zc[z0[q] + l] : 0.0;
         gv[q] = act ? g[z0[q] + l] : 0.0;
@@ -916,13 +934,22 @@ static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *g
                               st>>>(P, w.dz, gp, gout, w.p2, w.tk2, iter);
 }
 
+template <int MODE, bool ITER, bool FUSE, int CV>
+static void launch_k2t_cv(const bsls_bb_problem &P, const double *gp, double *gout,
+                          const BBWork &w, hipStream_t st, int64_t iter) {
+    allow_lds(bb_k2t<MODE, ITER, FUSE, CV>);
+    bb_k2t<MODE, ITER, FUSE, CV><<<(int)(P.ATt.nrb * P.ATt.ngroups), BSLS_TILE_THREADS,
+                                   tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(
+        P, w.dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter);
+}
+
 template <int MODE, bool ITER, bool FUSE>
 static void launch_k2t_mode(const bsls_bb_problem &P, const double *gp, double *gout,
                             const BBWork &w, hipStream_t st, int64_t iter) {
-    allow_lds(bb_k2t<MODE, ITER, FUSE>);
-    bb_k2t<MODE, ITER, FUSE><<<(int)(P.ATt.nrb * P.ATt.ngroups), BSLS_TILE_THREADS,
-                               tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(
-        P, w.dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter);
+    if (MODE != 1 && P.colv_codec == 2) launch_k2t_cv<MODE, ITER, FUSE, 2>(P, gp, gout, w, st, iter);
+    else if (MODE != 1 && P.colv_codec == 1)
+        launch_k2t_cv<MODE, ITER, FUSE, 1>(P, gp, gout, w, st, iter);
+    else launch_k2t_cv<MODE, ITER, FUSE, 0>(P, gp, gout, w, st, iter);
 }
 
 template <bool ITER, bool FUSE = false>
@@ -951,12 +978,20 @@ static bool k3_merge(const bsls_bb_problem &P) {
     return e ? atoi(e) != 0 : P.npacks >= 65536;
 }
 
+template <int CV>
+static void launch_k3_cv(const bsls_bb_problem &P, int64_t iter, const double *zc,
+                         const double *g, double *zn, const BBWork &w, hipStream_t st) {
+    if (k3_merge(P))
+        bb_k3<2, true, CV><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+    else
+        bb_k3<1, false, CV><<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+}
+
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
                       double *zn, const BBWork &w, hipStream_t st) {
-    if (k3_merge(P))
-        bb_k3<2, true><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
-    else
-        bb_k3<1, false><<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+    if (P.colv && P.colv_codec == 2) launch_k3_cv<2>(P, iter, zc, g, zn, w, st);
+    else if (P.colv && P.colv_codec == 1) launch_k3_cv<1>(P, iter, zc, g, zn, w, st);
+    else launch_k3_cv<0>(P, iter, zc, g, zn, w, st);
     if (P.long_packs && P.nlong > 0)
         bb_k3_long<<<(int)P.nlong, LONG_T, 0, st>>>(P, iter, zc, g, zn, w.dz);
 }
@@ -993,6 +1028,8 @@ static bool tiles_ok(const bsls_tiles &T, int64_t rows, int64_t cols, int64_t ha
 static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
     if (p->shard_role < 0 || p->shard_role > 2) return BSLS_E_ARG;
+    if (p->colv_codec < 0 || p->colv_codec > 2 || (p->colv_codec && (!p->colv_n || !p->colv)))
+        return BSLS_E_ARG;
     const bool general = p->colv == nullptr;
     if (p->At.ent) {
         if (!tiles_ok(p->At, p->m, p->n, 0, general, false)) return BSLS_E_ARG;

@@ -151,6 +151,9 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
     const bool act = t < s.nh;
     const double yp = dpp_shr1_d(s.Y);
     const bool cs = act & ((s.BS != 0) | !(s.Y <= yp));   // lane 0 is always a block start
+    // every run starts a chain (the converged pack's check pass, usually):
+    // no chain has two runs, so none pools -- leave before any LDS traffic
+    if (!ballot_b(act & !cs)) return false;
     const uint64_t CS = ballot_b(cs);
     // chain c of this lane (lanes >= nh: the last chain, unused); the
     // table holds every chain's first run, then nh

@@ -820,6 +820,14 @@ class BBEngine:
             ti = self.AT_til.img
             self.wpart = torch.zeros(ti['ngroups'] * ti['nrb'] * (ti['H'] + 1), **dev)
         self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
+        # the scales as the kernels read them every iteration: the narrowest
+        # exact type (flows are integers: _Float16; value_codec)
+        self.colv_codec, self.colv_n = 0, None
+        if self.scaled:
+            flag, cn = value_codec(np.asarray(colv, dtype=np.float64), 2)
+            if flag:
+                self.colv_codec = 2 if flag == _native.TILE_VAL16 else 1
+                self.colv_n = torch.from_numpy(cn).cuda()
         P = BBProblem()
         P.m, P.n, P.nz, P.nblocks = self.m, lay.n, lay.nz, lay.p
         if self.A_pan is not None:
@@ -833,6 +841,8 @@ class BBEngine:
         P.wpart = self.wpart.data_ptr() if self.wpart is not None else None
         P.work_bytes = self.work.numel()
         P.colv = self.colv.data_ptr() if self.scaled else None
+        P.colv_n = self.colv_n.data_ptr() if self.colv_n is not None else None
+        P.colv_codec = self.colv_codec
         P.rpart = self.rpart.data_ptr()
         P.target = self.target.data_ptr()
         P.xstarts, P.zstarts, P.xz = (lay.xstarts.data_ptr(), lay.zstarts.data_ptr(),

@@ -339,6 +339,12 @@ typedef struct bsls_bb_problem {
     int64_t nlong;
     const int64_t *long_off;
     void *long_scratch;
+    /* colv in a narrower type when every scale converts to it exactly (the
+     * host checks; the kernels widen back to the same doubles): colv_codec 1 =
+     * float, 2 = _Float16 at colv_n; 0 = read colv itself.  K2's epilogue and K3
+     * read the scales of every route per iteration (C5: 80 MB as doubles). */
+    const void *colv_n;
+    int64_t colv_codec;
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);

@@ -285,7 +285,7 @@ def test_stored_value_codecs_vs_oracle(cuda, orc, codec):
     sh = make_shard(60_000, 3_000, 6_000, per_col=16, seed=19)
     A = sh['A'].copy()
     if codec == 'f32':
-        A.data = A.data * (1.0 + 2.0 ** -20)          # exact in float, not in _Float16
+        A.data = A.data * (1.0 + 2.0 ** -12)          # <= 22 bits: exact in float, not in _Float16
     elif codec == 'f64':
         A.data = A.data * (1.0 + np.random.RandomState(3).rand(A.nnz) * 1e-3)
     A = sps.csr_matrix(A)

@@ -58,6 +58,23 @@ for s in $STEPS; do
       timeout -k 10 400 python bench.py --rehearse-shard 8 --steps 200 --warmup 20 \
           > $OUT/rehearse8.log 2>&1
       rc=$?; echo "rehearse rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    pmc)
+      # one rocprofv3 pass per counter group (FETCH_SIZE and WRITE_SIZE cannot
+      # share a pass) over tools/kprof.py; traffic -> gpurun_out/traffic.json
+      for cfg in ${PMC_CFG:-C3 C5}; do
+        extra=""
+        [ "$cfg" = C3 ] && extra="--proj 10 --iso 10"
+        i=0
+        for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+          i=$((i+1))
+          rm -rf $OUT/pmc_${cfg}_$i
+          timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_${cfg}_$i -o pmc \
+              -- python3 tools/kprof.py --config $cfg --iters 10 $extra > $OUT/pmc_${cfg}_$i.log 2>&1
+          rc=$?; echo "pmc $cfg $i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
+        done
+        python3 tools/traffic.py $cfg $OUT/traffic.json $OUT/pmc_${cfg}_1 $OUT/pmc_${cfg}_2 \
+            > /dev/null 2> $OUT/traffic_$cfg.err
+      done ;;
     prof)
       for k in $PROF; do
         case "$k" in

@@ -21,6 +21,8 @@ def main():
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--proj', type=int, default=20)
     ap.add_argument('--config', default='C3')
+    ap.add_argument('--iso', type=int, default=0,
+                    help='planned standalone PAVA calls on the C3/C4 z layout')
     args = ap.parse_args()
     from synthetic import make_shard, add_noise, proj_input, CONFIGS, SEED
     from device import BBEngine
@@ -55,6 +57,20 @@ def main():
             y.copy_(y0)
             check(L.bsls_proj_multi_simplex(ptr(y), ptr(st), p, n, mb, ptr(ws), ws.numel(),
                                             stream_handle()), 'proj')
+        torch.cuda.synchronize()
+    if args.iso:
+        from device import iso_plan
+        c3 = CONFIGS['C3']
+        rs = np.random.RandomState(SEED)
+        sizes = rs.multinomial(c3['n'] - c3['p'], np.ones(c3['p']) / c3['p']) + 1
+        zs = np.concatenate(([0], np.cumsum(sizes - 1)[:-1])).astype(np.int64)
+        nz = int((sizes - 1).sum())
+        y0 = torch.from_numpy(rs.rand(nz) - 0.3 * rs.randn(nz)).cuda()
+        y = y0.clone()
+        plan = iso_plan(zs, nz)
+        for _ in range(args.iso):
+            y.copy_(y0)
+            plan.apply(y)
         torch.cuda.synchronize()
     print('kprof done', eng.scalars()[:5])
 
