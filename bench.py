@@ -330,6 +330,59 @@ def bench_lbfgs(sh, b, rounds=16, reps=10, corrections=50):
             'iterations_per_s': its / (ms * 1e-3), 'backtracks': bts, 'finite': ok}
 
 
+def bench_gd_lbfgs(sh, b, iters=20, reps=20, m=50):
+    """LBFGS.solve (python/LBFGS.py:56-123) through GradientDescent('LBFGS') on
+    the C3 z-space problem over the BBEngine closures: wall time per
+    iteration (weak Wolfe line search decisions on the host, as the
+    reference), and the device direction alone (csrc/lbfgs.hip: multi-dot
+    of {g, y_new, s_new} against the 2m + 2 history columns, one-wave
+    recursion, combine over 2m + 1 vectors, the push) on a full ring of m
+    pairs, timed with HIP events on the stream it runs on.  Algorithmic
+    bytes per direction + push: (3 + 2m + 2) n reads (multi-dot, each vector
+    once) + (2m + 1) n reads + n writes (combine) + 3 n copies in (6 n) + the
+    pair's copy into its slot (4 n), 8 B each."""
+    import torch
+    import LBFGS
+    from device import BBEngine
+    from gradient_descent import GradientDescent
+    opts = {'max_iter': iters, 'verbose': 0, 'opt_tol': 1e-30}
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options=opts, AT=sh['AT'])
+    gd = GradientDescent(z0=np.zeros(eng.nz), method='LBFGS', options=dict(opts), engine=eng)
+    gd.run()                                    # warm (allocations, first launches)
+    torch.cuda.synchronize()
+    gd = GradientDescent(z0=np.zeros(eng.nz), method='LBFGS', options=dict(opts), engine=eng)
+    t0 = time.perf_counter()
+    iters_, _, _ = gd.run()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    n = eng.nz
+    rs = np.random.RandomState(1)
+    H = LBFGS._DeviceHistory(torch.zeros(n, dtype=torch.float64, device='cuda'), m)
+    vec = lambda: torch.from_numpy(rs.randn(n)).cuda()
+    g, yn, sn = vec(), vec(), vec()
+    for _ in range(m):                          # a full ring
+        H.direction(g, yn, sn)
+        H.push(1.0)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        d = H.direction(g, yn, sn)
+        H.push(1.0)
+    ev[1].record()
+    torch.cuda.synchronize()
+    us = ev[0].elapsed_time(ev[1]) * 1e3 / reps
+    byts = 8 * n * ((3 + 2 * m + 2) + (2 * m + 2) + 6 + 4)
+    del H, d
+    torch.cuda.empty_cache()
+    return {'n': n, 'corrections': m, 'iterations': int(iters_[-1]),
+            'ms_per_iteration': wall * 1e3 / max(int(iters_[-1]), 1),
+            'direction': {'us': us, 'alg_bytes': byts, 'achieved_GB_s': byts / us * 1e-3,
+                          'peak_GB_s': HBM_PEAK / 1e9, 'frac': byts / us * 1e-3 / (HBM_PEAK / 1e9),
+                          'note': 'direction + push per iteration (multi-dot, coef, combine, '
+                                  'copies), HIP events, full ring of m pairs'}}
+
+
 def bench_c1():
     """BASELINE configs[0]: main.py --method BB --device cpu on the
     tests/fast/test_main.py problem (bsls_utils.generate_data() defaults, the
@@ -683,7 +736,8 @@ def host_info(threads):
             'OPENBLAS_NUM_THREADS': os.environ.get('OPENBLAS_NUM_THREADS')}
 
 
-LEGS = ('main', 'c3', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'c1', 'cpu')
+LEGS = ('main', 'c3', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'gdlbfgs', 'c1',
+        'cpu')
 
 
 def traffic_file():
@@ -813,7 +867,7 @@ def extras(args, legs, out, tfile):
     import torch
     steps3 = max(args.steps, 50)
     sh3 = b3 = None
-    if legs & {'c3', 'c3sv', 'xspace', 'md', 'dore', 'lbfgs', 'cpu'}:
+    if legs & {'c3', 'c3sv', 'xspace', 'md', 'dore', 'lbfgs', 'gdlbfgs', 'cpu'}:
         sh3, b3 = build_problem('C3', 1, 0, None)
     if 'c3' in legs:
         eng3, run3 = build_engine(sh3, b3, 1, None, 1)
@@ -852,6 +906,9 @@ def extras(args, legs, out, tfile):
         out['dore'] = bench_dore(sh3, b3)
     if 'lbfgs' in legs:
         out['lbfgs'] = bench_lbfgs(sh3, b3)
+    if 'gdlbfgs' in legs:
+        out['lbfgs_solve'] = bench_gd_lbfgs(sh3, b3)
+        torch.cuda.empty_cache()
     if 'c1' in legs:
         out['c1_cpu_path'] = bench_c1()
     log('extras done')

@@ -1,11 +1,78 @@
 """Projected limited-memory BFGS with a bisection weak-Wolfe line search
 (reference: python/LBFGS.py:9-123).  Off the north-star hot path; kept so that
 GradientDescent(method='LBFGS') dispatches.  Works on NumPy arrays or on
-HIP-resident torch tensors through the device closures."""
+HIP-resident torch tensors through the device closures.
+
+On the device the search direction (LBFGS.py:59-71) and the history rotation
+(:75-77) run on csrc/lbfgs.hip (_DeviceHistory): the m pairs live in a ring of
+device slots with their Gram matrices, and one direction is one multi-dot pass,
+one one-wave recursion on the dots and one combine pass -- instead of 2m
+dependent dot products (each a device -> host read) and 2m AXPYs.  The line
+search's decisions (f(pt) >= ..., LBFGS.py:26-53) stay on the host as in the
+reference."""
+import ctypes
 import math
 import time
 
-from _arr import copy, dot, norm
+from _arr import copy, dot, is_torch, norm
+
+MAX_DEVICE_CORRECTIONS = 127     # bsls_lbfgs_coef
+
+
+class _DeviceHistory:
+    """The reference's lists Y, S, rho (m zero pairs initially, LBFGS.py:51)
+    as a ring of device slots: slot (head + k) % m = pair k (0 the oldest)."""
+
+    def __init__(self, x, m):
+        import torch
+        import _native
+        self.L, self.torch, self.native = _native.lib(), torch, _native
+        self.m, self.n, self.head = m, x.numel(), 0
+        dev, f64 = x.device, torch.float64
+        self.S = torch.zeros((m, self.n), dtype=f64, device=dev)
+        self.Y = torch.zeros((m, self.n), dtype=f64, device=dev)
+        self.g = torch.empty(self.n, dtype=f64, device=dev)
+        self.yn = torch.empty_like(self.g)
+        self.sn = torch.empty_like(self.g)
+        self.state = torch.zeros(self.L.bsls_lbfgs_state_size(m) // 8, dtype=f64, device=dev)
+        self.K = 2 * m + 2
+        self.dots = torch.empty(3 * self.K, dtype=f64, device=dev)
+        wb = self.L.bsls_multi_dot_workspace_size(3, self.K)
+        self.work = torch.empty((wb + 7) // 8, dtype=f64, device=dev)
+        self.wbytes = self.work.numel() * 8
+        S, Y = [r.data_ptr() for r in self.S], [r.data_ptr() for r in self.Y]
+        ptrs = lambda v: torch.tensor(v, dtype=torch.int64).to(dev)
+        self.rows = ptrs([self.g.data_ptr(), self.yn.data_ptr(), self.sn.data_ptr()])
+        self.cols = ptrs(S + Y + [self.yn.data_ptr(), self.sn.data_ptr()])
+        self.vecs = ptrs([self.g.data_ptr()] + S + Y)
+        coef_off = m + 2 * m * m                       # bsls_lbfgs_state_size's layout
+        self.coef = self.state[coef_off:coef_off + 2 * m + 1]
+
+    def direction(self, g_new, y_new, s_new):
+        """-r of LBFGS.py:59-71 (no host read)."""
+        P, ck, L = self.native.ptr, self.native.check, self.L
+        st = self.native.stream_handle()
+        self.g.copy_(g_new.reshape(-1))
+        self.yn.copy_(y_new.reshape(-1))
+        self.sn.copy_(s_new.reshape(-1))
+        ck(L.bsls_multi_dot(P(self.rows), 3, P(self.cols), self.K, self.n, P(self.dots),
+                            P(self.work), self.wbytes, st), 'bsls_multi_dot')
+        ck(L.bsls_lbfgs_coef(self.m, self.head, P(self.state), P(self.dots), st), 'bsls_lbfgs_coef')
+        d = self.torch.empty_like(self.g)
+        ck(L.bsls_multi_axpy(P(self.vecs), 2 * self.m + 1, P(self.coef), self.n, P(d), st),
+           'bsls_multi_axpy')
+        return d.reshape(g_new.shape)
+
+    def push(self, rho_new):
+        """Y = Y[1:] + [y_new] etc. (LBFGS.py:75-77): the oldest slot takes the
+        pair of the last direction() call, its Gram rows from the same dots."""
+        P, L = self.native.ptr, self.L
+        st = self.native.stream_handle()
+        h = self.head
+        self.native.check(L.bsls_lbfgs_push(self.m, h, ctypes.c_double(rho_new), P(self.state),
+                                            P(self.dots), P(self.yn), P(self.sn), P(self.Y[h]),
+                                            P(self.S[h]), self.n, st), 'bsls_lbfgs_push')
+        self.head = (h + 1) % self.m
 
 
 def weak_wolfe_ls(x, d, f, nabla_f, proj=lambda v: v, c1=1e-3, c2=0.9):
@@ -48,16 +115,24 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
     i, stop = 0, False
     x = x0
     zero = x * 0
-    Y, S, rho = [zero] * m, [zero] * m, [0.0] * m
+    hist = None
+    if is_torch(x) and x.is_cuda and 1 <= m <= MAX_DEVICE_CORRECTIONS:
+        hist = _DeviceHistory(x, m)
+    else:
+        Y, S, rho = [zero] * m, [zero] * m, [0.0] * m
     g_new = nabla_f(x)
     y_new, s_new = g_new, zero + 1
     rho_new = 1 / dot(y_new, s_new)
     while not stop:
         i += 1
-        d = direction(g_new, y_new, s_new, rho, Y, S)
-        Y = Y[1:] + [y_new]
-        S = S[1:] + [s_new]
-        rho = rho[1:] + [rho_new]
+        if hist is not None:
+            d = hist.direction(g_new, y_new, s_new)
+            hist.push(rho_new)
+        else:
+            d = direction(g_new, y_new, s_new, rho, Y, S)
+            Y = Y[1:] + [y_new]
+            S = S[1:] + [s_new]
+            rho = rho[1:] + [rho_new]
         t = weak_wolfe_ls(x, d, f, nabla_f, proj=proj or (lambda v: v))
         s_new = t * d
         x_next = x + s_new

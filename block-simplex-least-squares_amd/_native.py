@@ -144,6 +144,12 @@ _SIGS = {
     'bsls_xbb_init': (_int, [ctypes.POINTER(XBBProblem), _vp]),
     'bsls_xbb_rounds': (_int, [ctypes.POINTER(XBBProblem), _i64, _vp]),
     'bsls_md_step': (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _dbl, _vp]),
+    'bsls_multi_dot_workspace_size': (_sz, [_i64, _i64]),
+    'bsls_multi_dot': (_int, [_vp, _int, _vp, _int, _i64, _vp, _vp, _sz, _vp]),
+    'bsls_multi_axpy': (_int, [_vp, _int, _vp, _i64, _vp, _vp]),
+    'bsls_lbfgs_state_size': (_sz, [_i64]),
+    'bsls_lbfgs_coef': (_int, [_i64, _i64, _vp, _vp, _vp]),
+    'bsls_lbfgs_push': (_int, [_i64, _i64, _dbl, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     'bsls_quad_obj': (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     'bsls_line_search': (_int, [_vp, _dbl, _vp, _vp, _dbl, _vp, _vp, _vp, _i64, _vp, _vp]),
     'bsls_csr_plan_tiles': (_i64, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64]),

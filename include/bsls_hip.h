@@ -575,6 +575,37 @@ int bsls_md_update_packs(double *d_x, const double *d_g, const int64_t *d_pk_x0,
 int bsls_md_step(const double *d_x, const double *d_g, double *d_y, const int64_t *d_starts,
                  int64_t nblocks, int64_t n, double t, void *stream);
 
+/* ---- LBFGS.solve's direction (python/LBFGS.py:59-71), vector-free ----------
+ * The two-loop recursion over the m stored pairs runs on dot products: one
+ * pass computing every dot an iteration needs, the m-step loops on scalars in
+ * one wave, one combine pass.  Replaces the 2m dependent dots and 2m AXPYs of
+ * `direction` (python/LBFGS.py:59-71) and the list rotation of :75-77.
+ *
+ * bsls_multi_dot: d_out[j * K + k] = d_rows[j] . d_cols[k] (1 <= J <= 4;
+ * d_rows / d_cols are DEVICE arrays of device pointers, every vector n
+ * doubles).  Fixed summation order (deterministic). */
+size_t bsls_multi_dot_workspace_size(int64_t J, int64_t K);
+int bsls_multi_dot(const double *const *d_rows, int J, const double *const *d_cols, int K,
+                   int64_t n, double *d_out, void *d_work, size_t work_bytes, void *stream);
+/* d_out[i] = sum_k d_coef[k] * d_vecs[k][i], k ascending (1 <= K <= 256). */
+int bsls_multi_axpy(const double *const *d_vecs, int K, const double *d_coef, int64_t n,
+                    double *d_out, void *stream);
+/* History state of m <= 127 pairs (ring slot (head + k) % m = pair k, 0 the
+ * oldest): rho[m], SY[m][m] (s_a . y_b), YY[m][m], coef[2m + 1], scratch;
+ * zero-initialised = the reference's m zero pairs (LBFGS.py:51). */
+size_t bsls_lbfgs_state_size(int64_t m);
+/* d_dots: bsls_multi_dot of rows {g_new, y_new, s_new} against columns
+ * {S slot 0..m-1, Y slot 0..m-1, y_new, s_new} (K = 2m + 2).  Writes
+ * coef = [a, b_0..b_{m-1}, c_0..c_{m-1}] with d = a g_new + sum b_j S_j +
+ * sum c_j Y_j the reference's `direction` (H from y_new, s_new). */
+int bsls_lbfgs_coef(int64_t m, int64_t head, double *d_state, const double *d_dots,
+                    void *stream);
+/* Pushes (y_new, s_new, rho_new) into ring slot `slot` (the oldest, = head):
+ * copies the vectors, fills the slot's Gram rows from the same d_dots. */
+int bsls_lbfgs_push(int64_t m, int64_t slot, double rho_new, double *d_state,
+                    const double *d_dots, const double *d_y_new, const double *d_s_new,
+                    double *d_y_slot, double *d_s_slot, int64_t n, void *stream);
+
 /* Library / device info (for the loader's self-check). */
 const char *bsls_version(void);
 int bsls_device_arch(char *buf, int buflen);

@@ -13,6 +13,7 @@ Contents
     restatement;
   * numpy restatements of the solver loops the hot path runs inside:
       bb_solve            python/BB.py:7-45
+      lbfgs_solve         python/LBFGS.py:56-123 (+ weak_wolfe_ls :9-53)
       stopping            python/solvers.py:40-63
       dore_solve          python/DORE.py:6-90
       md_least_squares    python/mirror_descent.py:7-53
@@ -30,6 +31,7 @@ tests/golden/make_golden.py, and against _ref when it is present).
 """
 import ctypes
 import logging
+import math
 import os
 import subprocess
 import time
@@ -370,6 +372,95 @@ def bb_trace(A, b, block_sizes, iters, record_every=1, options=None):
     opts = options or {'max_iter': iters, 'verbose': 0, 'opt_tol': 1e-30}
     bb_solve(P['z0'], P['f'], P['nabla_f'], stopping, record_every=record_every,
              proj=P['proj'], log=log, options=opts)
+    return rec
+
+
+def weak_wolfe_ls(x, d, f, nabla_f, proj=lambda v: v, c1=1e-3, c2=0.9):
+    """LBFGS.py:9-53: bisection on t until the Armijo and curvature
+    conditions hold (f(proj x) and d.nabla_f(proj x) fixed, as :18-19)."""
+    lo, hi, t = 0.0, float('inf'), 1
+    px = proj(x)
+    gx = nabla_f(px)
+    while True:
+        pt = proj(x + t * d)
+        stop = False
+        if f(pt) >= f(px) + c1 * t * d.dot(gx):
+            hi = t
+            t = 0.5 * (lo + hi)
+        elif d.dot(nabla_f(pt)) < c2 * d.dot(gx):
+            lo = t
+            t = 2 * lo if hi == float('inf') else 0.5 * (lo + hi)
+        else:
+            stop = True
+        if stop or abs(lo - hi) <= 1e-14 or la.norm(t * d) <= 1e-8:
+            return t
+
+
+def lbfgs_solve(x0, f, nabla_f, stopping_fn, m=50, record_every=500, proj=None, log=None,
+                options=None):
+    """LBFGS.solve (LBFGS.py:56-123): the two-loop recursion over the last m
+    pairs (search_dir :60-71, lists of m zero pairs initially :80), the weak
+    Wolfe line search, the y.s == 0 exit (:105-108)."""
+    def search_dir(g_new, y_new, s_new, rho, y, s):
+        q = g_new
+        alpha = [0] * m
+        for k in range(m - 1, -1, -1):
+            alpha[k] = rho[k] * (s[k].dot(q))
+            q = q - alpha[k] * y[k]
+        r = (y_new.dot(s_new) / (y_new.dot(y_new))) * q
+        for k in range(m):
+            beta = rho[k] * y[k].dot(r)
+            r = r + s[k] * (alpha[k] - beta)
+        return -r
+
+    start = log(0, x0, 0)
+    i, stop = 0, False
+    x = x0
+    n = x.shape[0]
+    y, s = [np.zeros(n)] * m, [np.zeros(n)] * m
+    g_new = nabla_f(x)
+    y_new, s_new = g_new, np.ones(n)
+    rho, rho_new = [0] * m, 1 / (y_new.dot(s_new))
+    while not stop:
+        i += 1
+        d = search_dir(g_new, y_new, s_new, rho, y, s)
+        y = y[1:] + [y_new]
+        s = s[1:] + [s_new]
+        rho = rho[1:] + [rho_new]
+        t = weak_wolfe_ls(x, d, f, nabla_f, proj=proj)
+        s_new = t * d
+        x_next = x + s_new
+        if proj:
+            x_next = proj(x_next)
+        g = g_new
+        g_new = nabla_f(x_next)
+        y_new = g_new - g
+        if y_new.dot(s_new) == 0:
+            break
+        rho_new = 1 / (y_new.dot(s_new))
+        x = x_next
+        fx = f(x)
+        if math.isnan(fx):
+            raise ArithmeticError('objective function evaluates to NaN')
+        stop = stopping_fn(g_new, fx, i, t, d=d, options=options)
+        if i % record_every == 0:
+            start = log(i, x, time.time() - start)
+    log(i, x, time.time() - start)
+    return x
+
+
+def lbfgs_trace(A, b, block_sizes, iters, record_every=1):
+    """lbfgs_solve from GradientDescent('LBFGS')'s start (z0 + 1,
+    gradient_descent.py:49) on main.solve_in_z's closures; return {iter: z}."""
+    P = solve_in_z_parts(A, b, block_sizes)
+    rec = {}
+
+    def log(i, state, dt):
+        rec[i] = np.array(state)
+        return 0.0
+    lbfgs_solve(P['z0'] + 1, P['f'], P['nabla_f'], stopping, record_every=record_every,
+                proj=P['proj'], log=log,
+                options={'max_iter': iters, 'verbose': 0, 'opt_tol': 1e-30})
     return rec
 
 

@@ -423,6 +423,43 @@ def gen_lbfgs_traces():
         out['%s_A_indptr' % tag], out['%s_A_shape' % tag] = A.indptr, np.array(A.shape)
         out['%s_b' % tag], out['%s_starts' % tag] = b, starts
         out['%s_x_init' % tag] = x_init
+    # LBFGS.solve (python/LBFGS.py:56-123) through GradientDescent('LBFGS')'s
+    # start (z0 + 1, gradient_descent.py:49) on a well-conditioned z-space
+    # problem (2000 links for 1000 routes: a 1e-15 gradient perturbation stays
+    # below 1e-12 over 60 iterations, where the plugins.npz problem amplifies
+    # it to 4e-8 by iteration 6), every iterate (record_every = 1)
+    import numpy.linalg as la
+    import LBFGS
+    import solvers
+    from bsls_utils import x2z, particular_x0, block_sizes_to_N
+    from c_extensions.c_extensions import isotonic_regression_multi_c
+    A, b, xs, sizes = sparse_problem(SEED + 33, 1000, 50, 2000, per_col=16, noise=0.01)
+    x0 = particular_x0(sizes)
+    N = block_sizes_to_N(sizes)
+    z0 = x2z(x0, sizes)
+    target = A.dot(x0) - b
+    AT = A.T.tocsr(); NT = N.T.tocsr()
+    f = lambda z: 0.5 * la.norm(A.dot(N.dot(z)) + target) ** 2
+    nabla_f = lambda z: NT.dot(AT.dot(A.dot(N.dot(z)) + target))
+    cum = np.concatenate(([0], np.cumsum(sizes - 1)))
+
+    def proj(x):
+        isotonic_regression_multi_c(x, cum[:-1])
+        return np.maximum(np.minimum(x, 1.), 0.)
+    rec = {}
+
+    def log(i, state, dt):
+        rec[i] = np.array(state)
+        return 0.0
+    with contextlib.redirect_stdout(io.StringIO()):
+        LBFGS.solve(z0 + 1, f, nabla_f, solvers.stopping, record_every=1, proj=proj, log=log,
+                    options={'max_iter': 60, 'verbose': 0, 'opt_tol': 1e-30})
+    keep = sorted(rec)
+    out['gd_iters'] = np.array(keep)
+    out['gd_states'] = np.array([rec[i] for i in keep])
+    out['gd_A_data'], out['gd_A_indices'] = A.data, A.indices
+    out['gd_A_indptr'], out['gd_A_shape'] = A.indptr, np.array(A.shape)
+    out['gd_b'], out['gd_block_sizes'] = b, np.asarray(sizes)
     np.savez_compressed(os.path.join(OUT, 'lbfgs.npz'), **out)
 
 

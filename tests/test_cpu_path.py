@@ -201,3 +201,22 @@ def test_lbfgs_cpu_path(golden):
     assert list(iters) == list(P['lbfgs_iters'])
     for k, s in enumerate(states):
         assert exact(s, P['lbfgs_states'][k]), k
+
+
+def test_lbfgs_cpu_path_60_iterations(golden):
+    """The same host path over the 60-iteration LBFGS.solve fixture
+    (tests/golden/lbfgs.npz gd_*: the reference's run, every iterate): the
+    start and the 60th iterate (GradientDescent logs 0 and the end), bit for
+    bit."""
+    import scipy.sparse as sps
+    from bsls_utils import particular_x0, block_sizes_to_N
+    from main import solve_in_z_cpu
+    d = golden('lbfgs.npz')
+    A = sps.csr_matrix((d['gd_A_data'], d['gd_A_indices'], d['gd_A_indptr']),
+                       shape=tuple(d['gd_A_shape']))
+    sizes = d['gd_block_sizes']
+    iters, _, states = solve_in_z_cpu(A, d['gd_b'], particular_x0(sizes),
+                                      block_sizes_to_N(sizes), sizes, 'LBFGS',
+                                      options={'max_iter': 60, 'verbose': 0, 'opt_tol': 1e-30})
+    assert list(iters) == [0, 60]
+    assert exact(states[0], d['gd_states'][0]) and exact(states[-1], d['gd_states'][-1])

@@ -247,3 +247,105 @@ def test_lbfgs_closures_on_reference_trajectory(cuda, golden, orc):
     assert sorted(rec) == list(range(6))
     for i in range(6):
         assert rel(rec[i], G['lbfgs_trace_states'][i]) < 1e-6, i
+
+
+def test_lbfgs_60_iterations_vs_reference(cuda, golden):
+    """GradientDescent('LBFGS') on the device (engine closures, the history
+    ring of csrc/lbfgs.hip) over the 60-iteration fixture of a
+    well-conditioned problem (tests/golden/lbfgs.npz gd_*, where a 1e-15
+    perturbation stays below 1e-12): every iterate within 1e-6 of the
+    reference's run."""
+    import torch
+    import LBFGS
+    import solvers
+    from device import BBEngine
+    G = golden('lbfgs.npz')
+    eng = BBEngine(_csr(G, 'gd'), G['gd_b'], G['gd_block_sizes'])
+    rec = {}
+
+    def log(i, s, dt):
+        rec[i] = s.detach().cpu().numpy().copy()
+        return 0.0
+    z0 = torch.ones(eng.nz, dtype=torch.float64, device='cuda')
+    LBFGS.solve(z0, eng.f, eng.nabla_f, solvers.stopping, record_every=1, proj=eng.proj,
+                log=log, options={'max_iter': 60, 'verbose': 0, 'opt_tol': 1e-30})
+    assert sorted(rec) == list(G['gd_iters'])
+    for k, it in enumerate(G['gd_iters']):
+        assert rel(rec[int(it)], G['gd_states'][k]) < 1e-6, it
+    # and through the dispatcher (logs 0 and the end)
+    opts = {'max_iter': 60, 'verbose': 0, 'opt_tol': 1e-30}
+    eng2, gd, iters, states = _gd_run(G, 'gd', 'LBFGS', opts)
+    assert list(iters) == [0, 60]
+    assert rel(states[-1], G['gd_states'][-1]) < 1e-6
+
+
+@pytest.mark.parametrize('m,pushes', [(1, 3), (5, 3), (5, 12), (50, 70)])
+def test_lbfgs_device_history_direction(cuda, m, pushes):
+    """_DeviceHistory.direction / push (csrc/lbfgs.hip: multi-dot, one-wave
+    recursion on the Gram matrices, combine) against the reference's vector
+    recursion (python/LBFGS.py:60-71) over the same lists, before and after
+    the ring wraps: 1e-11 relative."""
+    import torch
+    import LBFGS
+    rs = np.random.RandomState(m * 100 + pushes)
+    n = 3001
+    Y, S, rho = [np.zeros(n)] * m, [np.zeros(n)] * m, [0.0] * m
+    x = torch.zeros(n, dtype=torch.float64, device='cuda')
+    H = LBFGS._DeviceHistory(x, m)
+
+    def ref_dir(g, yn, sn):
+        q = g
+        alpha = [0.0] * m
+        for k in range(m - 1, -1, -1):
+            alpha[k] = rho[k] * S[k].dot(q)
+            q = q - alpha[k] * Y[k]
+        r = (yn.dot(sn) / yn.dot(yn)) * q
+        for k in range(m):
+            beta = rho[k] * Y[k].dot(r)
+            r = r + S[k] * (alpha[k] - beta)
+        return -r
+    T = lambda v: torch.from_numpy(v.copy()).cuda()
+    for p in range(pushes):
+        g, sn = rs.randn(n), rs.randn(n)
+        yn = sn * (1 + rs.rand(n)) + 0.1 * rs.randn(n)      # y.s > 0, as on a convex f
+        rn = 1.0 / yn.dot(sn)
+        d = H.direction(T(g), T(yn), T(sn)).cpu().numpy()
+        want = ref_dir(g, yn, sn)
+        assert rel(d, want) < 1e-11, p
+        H.push(rn)
+        Y, S, rho = Y[1:] + [yn], S[1:] + [sn], rho[1:] + [rn]
+    assert H.head == pushes % m
+
+
+def test_multi_dot_and_axpy(cuda):
+    """bsls_multi_dot / bsls_multi_axpy against NumPy (J = 1..4, K across
+    column chunks, ragged n), 1e-13 relative; deterministic (two runs bit
+    for bit)."""
+    import torch
+    import _native
+    L = _native.lib()
+    rs = np.random.RandomState(5)
+    n = 70_001
+    V = torch.from_numpy(rs.randn(40, n)).cuda()
+    ptrs = lambda rows: torch.tensor([V[i].data_ptr() for i in rows], dtype=torch.int64).cuda()
+    st = _native.stream_handle()
+    Vh = V.cpu().numpy()
+    for J, K in [(1, 1), (2, 17), (3, 33), (4, 16)]:
+        rows, cols = list(range(J)), list(range(40 - K, 40))
+        out = torch.empty(J * K, dtype=torch.float64, device='cuda')
+        wb = L.bsls_multi_dot_workspace_size(J, K)
+        w = torch.empty((wb + 7) // 8, dtype=torch.float64, device='cuda')
+        R, C = ptrs(rows), ptrs(cols)
+        outs = []
+        for _ in range(2):
+            _native.check(L.bsls_multi_dot(_native.ptr(R), J, _native.ptr(C), K, n,
+                                           _native.ptr(out), _native.ptr(w), wb, st))
+            outs.append(out.cpu().numpy().copy())
+        want = (Vh[rows] @ Vh[cols].T).reshape(-1)
+        assert rel(outs[0], want) < 1e-13
+        assert np.array_equal(outs[0], outs[1])
+    coef = torch.from_numpy(rs.randn(25)).cuda()
+    out = torch.empty(n, dtype=torch.float64, device='cuda')
+    _native.check(L.bsls_multi_axpy(_native.ptr(ptrs(range(25))), 25, _native.ptr(coef), n,
+                                    _native.ptr(out), st))
+    assert rel(out.cpu().numpy(), coef.cpu().numpy() @ Vh[:25]) < 1e-13

@@ -370,6 +370,20 @@ def test_golden_batch_solve_lbfgs(orc, golden, tag):
         assert exact(sol['progress'], d[key + '_prog'])
 
 
+def test_golden_lbfgs_solve(orc, golden):
+    """LBFGS.solve (python/LBFGS.py:56-123) from GradientDescent('LBFGS')'s
+    start z0 + 1 over main.solve_in_z's closures, 60 iterations, every iterate
+    (tests/golden/lbfgs.npz gd_*): the restatement reproduces the reference
+    bit for bit (history of m = 50 zero pairs, weak Wolfe bisection)."""
+    d = golden('lbfgs.npz')
+    A = sps.csr_matrix((d['gd_A_data'], d['gd_A_indices'], d['gd_A_indptr']),
+                       shape=tuple(d['gd_A_shape']))
+    rec = orc.lbfgs_trace(A, d['gd_b'], d['gd_block_sizes'], int(d['gd_iters'][-1]))
+    assert sorted(rec) == list(d['gd_iters'])
+    for k, it in enumerate(d['gd_iters']):
+        assert exact(rec[int(it)], d['gd_states'][k]), it
+
+
 @pytest.mark.parametrize('tag', ['s', 'c'])
 def test_golden_batch_solve_md(orc, golden, tag):
     """BATCH.solve_MD (python/BATCH.py:217-250), decreasing_step_size(i, 1, 1e8)."""
