@@ -361,10 +361,14 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
 // product; the rows' scales sit in LDS beside the sums); MODE 3: scaled
 // incidence with several groups (no bit pattern to keep): w_i = colv_i *
 // sum r, one product per row after the group sums, and the whole LDS for rows.
-// FUSE (stage 8, column-sharded): the finishing workgroup of row block rb also
-// sums r_i^2 over the rows [rb m / nrb, (rb + 1) m / nrb) of r (already the
-// all-reduced residual), and the last one records f and runs the stopping
-// test of iteration iter - 1 before it stores this iteration's sums.
+// FUSE (stage 8, column-sharded): every workgroup first sums r_i^2 over its
+// slice of r (already the all-reduced residual; slice blockIdx of nrb * G, so
+// the linear read also warms the caches the walk gathers r from), the
+// finishing workgroup of row block rb adds its groups' slices in group order
+// (through wpart's tail, see bsls_bb_problem.wpart), and the last one records
+// f and runs the stopping test of iteration iter - 1 before it stores this
+// iteration's sums.  (At the end of the finishing workgroups only, the slice
+// sums cost 13 us of tail in the 8-way rehearsal.)
 template <int MODE, bool ITER, bool FUSE = false, int CV = 0>
 __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
                                                const double *__restrict__ gp,
@@ -382,6 +386,18 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     double *rc = lds + HR;
     const int64_t i0 = rb * T.H;
     const int64_t nloc = (i0 + T.H + 1 <= P.n) ? T.H + 1 : P.n - i0;   // rows incl. the halo
+    const int64_t G = T.ngroups;
+    double rr[1] = {0.0};
+    if constexpr (FUSE) {
+        if (ITER) {
+            const int64_t ns = T.nrb * G, sl = rb * G + g;
+            const int64_t q0 = sl * P.m / ns, q1 = (sl + 1) * P.m / ns;
+            for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
+                const double v = P.r[i];
+                rr[0] += v * v;
+            }
+        }
+    }
     for (int i = threadIdx.x; i < HR; i += blockDim.x) {
         rows[i] = 0.0;
         if (MODE == 2) rc[i] = (i < nloc) ? colv_t<CV>(P, i0 + i) : 0.0;
@@ -389,7 +405,14 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     __syncthreads();
     tile_walk_any<(MODE == 3 ? 0 : MODE)>(T, rb, g, P.r, rows, rc);
     __syncthreads();
-    const int64_t G = T.ngroups;
+    // wpart's tail: one slot per (group, row block) for the slices' r^2 sums
+    double *rrp = P.wpart + G * T.nrb * (T.H + 1);
+    if (FUSE && ITER && G > 1) {
+        block_sum<1>(rr, red);
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&rrp[g * T.nrb + rb], rr[0], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     bool fin = true;
     // dealt image, one group (MODE 3): w_i = colv_i * (sum of r over row i),
     // one product per row (the sums' order is not fixed anyway), formed in the
@@ -476,10 +499,15 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     }
     if (!ITER || !fin) return;
     if constexpr (FUSE) {
-        const int64_t q0 = rb * P.m / T.nrb, q1 = (rb + 1) * P.m / T.nrb;
-        for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
-            const double v = P.r[i];
-            sums[4] += v * v;
+        if (G == 1) {
+            sums[4] = rr[0];
+        } else if (threadIdx.x == 0) {
+            // (the group partials' hand-off above orders these slots too)
+            double o = 0.0;
+            for (int64_t c = 0; c < G; ++c)
+                o += __hip_atomic_load(&rrp[c * T.nrb + rb], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            sums[4] = o;
         }
     }
     block_sum<NS>(sums, red);

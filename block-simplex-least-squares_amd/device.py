@@ -818,7 +818,8 @@ class BBEngine:
         self.wpart = None
         if self.AT_til is not None and self.AT_til.img['ngroups'] > 1:
             ti = self.AT_til.img
-            self.wpart = torch.zeros(ti['ngroups'] * ti['nrb'] * (ti['H'] + 1), **dev)
+            # + one slot per (group, row block): stage 8's r^2 slices
+            self.wpart = torch.zeros(ti['ngroups'] * ti['nrb'] * (ti['H'] + 2), **dev)
         self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
         # the scales as the kernels read them every iteration: the narrowest
         # exact type (flows are integers: _Float16; value_codec)

@@ -324,7 +324,8 @@ typedef struct bsls_bb_problem {
     /* Tile images replacing the panels when their ent is not NULL (then A / AT
      * are not read): At for K1 (halo 0; ngroups partials in rpart), ATt for K2
      * (halo 1; with ngroups > 1 the partial row sums go through wpart,
-     * ngroups * nrb * (H + 1) doubles). */
+     * ngroups * nrb * (H + 1) doubles, then ngroups * nrb slots for stage 8's
+     * r^2 slices: ngroups * nrb * (H + 2) doubles in all). */
     bsls_tiles At;
     bsls_tiles ATt;
     double *wpart;

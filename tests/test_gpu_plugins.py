@@ -86,10 +86,17 @@ def test_main_end_to_end(cuda, golden, tmp_path, vi, det):
     assert rel(output['percent flow allocated incorrectly'][:-1],
                G['main%d_pct' % vi][:-1]) < 1e-6
     # the run ends at an exact-zero sum(delta_g) (BB.py:22) or at ||g||^2 <= 1e-30:
-    # both depend on the last bits of a converged trajectory, so the final
-    # iteration is pinned to the reference's order of magnitude and the final
-    # state to the solution (both runs reach 0.5||Ax-b||^2 < 1e-16)
-    assert abs(iters[-1] - ref_iters[-1]) <= max(10, ref_iters[-1] // 4), (iters, ref_iters)
+    # both depend on the last bits of a converged trajectory (the device sums
+    # in another order than NumPy), so the final iteration is pinned to a band
+    # around the reference's and the final state to the solution (both runs
+    # reach 0.5||Ax-b||^2 < 1e-16).  Measured on MI355X (tools/exit_iters.py,
+    # round 3): reference 454 / 569 / 745; fixed-order engine 443 / 572 / 774
+    # on every run (so pinned exactly, a regression check of its order); the
+    # default engine 443-445 / 552-570 / 773-785
+    DET_EXIT = [443, 572, 774]
+    if det:
+        assert iters[-1] == DET_EXIT[vi], (iters[-1], DET_EXIT[vi])
+    assert abs(iters[-1] - ref_iters[-1]) <= max(10, ref_iters[-1] // 16), (iters, ref_iters)
     assert G['main%d_err' % vi][-1] < 1e-16
 
 

@@ -54,6 +54,9 @@ for s in $STEPS; do
     legs)
       timeout -k 10 600 python bench.py --legs "${LEGS:-lbfgs}" > $OUT/bench_legs.log 2>&1
       rc=$?; echo "legs rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    exit)
+      timeout -k 10 300 python tools/exit_iters.py > $OUT/exit_iters.log 2>&1
+      rc=$?; echo "exit rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
     rehearse)
       timeout -k 10 400 python bench.py --rehearse-shard 8 --steps 200 --warmup 20 \
           > $OUT/rehearse8.log 2>&1
@@ -75,6 +78,19 @@ for s in $STEPS; do
         python3 tools/traffic.py $cfg $OUT/traffic.json $OUT/pmc_${cfg}_1 $OUT/pmc_${cfg}_2 \
             > /dev/null 2> $OUT/traffic_$cfg.err
       done ;;
+    sq)
+      # SQ occupancy / issue / wait counters over the C3 kernels, the C2
+      # projection and the planned standalone PAVA (two passes, 8 SQ each)
+      i=0
+      for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+                 "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"; do
+        i=$((i+1))
+        rm -rf $OUT/sq_$i
+        timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/sq_$i -o pmc \
+            -- python3 tools/kprof.py --config C3 --iters 5 --proj 5 --iso 10 > $OUT/sq_$i.log 2>&1
+        rc=$?; echo "sq $i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
+      done
+      python3 tools/pmc_summary.py $OUT/sq_1 $OUT/sq_2 > $OUT/r03_sq_summary_C3.txt 2>&1 ;;
     prof)
       for k in $PROF; do
         case "$k" in
