@@ -474,7 +474,7 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
 // C2 grid is ~6 waves per SIMD instead of ~1.5, so loads, the sort and chain,
 // and stores of different waves overlap.  Measured: 27.2 against 20.3 us at
 // C2 -- the full 64-sort per quad is 4x the one-lane path's VALU work (9.0M
-// against 2.8M instructions per launch, VALU-bound); BSLS_PROJ_QUAD=1 only.
+// against 2.8M instructions per launch, VALU-bound); BSLS_PROJ_LANES=4 only.
 constexpr int QB = WAVE / 4;                 // blocks per wave
 constexpr int QCAP = QB * SMALL_MAX;         // a range of QB blocks <= 64 fits
 constexpr int QBUF = QCAP + 2 * WAVE + 2;
@@ -752,6 +752,267 @@ __global__ __launch_bounds__(64) void proj_quad_kernel(double *__restrict__ y,
     }
 }
 
+// ---- one lane PAIR per block (proj_pair_kernel) ----------------------------
+// Two lanes per block of <= 64 entries, 32 blocks per wave (3125 waves at C2,
+// ~3 per SIMD, all resident: 11 KB of LDS each): lane h of a pair holds
+// entries h, h + 2, h + 4, ... (<= 32 each; adjacent lanes read adjacent
+// doubles).  Each lane selects its 16 largest (the top-16
+// networks of proj_net.hpp on <= 32 entries), one DPP exchange merges the two
+// top-16s (half-cleaner + bitonic merge) into the block's top 16, sorted, in
+// both lanes, and the early-settling chain runs over them as in
+// lane_block_lds.  A wave with a block still open after 16 sorts its blocks
+// fully: each lane sorts its 32, a cross-pair merge leaves the block's
+// largest 32 in lane 0 and the rest in lane 1, and the chain continues from
+// lane 0 into lane 1.  Same arithmetic as the one-lane path, bit-identical.
+constexpr int PRB = WAVE / 2;                // blocks per wave
+constexpr int PRCAP = 1280;                  // staged range (C2 max ~1170)
+constexpr int PRBUF = PRCAP + 2 * WAVE + 2;
+constexpr int QP_PAIR0 = 0xA0;               // [0,0,2,2]: lane 1 of a pair reads lane 0
+
+template <int N, int M>
+__device__ __forceinline__ void bitonic_merge_n(double (&v)[M]) {
+#pragma unroll
+    for (int j = N / 2; j > 0; j >>= 1) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if ((i & j) == 0) {
+                double hi, lo;
+                asm volatile("v_max_f64 %0, %2, %3\n\tv_min_f64 %1, %2, %3"
+                             : "=&v"(hi), "=v"(lo)
+                             : "v"(v[i]), "v"(v[i + j]));
+                v[i] = hi;
+                v[i + j] = lo;
+            }
+        }
+    }
+}
+
+// the 16 largest of this lane's KB2 (<= 32) entries into v[0 .. 16), sorted
+template <int KB2>
+__device__ __forceinline__ void pair_top16(double (&v)[32]) {
+    if constexpr (KB2 <= 16) bitonic_flip<16, KB2>(*reinterpret_cast<double(*)[16]>(&v[0]));
+    else if constexpr (KB2 <= 24) Top16<24>::template run<0>(v);
+    else Top16<32>::template run<0>(v);
+}
+
+// lambda of a pair's block from the full sort (rare path): lane 0 holds
+// u_0..u_31, lane 1 u_32..u_63, both sorted descending
+__device__ __forceinline__ double pair_lambda_full(const double (&u)[32], int h, int k, double Mx) {
+    const double kk = (double)k;
+    const double margin = kk * 0x1p-49 * (1. + 2. * kk * Mx);
+    QChain c;
+    c.run = u[0];
+    c.D0 = 1. - c.run;
+    c.Drho = c.D0;
+    c.rho = 0;
+    c.a = 0;
+    c.live = k > 1;
+    const bool mine0 = h == 0;
+    // lane 0's 32 (as two runs of 16 indices, the ballot exits every 4 steps)
+    {
+        double lo16[16], hi16[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            lo16[j] = u[j];
+            hi16[j] = u[16 + j];
+        }
+        qchain_steps<1>(lo16, 0, k, margin, mine0, c);
+        qchain_steps<0>(hi16, 16, k, margin, mine0, c);
+        // hand the state to lane 1 (lane 0 keeps its own) and go on there
+        c.run = qperm_d<QP_PAIR0>(c.run);
+        c.D0 = qperm_d<QP_PAIR0>(c.D0);
+        c.Drho = qperm_d<QP_PAIR0>(c.Drho);
+        c.rho = qperm_i<QP_PAIR0>(c.rho);
+        c.a = qperm_i<QP_PAIR0>(c.a);
+        c.live = qperm_i<QP_PAIR0>(c.live);
+        qchain_steps<0>(lo16, 32, k, margin, !mine0, c);
+        qchain_steps<0>(hi16, 48, k, margin, !mine0, c);
+    }
+    // lane 1 of the pair holds the block's state
+    const int src = (threadIdx.x & ~1) + 1;
+    double lam = c.rho == 0 ? c.D0 : c.Drho / ((double)c.rho + 1.);
+    lam = __shfl(lam, src, WAVE);
+    const int amb = __shfl(c.a, src, WAVE);
+    if (__builtin_amdgcn_ballot_w64(amb != 0)) {
+        double lo16[16], hi16[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            lo16[j] = u[j];
+            hi16[j] = u[16 + j];
+        }
+        double run = u[0], lx = 1. - u[0];
+        qexact_steps(lo16, 0, 1, mine0 ? k : 0, run, lx);
+        qexact_steps(hi16, 16, 0, mine0 ? k : 0, run, lx);
+        run = qperm_d<QP_PAIR0>(run);
+        lx = qperm_d<QP_PAIR0>(lx);
+        qexact_steps(lo16, 32, 0, mine0 ? 0 : k, run, lx);
+        qexact_steps(hi16, 48, 0, mine0 ? 0 : k, run, lx);
+        lx = __shfl(lx, src, WAVE);
+        if (amb != 0) lam = lx;
+    }
+    return lam;
+}
+
+template <int KB2>
+__device__ __forceinline__ double pair_lambda(double *base, int h, int k) {
+    double v[32];
+    uint32_t hx = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const bool in = j < KB2 && 2 * j + h < k;
+        const double t = in ? base[2 * j + h] : -INFINITY;
+        const uint32_t hh = (uint32_t)((uint64_t)__double_as_longlong(t) >> 32) & 0x7fffffffu;
+        hx = (in && hh > hx) ? hh : hx;
+        v[j] = t;
+    }
+    hx = max(hx, (uint32_t)qperm_i<QP_XOR1>((int)hx));
+    const double Mx = __longlong_as_double((long long)(((uint64_t)hx << 32) | 0xffffffffull));
+    pair_top16<KB2>(v);
+    // the block's top 16 in both lanes: max(A_i, B_{15-i}), bitonic merge
+    // (pairwise, so no second array of 16 is live)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double a = v[i], c = v[15 - i];
+        const double pa = qperm_d<QP_XOR1>(c), pc = qperm_d<QP_XOR1>(a);
+        v[i] = fmax(a, pa);
+        v[15 - i] = fmax(c, pc);
+    }
+    bitonic_merge_n<16>(v);
+    const double kk = (double)k;
+    const double margin = kk * 0x1p-49 * (1. + 2. * kk * Mx);
+    Chain c = chain_begin(v, k);
+    chain_steps<1, 16>(v, k, margin, c);
+    const bool full = __builtin_amdgcn_ballot_w64(c.live && k > 16) != 0;
+    if (!full) {
+        double lam = chain_lambda(c);
+        if (__builtin_amdgcn_ballot_w64(c.a != 0)) {
+            if (c.a != 0) lam = lambda_sorted<32, 16>(v, k < 16 ? k : 16);
+        }
+        return lam;
+    }
+    // rare: sort the block fully across the pair
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = (j < KB2 && 2 * j + h < k) ? base[2 * j + h] : -INFINITY;
+    bitonic_flip<32, 32>(v);
+    {
+        const bool lo = h != 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const double a = v[i], c = v[31 - i];
+            const double pa = qperm_d<QP_XOR1>(c), pc = qperm_d<QP_XOR1>(a);
+            v[i] = lo ? fmin(a, pa) : fmax(a, pa);
+            v[31 - i] = lo ? fmin(c, pc) : fmax(c, pc);
+        }
+        bitonic_merge_n<32>(v);
+    }
+    return pair_lambda_full(v, h, k, Mx);
+}
+
+// lambda, then y = max(lambda + y, 0) over this lane's entries: every read in
+// flight before the writes (straight-line, as lane_block_lds)
+template <int KB2>
+__device__ __forceinline__ void pair_block(double *base, int h, int k) {
+    const double lam = pair_lambda<KB2>(base, h, k);
+    asm volatile("" ::: "memory");
+    double o[KB2];
+#pragma unroll
+    for (int j = 0; j < KB2; ++j) o[j] = (2 * j + h < k) ? base[2 * j + h] : 0.0;
+#pragma unroll
+    for (int j = 0; j < KB2; ++j)
+        if (2 * j + h < k) base[2 * j + h] = relu_ref(lam + o[j]);
+}
+
+// Blocks <= 64, one lane pair each, the wave's 32 consecutive blocks staged
+// in LDS (a range longer than PRCAP -- a block > 64 inside, or an unusually
+// heavy run -- is read from global memory).
+__global__ __launch_bounds__(64, 3) void proj_pair_kernel(double *__restrict__ y,
+                                                       const int64_t *__restrict__ starts,
+                                                       int64_t nb, int64_t n,
+                                                       int64_t *__restrict__ big_list,
+                                                       unsigned *__restrict__ big_count,
+                                                       int allow_big,
+                                                       const double *__restrict__ gate) {
+    __shared__ __attribute__((aligned(16))) double buf[PRBUF];
+    if (gate && *gate != 1.0) return;
+    const int lane = threadIdx.x;
+    const int h = lane & 1;
+    const int64_t b0 = (int64_t)blockIdx.x * PRB;
+    const int64_t b = b0 + (lane >> 1);
+    int k = 0;
+    int64_t s = 0, e = 0;
+    if (b < nb) {
+        s = starts[b];
+        e = block_end(starts, nb, b, n);
+        const int64_t kk = e - s;
+        if (kk > SMALL_MAX) {
+            if (allow_big && h == 0) {
+                unsigned slot = atomicAdd(big_count, 1u);
+                big_list[slot] = b;
+            }
+        } else {
+            k = (int)kk;
+        }
+    }
+    const int kmax = wave_max(k);
+    if (kmax == 0) return;
+    const int lastp = (int)((nb - b0 < PRB ? nb - b0 : PRB) - 1);
+    const int64_t s0 = uni64(s, 0);
+    const int64_t e1 = uni64(e, 2 * lastp);
+    const int64_t total = e1 - s0;
+    double *src = y + s0;
+    const int sh = (int)(((uintptr_t)src >> 3) & 1);
+    const bool staged = total <= PRCAP;
+    const int tot = staged ? (int)total : 0;
+    const int npair = staged ? (tot - sh) >> 1 : 0;
+    if (staged) {
+        const char *gs = (const char *)(src + sh);
+        char *ls = (char *)(buf + 2 * sh);
+        for (int p = 0; p * WAVE < npair; ++p) {
+            const int i = p * WAVE + lane;
+            if (i < npair)
+                __builtin_amdgcn_global_load_lds((const void *)(gs + 16 * i),
+                                                 (__attribute__((address_space(3))) void *)(ls + 1024 * p),
+                                                 16, 0, 0);
+        }
+        if (lane == 0) {
+            if (sh) buf[1] = src[0];
+            if ((tot - sh) & 1) buf[sh + tot - 1] = src[tot - 1];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    double *base = staged ? buf + ((k > 0) ? (int)(s - s0) + sh : 0) : y + s;
+    if (kmax <= 32) pair_block<16>(base, h, k);
+    else if (kmax <= 48) pair_block<24>(base, h, k);
+    else pair_block<32>(base, h, k);
+    if (!staged) return;
+    __syncthreads();
+    double *dst = y + s0 + sh;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(dst, 0, npair * 16, 0x00020000);
+    constexpr int SB = 8;
+    for (int c0 = 0; c0 < npair; c0 += SB * WAVE) {
+        double2 t[SB];
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+            const int p = c0 + q * WAVE + lane;
+            t[q] = *(const double2 *)&buf[2 * sh + 2 * (p < npair ? p : 0)];
+        }
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+            const int p = c0 + q * WAVE + lane;
+            if (p < npair)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(HIP_vector_type<unsigned, 4>::Native_vec_, t[q]), rs,
+                    16 * p, 0, 16);
+        }
+    }
+    if (lane == 0) {
+        if (sh) y[s0] = buf[1];
+        if ((tot - sh) & 1) y[s0 + tot - 1] = buf[sh + tot - 1];
+    }
+}
+
 // In-place descending bitonic sort of u[0..P) by the whole workgroup
 // (u in LDS or in global memory private to this workgroup).
 template <typename Ptr>
@@ -1001,13 +1262,17 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
     // (max_block is the caller's bound on every block length, like the
     // workspace size derived from it): otherwise no reset launch at all
     if (max_block > SMALL_MAX) BSLS_CHECK(hipMemsetAsync(w.count, 0, 16, st));
-    static const int quad = [] {
-        const char *e = getenv("BSLS_PROJ_QUAD");
-        return e ? atoi(e) : 0;   // measured slower at C2: A/B only
+    // BSLS_PROJ_LANES = 1 (one lane per block), 2 (a lane pair), 4 (a quad)
+    static const int lanes = [] {
+        const char *e = getenv("BSLS_PROJ_LANES");
+        return e ? atoi(e) : 1;
     }();
-    if (!BALL && quad)
+    if (!BALL && lanes == 4)
         proj_quad_kernel<<<grid_for(nb, QB), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
                                                             max_block > SMALL_MAX, gate);
+    else if (!BALL && lanes == 2)
+        proj_pair_kernel<<<grid_for(nb, PRB), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                             max_block > SMALL_MAX, gate);
     else
         proj_lds_kernel<BALL><<<grid_for(nb, WAVE), WAVE, 0, st>>>(y, starts, nb, n, w.list,
                                                                     w.count, max_block > SMALL_MAX,

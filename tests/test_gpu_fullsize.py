@@ -147,3 +147,39 @@ def test_c4_mirror_descent_vs_oracle(c3, orc):
         assert np.all(np.isfinite(x))
         err = float(np.max(np.abs(x - xr) / np.maximum(np.abs(xr), 1e-300)))
         assert err < 1e-10, (it, err)
+
+
+def test_c3_deterministic_run_to_exit(cuda):
+    """The whole C3 BB run (noise-free data, main.py's opt_tol 1e-30, early
+    exits on) under the fixed-order engine (deterministic=True): a second run
+    stops at the same iteration, for the same reason, with the same z bit for
+    bit -- the exit iteration of a full-size run is a reproducible number
+    ('no test pins the exit iteration of the full C3 run') -- and
+    the run has converged (0.5 ||A x - b||^2 below 1e-12 of 0.5 ||b||^2)."""
+    import torch
+    import _native
+    from synthetic import make_shard, CONFIGS, SEED
+    from device import BBEngine
+    c = CONFIGS['C3']
+    sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+    b = np.asarray(sh['Ax'], dtype=np.float64)
+    runs = []
+    for _ in range(2):
+        eng = BBEngine(sh['A'], b, sh['block_sizes'],
+                       options={'max_iter': 50_000, 'opt_tol': 1e-30}, AT=sh['AT'],
+                       deterministic=True)
+        z = eng.solve(to_host=True, record_every=10 ** 9)
+        runs.append((eng.iterations, eng.stop_reason, z.cpu().numpy().copy(),
+                     float(eng.scalars()[_native.S_FX])))
+        del eng
+        torch.cuda.empty_cache()
+    (i0, s0, z0, f0), (i1, s1, z1, f1) = runs
+    print('C3 deterministic exit: iteration %d, reason %d, f %.3e' % (i0, s0, f0))
+    assert (i0, s0) == (i1, s1)
+    assert np.array_equal(z0.view(np.int64), z1.view(np.int64))
+    assert f0 == f1
+    assert f0 <= 1e-12 * 0.5 * float(b @ b)
+    # measured on MI355X (round 3): iteration 13830, the exact-zero sum(dg)
+    # exit (BB.py:22, STOP_NOCHANGE), f 5.7e-17 --
+    # a regression pin of the fixed-order engine's arithmetic
+    assert (i0, s0) == (13830, _native.STOP_NOCHANGE)
