@@ -118,6 +118,21 @@ def test_invalid_arguments_rejected_without_launch(native):
     assert L.bsls_isotonic_multi(4, None, None, 1, 1, None, 1, 1, None, 0, None, None) == \
         native.BSLS_E_ARG
     assert L.bsls_bb_prologue(None, None) == native.BSLS_E_ARG
+    # LBFGS.solve's history kernels (csrc/lbfgs.hip): argument and workspace
+    # checks come before any launch
+    p = ctypes.c_void_p(8)
+    assert L.bsls_multi_dot(p, 0, p, 4, 10, p, p, 1 << 20, None) == native.BSLS_E_ARG
+    assert L.bsls_multi_dot(p, 5, p, 4, 10, p, p, 1 << 20, None) == native.BSLS_E_ARG
+    assert L.bsls_multi_dot(p, 3, p, 4, 10, p, p, 8, None) == native.BSLS_E_WORKSPACE
+    assert L.bsls_multi_axpy(p, 257, p, 10, p, None) == native.BSLS_E_ARG
+    assert L.bsls_lbfgs_coef(0, 0, p, p, None) == native.BSLS_E_ARG
+    assert L.bsls_lbfgs_coef(128, 0, p, p, None) == native.BSLS_E_ARG
+    assert L.bsls_lbfgs_coef(5, 5, p, p, None) == native.BSLS_E_ARG
+    assert L.bsls_lbfgs_push(5, -1, 1.0, p, p, p, p, p, p, 10, None) == native.BSLS_E_ARG
+    # sizes: rho, SY, YY, coef, scratch; multi-dot partials per column chunk
+    assert L.bsls_lbfgs_state_size(50) == 8 * (50 + 2 * 50 * 50 + 101 + 150)
+    assert L.bsls_multi_dot_workspace_size(3, 102) >= 8 * 3 * 102
+    assert L.bsls_multi_dot_workspace_size(0, 10) == 0
 
 
 def test_isotonic_pack_plan(native):
