@@ -1410,25 +1410,11 @@ extern "C" int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int
     const bsls_bb_problem &P = *p;
     hipStream_t st = (hipStream_t)stream;
     const BBWork w = bb_layout(P);
-    // BSLS_BB_FUSE_RR=1: the schedule of the sharded path on one GPU -- K1's
-    // finish without the ||r||^2 reduction, which the next K2 folds in
-    // (stage 8), plus one stage-9 launch per call for its last iteration
-    static const bool fuse_rr = [] {
-        const char *e = getenv("BSLS_BB_FUSE_RR");
-        return e ? atoi(e) != 0 : false;
-    }();
     for (int64_t i = first_iter; i < first_iter + count; ++i) {
         const int zc = (int)((i - 1) & 1), zn = (int)(i & 1);
-        if (fuse_rr) launch_k2<true, true>(P, P.g[zc], P.g[zn], w, st, i);
-        else launch_k2<true>(P, P.g[zc], P.g[zn], w, st);
+        launch_k2<true>(P, P.g[zc], P.g[zn], w, st);
         launch_k3(P, i, P.z[zc], P.g[zn], P.z[zn], w, st);
-        if (fuse_rr) launch_k1<true, true, false>(P, i, w, st);
-        else launch_k1<true, true, true>(P, i, w, st);
-        BSLS_LAUNCH_CHECK();
-    }
-    if (fuse_rr && count > 0) {
-        bb_r_finish<<<(grid_for(P.m, 256) < R_FINISH_GRID ? grid_for(P.m, 256) : R_FINISH_GRID),
-                      256, 0, st>>>(P, first_iter + count - 1, w.pf, w.tkf, 0);
+        launch_k1<true, true, true>(P, i, w, st);
         BSLS_LAUNCH_CHECK();
     }
     return BSLS_OK;

@@ -460,559 +460,6 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
     }
 }
 
-// ---- one QUAD per block (proj_quad_kernel) ---------------------------------
-// Four lanes per block of <= 64 entries, 16 blocks per wave: lane q of a quad
-// holds entries [16q, 16q + 16) of its block (-inf padding).  Sort: each lane
-// sorts its 16 (flip bitonic), then two bitonic merge levels across the quad
-// by DPP quad permutes -- lane pairs (xor 1) merge into sorted 32s, the pairs
-// (xor 3, registers reversed; then xor 1 at distance 16) into the sorted 64:
-// lane q ends with u_{16q} >= ... >= u_{16q+15} of the whole block.  Chain:
-// the early-settling chain of lane_block_lds over lane 0's registers, handed
-// to lane 1, 2, 3 (DPP shift) only while a block is still open; ambiguous
-// blocks redo the reference's division chain the same way.  Same arithmetic
-// as the one-lane path (bit-identical results), four times the waves: the
-// C2 grid is ~6 waves per SIMD instead of ~1.5, so loads, the sort and chain,
-// and stores of different waves overlap.  Measured: 27.2 against 20.3 us at
-// C2 -- the full 64-sort per quad is 4x the one-lane path's VALU work (9.0M
-// against 2.8M instructions per launch, VALU-bound); BSLS_PROJ_LANES=4 only.
-constexpr int QB = WAVE / 4;                 // blocks per wave
-constexpr int QCAP = QB * SMALL_MAX;         // a range of QB blocks <= 64 fits
-constexpr int QBUF = QCAP + 2 * WAVE + 2;
-
-// quad_perm DPP controls (lane q of each quad reads lane perm[q])
-constexpr int QP_XOR1 = 0xB1;   // [1,0,3,2]
-constexpr int QP_XOR3 = 0x1B;   // [3,2,1,0]
-constexpr int QP_SHR1 = 0x90;   // [0,0,1,2]
-
-template <int CTRL>
-__device__ __forceinline__ double qperm_d(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
-template <int CTRL>
-__device__ __forceinline__ int qperm_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
-}
-
-// descending merge of a bitonic 16 (half-cleaners at 8, 4, 2, 1)
-__device__ __forceinline__ void bitonic_merge16(double (&v)[16]) {
-#pragma unroll
-    for (int j = 8; j > 0; j >>= 1) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if ((i & j) == 0) {
-                double hi, lo;
-                asm volatile("v_max_f64 %0, %2, %3\n\tv_min_f64 %1, %2, %3"
-                             : "=&v"(hi), "=v"(lo)
-                             : "v"(v[i]), "v"(v[i + j]));
-                v[i] = hi;
-                v[i + j] = lo;
-            }
-        }
-    }
-}
-
-// the quad's 64 entries sorted descending across its lanes (see above)
-__device__ __forceinline__ void quad_sort64(double (&v)[16], int ql) {
-    bitonic_flip<16, 16>(v);
-    {   // pairs: even lane max(A_i, B_{15-i}), odd lane min -> sorted 32s
-        double p[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) p[i] = qperm_d<QP_XOR1>(v[15 - i]);
-        const bool lo = ql & 1;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = lo ? fmin(v[i], p[i]) : fmax(v[i], p[i]);
-        bitonic_merge16(v);
-    }
-    {   // the two 32s: lanes 0,1 max against lanes 3,2 reversed, 2,3 min
-        double p[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) p[i] = qperm_d<QP_XOR3>(v[15 - i]);
-        const bool lo = ql >= 2;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = lo ? fmin(v[i], p[i]) : fmax(v[i], p[i]);
-        // each half is a bitonic 32 over a lane pair: distance 16 across it
-#pragma unroll
-        for (int i = 0; i < 16; ++i) p[i] = qperm_d<QP_XOR1>(v[i]);
-        const bool odd = ql & 1;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = odd ? fmin(v[i], p[i]) : fmax(v[i], p[i]);
-        bitonic_merge16(v);
-    }
-}
-
-// chain state handed along the quad
-struct QChain {
-    double run, D0, Drho;
-    int rho, a, live;
-};
-
-__device__ __forceinline__ void qchain_shift(QChain &c) {
-    c.run = qperm_d<QP_SHR1>(c.run);
-    c.D0 = qperm_d<QP_SHR1>(c.D0);
-    c.Drho = qperm_d<QP_SHR1>(c.Drho);
-    c.rho = qperm_i<QP_SHR1>(c.rho);
-    c.a = qperm_i<QP_SHR1>(c.a);
-    c.live = qperm_i<QP_SHR1>(c.live);
-}
-
-// chain_steps over this lane's registers as sorted indices base + j
-template <int J0>
-__device__ __forceinline__ void qchain_steps(const double (&u)[16], int base, int k, double margin,
-                                             bool mine, QChain &c) {
-#pragma unroll
-    for (int j = J0; j < 16; ++j) {
-        if (((j - J0) & 3) == 0 && !__builtin_amdgcn_ballot_w64(mine && c.live)) break;
-        const int i = base + j;
-        const bool live = c.live && (i < k);
-        c.run = c.run + u[j];
-        const double D = 1. - c.run;
-        const double ip1 = (double)i + 1.;
-        const double E = __builtin_fma(ip1, u[j], D);
-        const double T = ip1 * __builtin_fma(__builtin_fabs(u[j]), 0x1p-51, 0x1p-1070);
-        const bool ok = live && (E > T);
-        c.a |= (live && (E > 0.0) && !(E > T)) ? 1 : 0;
-        c.rho = ok ? i : c.rho;
-        c.Drho = ok ? D : c.Drho;
-        c.live = (live && !(E < -margin)) ? 1 : 0;
-        asm volatile("" : "+v"(c.Drho), "+v"(c.rho), "+v"(c.a), "+v"(c.run));
-    }
-}
-
-// lambda_sorted's division chain over this lane's registers (indices base + j)
-__device__ __forceinline__ void qexact_steps(const double (&u)[16], int base, int j0, int k,
-                                             double &run, double &lam) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int i = base + j;
-        if (j >= j0 && i < k) {
-            run = run + u[j];
-            const double cand = (1. - run) / ((double)i + 1.);
-            if (u[j] + cand > 0) lam = cand;
-        }
-    }
-}
-
-template <int CTRL>
-__device__ __forceinline__ double qbcast_d(double v) { return qperm_d<CTRL>(v); }
-
-// lambda of the quad's block (valid in every lane of the quad); u sorted
-// across the quad (quad_sort64), k entries, Mx >= max |u|
-__device__ __forceinline__ double quad_lambda(const double (&u)[16], int ql, int k, double Mx) {
-    const double kk = (double)k;
-    const double margin = kk * 0x1p-49 * (1. + 2. * kk * Mx);
-    QChain c;
-    c.run = u[0];
-    c.D0 = 1. - c.run;
-    c.Drho = c.D0;
-    c.rho = 0;
-    c.a = 0;
-    c.live = k > 1;
-    qchain_steps<1>(u, 0, k, margin, ql == 0, c);
-    int q = 0;
-    while (q < 3 && __builtin_amdgcn_ballot_w64(ql == q && c.live)) {
-        qchain_shift(c);            // lane q + 1 takes lane q's state
-        ++q;
-        qchain_steps<0>(u, 16 * q, k, margin, ql == q, c);
-    }
-    // the state sits in lane q of every quad: broadcast it
-    int src = (threadIdx.x & ~3) + q;
-    double lam = c.rho == 0 ? c.D0 : c.Drho / ((double)c.rho + 1.);
-    lam = __shfl(lam, src, WAVE);
-    const int amb = __shfl(c.a, src, WAVE);
-    if (__builtin_amdgcn_ballot_w64(amb != 0)) {
-        // the reference's chain with its divisions, lane by lane
-        double run = u[0], lx = 1. - u[0];
-        qexact_steps(u, 0, 1, (ql == 0) ? k : 0, run, lx);
-        src = threadIdx.x & ~3;
-        for (int h = 1; h < 4; ++h) {
-            if (!__builtin_amdgcn_ballot_w64(amb != 0 && 16 * h < k)) break;
-            run = qperm_d<QP_SHR1>(run);
-            lx = qperm_d<QP_SHR1>(lx);
-            qexact_steps(u, 16 * h, 0, (ql == h) ? k : 0, run, lx);
-            src = (threadIdx.x & ~3) + h;
-        }
-        // the front lane of the last hop holds every quad's result (a quad
-        // that finished earlier had it carried along unchanged)
-        lx = __shfl(lx, src, WAVE);
-        if (amb != 0) lam = lx;
-    }
-    return lam;
-}
-
-// Blocks <= 64, one quad each, the wave's 16 consecutive blocks staged in LDS
-// as proj_lds_kernel (a range holding a block > 64 is read from global).
-__global__ __launch_bounds__(64) void proj_quad_kernel(double *__restrict__ y,
-                                                       const int64_t *__restrict__ starts,
-                                                       int64_t nb, int64_t n,
-                                                       int64_t *__restrict__ big_list,
-                                                       unsigned *__restrict__ big_count,
-                                                       int allow_big,
-                                                       const double *__restrict__ gate) {
-    __shared__ __attribute__((aligned(16))) double buf[QBUF];
-    if (gate && *gate != 1.0) return;
-    const int lane = threadIdx.x;
-    const int ql = lane & 3;
-    const int64_t b0 = (int64_t)blockIdx.x * QB;
-    const int64_t b = b0 + (lane >> 2);
-    int k = 0;
-    int64_t s = 0, e = 0;
-    if (b < nb) {
-        s = starts[b];
-        e = block_end(starts, nb, b, n);
-        const int64_t kk = e - s;
-        if (kk > SMALL_MAX) {
-            if (allow_big && ql == 0) {
-                unsigned slot = atomicAdd(big_count, 1u);
-                big_list[slot] = b;
-            }
-        } else {
-            k = (int)kk;
-        }
-    }
-    const int kmax = wave_max(k);
-    if (kmax == 0) return;
-    const int lastq = (int)((nb - b0 < QB ? nb - b0 : QB) - 1);
-    const int64_t s0 = uni64(s, 0);
-    const int64_t e1 = uni64(e, 4 * lastq);
-    const int64_t total = e1 - s0;
-    double *src = y + s0;
-    const int sh = (int)(((uintptr_t)src >> 3) & 1);
-    const bool staged = total <= QCAP;
-    const int tot = staged ? (int)total : 0;
-    const int npair = staged ? (tot - sh) >> 1 : 0;
-    if (staged) {
-        const char *gs = (const char *)(src + sh);
-        char *ls = (char *)(buf + 2 * sh);
-        for (int p = 0; p * WAVE < npair; ++p) {
-            const int i = p * WAVE + lane;
-            if (i < npair)
-                __builtin_amdgcn_global_load_lds((const void *)(gs + 16 * i),
-                                                 (__attribute__((address_space(3))) void *)(ls + 1024 * p),
-                                                 16, 0, 0);
-        }
-        if (lane == 0) {
-            if (sh) buf[1] = src[0];
-            if ((tot - sh) & 1) buf[sh + tot - 1] = src[tot - 1];
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    // this lane's slice [16 ql, 16 ql + 16) of its block
-    double *base = staged ? buf + ((k > 0) ? (int)(s - s0) + sh : 0) : y + s;
-    const int j0 = 16 * ql;
-    double v[16];
-    uint32_t hx = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const bool in = j0 + j < k;
-        const double t = in ? base[j0 + j] : -INFINITY;
-        const uint32_t h = (uint32_t)((uint64_t)__double_as_longlong(t) >> 32) & 0x7fffffffu;
-        hx = (in && h > hx) ? h : hx;
-        v[j] = t;
-    }
-    hx = max(hx, (uint32_t)qperm_i<QP_XOR1>((int)hx));
-    hx = max(hx, (uint32_t)qperm_i<0x4E>((int)hx));     // [2,3,0,1]
-    const double Mx = __longlong_as_double((long long)(((uint64_t)hx << 32) | 0xffffffffull));
-    quad_sort64(v, ql);
-    const double lam = quad_lambda(v, ql, k, Mx);
-    asm volatile("" ::: "memory");
-    double o[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) o[j] = (j0 + j < k) ? base[j0 + j] : 0.0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-        if (j0 + j < k) base[j0 + j] = relu_ref(lam + o[j]);
-    if (!staged) return;
-    __syncthreads();
-    double *dst = y + s0 + sh;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(dst, 0, npair * 16, 0x00020000);
-    constexpr int SB = 8;
-    for (int c0 = 0; c0 < npair; c0 += SB * WAVE) {
-        double2 t[SB];
-#pragma unroll
-        for (int q = 0; q < SB; ++q) {
-            const int p = c0 + q * WAVE + lane;
-            t[q] = *(const double2 *)&buf[2 * sh + 2 * (p < npair ? p : 0)];
-        }
-#pragma unroll
-        for (int q = 0; q < SB; ++q) {
-            const int p = c0 + q * WAVE + lane;
-            if (p < npair)
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(HIP_vector_type<unsigned, 4>::Native_vec_, t[q]), rs,
-                    16 * p, 0, 16);
-        }
-    }
-    if (lane == 0) {
-        if (sh) y[s0] = buf[1];
-        if ((tot - sh) & 1) y[s0 + tot - 1] = buf[sh + tot - 1];
-    }
-}
-
-// ---- one lane PAIR per block (proj_pair_kernel) ----------------------------
-// Two lanes per block of <= 64 entries, 32 blocks per wave (3125 waves at C2,
-// ~3 per SIMD, all resident: 11 KB of LDS each): lane h of a pair holds
-// entries h, h + 2, h + 4, ... (<= 32 each; adjacent lanes read adjacent
-// doubles).  Each lane selects its 16 largest (the top-16
-// networks of proj_net.hpp on <= 32 entries), one DPP exchange merges the two
-// top-16s (half-cleaner + bitonic merge) into the block's top 16, sorted, in
-// both lanes, and the early-settling chain runs over them as in
-// lane_block_lds.  A wave with a block still open after 16 sorts its blocks
-// fully: each lane sorts its 32, a cross-pair merge leaves the block's
-// largest 32 in lane 0 and the rest in lane 1, and the chain continues from
-// lane 0 into lane 1.  Same arithmetic as the one-lane path, bit-identical.
-constexpr int PRB = WAVE / 2;                // blocks per wave
-constexpr int PRCAP = 1280;                  // staged range (C2 max ~1170)
-constexpr int PRBUF = PRCAP + 2 * WAVE + 2;
-constexpr int QP_PAIR0 = 0xA0;               // [0,0,2,2]: lane 1 of a pair reads lane 0
-
-template <int N, int M>
-__device__ __forceinline__ void bitonic_merge_n(double (&v)[M]) {
-#pragma unroll
-    for (int j = N / 2; j > 0; j >>= 1) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            if ((i & j) == 0) {
-                double hi, lo;
-                asm volatile("v_max_f64 %0, %2, %3\n\tv_min_f64 %1, %2, %3"
-                             : "=&v"(hi), "=v"(lo)
-                             : "v"(v[i]), "v"(v[i + j]));
-                v[i] = hi;
-                v[i + j] = lo;
-            }
-        }
-    }
-}
-
-// the 16 largest of this lane's KB2 (<= 32) entries into v[0 .. 16), sorted
-template <int KB2>
-__device__ __forceinline__ void pair_top16(double (&v)[32]) {
-    if constexpr (KB2 <= 16) bitonic_flip<16, KB2>(*reinterpret_cast<double(*)[16]>(&v[0]));
-    else if constexpr (KB2 <= 24) Top16<24>::template run<0>(v);
-    else Top16<32>::template run<0>(v);
-}
-
-// lambda of a pair's block from the full sort (rare path): lane 0 holds
-// u_0..u_31, lane 1 u_32..u_63, both sorted descending
-__device__ __forceinline__ double pair_lambda_full(const double (&u)[32], int h, int k, double Mx) {
-    const double kk = (double)k;
-    const double margin = kk * 0x1p-49 * (1. + 2. * kk * Mx);
-    QChain c;
-    c.run = u[0];
-    c.D0 = 1. - c.run;
-    c.Drho = c.D0;
-    c.rho = 0;
-    c.a = 0;
-    c.live = k > 1;
-    const bool mine0 = h == 0;
-    // lane 0's 32 (as two runs of 16 indices, the ballot exits every 4 steps)
-    {
-        double lo16[16], hi16[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            lo16[j] = u[j];
-            hi16[j] = u[16 + j];
-        }
-        qchain_steps<1>(lo16, 0, k, margin, mine0, c);
-        qchain_steps<0>(hi16, 16, k, margin, mine0, c);
-        // hand the state to lane 1 (lane 0 keeps its own) and go on there
-        c.run = qperm_d<QP_PAIR0>(c.run);
-        c.D0 = qperm_d<QP_PAIR0>(c.D0);
-        c.Drho = qperm_d<QP_PAIR0>(c.Drho);
-        c.rho = qperm_i<QP_PAIR0>(c.rho);
-        c.a = qperm_i<QP_PAIR0>(c.a);
-        c.live = qperm_i<QP_PAIR0>(c.live);
-        qchain_steps<0>(lo16, 32, k, margin, !mine0, c);
-        qchain_steps<0>(hi16, 48, k, margin, !mine0, c);
-    }
-    // lane 1 of the pair holds the block's state
-    const int src = (threadIdx.x & ~1) + 1;
-    double lam = c.rho == 0 ? c.D0 : c.Drho / ((double)c.rho + 1.);
-    lam = __shfl(lam, src, WAVE);
-    const int amb = __shfl(c.a, src, WAVE);
-    if (__builtin_amdgcn_ballot_w64(amb != 0)) {
-        double lo16[16], hi16[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            lo16[j] = u[j];
-            hi16[j] = u[16 + j];
-        }
-        double run = u[0], lx = 1. - u[0];
-        qexact_steps(lo16, 0, 1, mine0 ? k : 0, run, lx);
-        qexact_steps(hi16, 16, 0, mine0 ? k : 0, run, lx);
-        run = qperm_d<QP_PAIR0>(run);
-        lx = qperm_d<QP_PAIR0>(lx);
-        qexact_steps(lo16, 32, 0, mine0 ? 0 : k, run, lx);
-        qexact_steps(hi16, 48, 0, mine0 ? 0 : k, run, lx);
-        lx = __shfl(lx, src, WAVE);
-        if (amb != 0) lam = lx;
-    }
-    return lam;
-}
-
-template <int KB2>
-__device__ __forceinline__ double pair_lambda(double *base, int h, int k) {
-    double v[32];
-    uint32_t hx = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        const bool in = j < KB2 && 2 * j + h < k;
-        const double t = in ? base[2 * j + h] : -INFINITY;
-        const uint32_t hh = (uint32_t)((uint64_t)__double_as_longlong(t) >> 32) & 0x7fffffffu;
-        hx = (in && hh > hx) ? hh : hx;
-        v[j] = t;
-    }
-    hx = max(hx, (uint32_t)qperm_i<QP_XOR1>((int)hx));
-    const double Mx = __longlong_as_double((long long)(((uint64_t)hx << 32) | 0xffffffffull));
-    pair_top16<KB2>(v);
-    // the block's top 16 in both lanes: max(A_i, B_{15-i}), bitonic merge
-    // (pairwise, so no second array of 16 is live)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double a = v[i], c = v[15 - i];
-        const double pa = qperm_d<QP_XOR1>(c), pc = qperm_d<QP_XOR1>(a);
-        v[i] = fmax(a, pa);
-        v[15 - i] = fmax(c, pc);
-    }
-    bitonic_merge_n<16>(v);
-    const double kk = (double)k;
-    const double margin = kk * 0x1p-49 * (1. + 2. * kk * Mx);
-    Chain c = chain_begin(v, k);
-    chain_steps<1, 16>(v, k, margin, c);
-    const bool full = __builtin_amdgcn_ballot_w64(c.live && k > 16) != 0;
-    if (!full) {
-        double lam = chain_lambda(c);
-        if (__builtin_amdgcn_ballot_w64(c.a != 0)) {
-            if (c.a != 0) lam = lambda_sorted<32, 16>(v, k < 16 ? k : 16);
-        }
-        return lam;
-    }
-    // rare: sort the block fully across the pair
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = (j < KB2 && 2 * j + h < k) ? base[2 * j + h] : -INFINITY;
-    bitonic_flip<32, 32>(v);
-    {
-        const bool lo = h != 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const double a = v[i], c = v[31 - i];
-            const double pa = qperm_d<QP_XOR1>(c), pc = qperm_d<QP_XOR1>(a);
-            v[i] = lo ? fmin(a, pa) : fmax(a, pa);
-            v[31 - i] = lo ? fmin(c, pc) : fmax(c, pc);
-        }
-        bitonic_merge_n<32>(v);
-    }
-    return pair_lambda_full(v, h, k, Mx);
-}
-
-// lambda, then y = max(lambda + y, 0) over this lane's entries: every read in
-// flight before the writes (straight-line, as lane_block_lds)
-template <int KB2>
-__device__ __forceinline__ void pair_block(double *base, int h, int k) {
-    const double lam = pair_lambda<KB2>(base, h, k);
-    asm volatile("" ::: "memory");
-    double o[KB2];
-#pragma unroll
-    for (int j = 0; j < KB2; ++j) o[j] = (2 * j + h < k) ? base[2 * j + h] : 0.0;
-#pragma unroll
-    for (int j = 0; j < KB2; ++j)
-        if (2 * j + h < k) base[2 * j + h] = relu_ref(lam + o[j]);
-}
-
-// Blocks <= 64, one lane pair each, the wave's 32 consecutive blocks staged
-// in LDS (a range longer than PRCAP -- a block > 64 inside, or an unusually
-// heavy run -- is read from global memory).
-__global__ __launch_bounds__(64, 3) void proj_pair_kernel(double *__restrict__ y,
-                                                       const int64_t *__restrict__ starts,
-                                                       int64_t nb, int64_t n,
-                                                       int64_t *__restrict__ big_list,
-                                                       unsigned *__restrict__ big_count,
-                                                       int allow_big,
-                                                       const double *__restrict__ gate) {
-    __shared__ __attribute__((aligned(16))) double buf[PRBUF];
-    if (gate && *gate != 1.0) return;
-    const int lane = threadIdx.x;
-    const int h = lane & 1;
-    const int64_t b0 = (int64_t)blockIdx.x * PRB;
-    const int64_t b = b0 + (lane >> 1);
-    int k = 0;
-    int64_t s = 0, e = 0;
-    if (b < nb) {
-        s = starts[b];
-        e = block_end(starts, nb, b, n);
-        const int64_t kk = e - s;
-        if (kk > SMALL_MAX) {
-            if (allow_big && h == 0) {
-                unsigned slot = atomicAdd(big_count, 1u);
-                big_list[slot] = b;
-            }
-        } else {
-            k = (int)kk;
-        }
-    }
-    const int kmax = wave_max(k);
-    if (kmax == 0) return;
-    const int lastp = (int)((nb - b0 < PRB ? nb - b0 : PRB) - 1);
-    const int64_t s0 = uni64(s, 0);
-    const int64_t e1 = uni64(e, 2 * lastp);
-    const int64_t total = e1 - s0;
-    double *src = y + s0;
-    const int sh = (int)(((uintptr_t)src >> 3) & 1);
-    const bool staged = total <= PRCAP;
-    const int tot = staged ? (int)total : 0;
-    const int npair = staged ? (tot - sh) >> 1 : 0;
-    if (staged) {
-        const char *gs = (const char *)(src + sh);
-        char *ls = (char *)(buf + 2 * sh);
-        for (int p = 0; p * WAVE < npair; ++p) {
-            const int i = p * WAVE + lane;
-            if (i < npair)
-                __builtin_amdgcn_global_load_lds((const void *)(gs + 16 * i),
-                                                 (__attribute__((address_space(3))) void *)(ls + 1024 * p),
-                                                 16, 0, 0);
-        }
-        if (lane == 0) {
-            if (sh) buf[1] = src[0];
-            if ((tot - sh) & 1) buf[sh + tot - 1] = src[tot - 1];
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    double *base = staged ? buf + ((k > 0) ? (int)(s - s0) + sh : 0) : y + s;
-    if (kmax <= 32) pair_block<16>(base, h, k);
-    else if (kmax <= 48) pair_block<24>(base, h, k);
-    else pair_block<32>(base, h, k);
-    if (!staged) return;
-    __syncthreads();
-    double *dst = y + s0 + sh;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(dst, 0, npair * 16, 0x00020000);
-    constexpr int SB = 8;
-    for (int c0 = 0; c0 < npair; c0 += SB * WAVE) {
-        double2 t[SB];
-#pragma unroll
-        for (int q = 0; q < SB; ++q) {
-            const int p = c0 + q * WAVE + lane;
-            t[q] = *(const double2 *)&buf[2 * sh + 2 * (p < npair ? p : 0)];
-        }
-#pragma unroll
-        for (int q = 0; q < SB; ++q) {
-            const int p = c0 + q * WAVE + lane;
-            if (p < npair)
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(HIP_vector_type<unsigned, 4>::Native_vec_, t[q]), rs,
-                    16 * p, 0, 16);
-        }
-    }
-    if (lane == 0) {
-        if (sh) y[s0] = buf[1];
-        if ((tot - sh) & 1) y[s0 + tot - 1] = buf[sh + tot - 1];
-    }
-}
-
 // In-place descending bitonic sort of u[0..P) by the whole workgroup
 // (u in LDS or in global memory private to this workgroup).
 template <typename Ptr>
@@ -1262,21 +709,8 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
     // (max_block is the caller's bound on every block length, like the
     // workspace size derived from it): otherwise no reset launch at all
     if (max_block > SMALL_MAX) BSLS_CHECK(hipMemsetAsync(w.count, 0, 16, st));
-    // BSLS_PROJ_LANES = 1 (one lane per block), 2 (a lane pair), 4 (a quad)
-    static const int lanes = [] {
-        const char *e = getenv("BSLS_PROJ_LANES");
-        return e ? atoi(e) : 1;
-    }();
-    if (!BALL && lanes == 4)
-        proj_quad_kernel<<<grid_for(nb, QB), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
-                                                            max_block > SMALL_MAX, gate);
-    else if (!BALL && lanes == 2)
-        proj_pair_kernel<<<grid_for(nb, PRB), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
-                                                             max_block > SMALL_MAX, gate);
-    else
-        proj_lds_kernel<BALL><<<grid_for(nb, WAVE), WAVE, 0, st>>>(y, starts, nb, n, w.list,
-                                                                    w.count, max_block > SMALL_MAX,
-                                                                    gate);
+    proj_lds_kernel<BALL><<<grid_for(nb, WAVE), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                                  max_block > SMALL_MAX, gate);
     BSLS_LAUNCH_CHECK();
     if (max_block > SMALL_MAX) {
         int64_t nbig = nb < (n / (SMALL_MAX + 1) + 1) ? nb : (n / (SMALL_MAX + 1) + 1);

@@ -24,6 +24,8 @@ on MI355X; "gloo" runs the same orchestration in CPU tests with a fake stage
 backend.  Results depend on the rank count only through the summation order of
 the r all-reduce (within the 1e-6 iterate contract).
 """
+import os
+
 import numpy as np
 
 
@@ -73,8 +75,14 @@ class ShardedBB:
 
     SUMS = slice(5, 9)   # scal[SUMDG..GG]
 
-    def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None, rank=0):
+    def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None, rank=0, fuse=None):
         self.e = engine
+        # fuse: K2 folds in the previous iteration's ||r||^2 / f / stopping test
+        # (stage 8, one stage-9 launch per call); else stage 3 and a stage-9
+        # launch after every residual exchange.  BSLS_SHARD_FUSE=0|1 (A/B).
+        if fuse is None:
+            fuse = os.environ.get('BSLS_SHARD_FUSE', '1') != '0'
+        self.fuse = bool(fuse)
         # rank 0 adds target to its partial residual; the others zero theirs
         # once the run has stopped (bsls_bb_problem.shard_role)
         engine.set_shard_role(1 if rank == 0 else 2)
@@ -116,11 +124,16 @@ class ShardedBB:
     def iterate(self, first, count):
         e = self.e
         for i in range(first, first + count):
-            e.stage(8, i)        # K2 + f / stopping test of iteration i - 1
+            if self.fuse:
+                e.stage(8, i)    # K2 + f / stopping test of iteration i - 1
+            else:
+                e.stage(3, i)
             self.all_reduce(e.scal[self.SUMS])
             e.stage(4, i)
             self.residual(i)
-        if count > 0:
+            if not self.fuse:
+                e.stage(9, i)    # f / stopping test of iteration i
+        if count > 0 and self.fuse:
             e.stage(9, first + count - 1)   # f / stopping test of the last one
 
 

@@ -235,6 +235,23 @@ def test_two_rank_stop_keeps_final_residual(orc):
         assert d < 1e-10, (rank, d)
 
 
+@pytest.mark.timeout(600)
+def test_two_rank_unfused_schedule(orc, monkeypatch):
+    """ShardedBB(fuse=False) (BSLS_SHARD_FUSE=0: stage 3, then a stage-9 stop
+    test after every residual exchange, instead of stage 8's one-iteration
+    delay): the same trajectory as the fused schedule, and the same stop."""
+    iters = 10
+    fused = _spawn(2, iters)
+    monkeypatch.setenv('BSLS_SHARD_FUSE', '0')
+    plain = _spawn(2, iters)
+    for i in fused:
+        d = np.max(np.abs(fused[i] - plain[i])) / max(1.0, np.max(np.abs(fused[i])))
+        assert d < 1e-12, (i, d)
+    two = _spawn(2, 9, stop_at=5)
+    for rank in (0, 1):
+        assert two[rank]['scal'][0] == 2 and two[rank]['scal'][1] == 5
+
+
 def test_row_parts():
     sys.path.insert(0, PKG)
     from distributed import row_parts
