@@ -232,7 +232,7 @@ def bench_proj(reps=30, batch=16):
             'cpu_oracle_ms_1thread': cpu_s * 1e3, 'bit_exact_vs_oracle': ok}
 
 
-def bench_xspace(sh, b, rounds=40, reps=5):
+def bench_xspace(sh, b, rounds=40, reps=5, k1=None):
     """x-space BB (BATCH.solve_BB over get_solver_parts(is_sparse=True),
     SURVEY.md §8 rows a14/f2) on the same C3 matrix with the block simplex
     projection: device rounds (csrc/xbb.hip) over the panel operator
@@ -247,7 +247,16 @@ def bench_xspace(sh, b, rounds=40, reps=5):
     sizes = sh['block_sizes']
     starts = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
     x0 = np.repeat(1.0 / sizes, sizes)
-    _, proj, _, obj = get_solver_parts((sh['A'], b), starts, 1.0, is_sparse=True)
+    saved = os.environ.get('BSLS_LSQ_K1')
+    if k1:
+        os.environ['BSLS_LSQ_K1'] = k1      # DeviceLSQ reads it when it is built
+    try:
+        _, proj, _, obj = get_solver_parts((sh['A'], b), starts, 1.0, is_sparse=True)
+    finally:
+        if saved is None:
+            os.environ.pop('BSLS_LSQ_K1', None)
+        else:
+            os.environ['BSLS_LSQ_K1'] = saved
     eng = XBBEngine(obj, proj)
     x0d = torch.from_numpy(x0).cuda()
     eng.start(x0d, max_iter=10 ** 12, prog_tol=-1.0, hist_cap=1)
@@ -277,7 +286,9 @@ def bench_xspace(sh, b, rounds=40, reps=5):
     nr = rounds * reps
     common = 24 * nnz + 4 * (m + n + 2) + 24 * m + 16 * n + 32 * n
     byt = nr * common + (nr - bts) * (40 * n + 16 * n + 4 * (p + 1)) + bts * 24 * n
-    return {'operator': 'panels' if obj.lsq is not None else 'csr',
+    opname = 'csr' if obj.lsq is None else ('tiles residual + panels gradient'
+                                           if obj.lsq.k1 == 'tiles' else 'panels')
+    return {'operator': opname,
             'rounds': nr, 'us_per_round': ms * 1e3 / nr,
             'rounds_per_s': nr / (ms * 1e-3), 'iterations_per_s': its / (ms * 1e-3),
             'backtracks': bts, 'finite': ok,
@@ -900,6 +911,10 @@ def extras(args, legs, out, tfile):
         out['isotonic'] = bench_iso()
     if 'xspace' in legs:
         out['xspace_bb'] = bench_xspace(sh3, b3)
+        # the opt-in dealt-tile residual (not bit-reproducible: the
+        # reference's exact-revert exit needs the panels)
+        out['xspace_bb_tiles'] = bench_xspace(sh3, b3, k1='tiles')
+        torch.cuda.empty_cache()
     if 'md' in legs:
         out['mirror_descent'] = bench_md(sh3, b3)
     if 'dore' in legs:

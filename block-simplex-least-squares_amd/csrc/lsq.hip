@@ -13,6 +13,7 @@
 // products SciPy forms, one extra pass) and the gradient multiplies each
 // entry by its row's colv.
 #include "panels.hpp"
+#include "tiles.hpp"
 
 namespace bsls {
 
@@ -141,6 +142,50 @@ __global__ __launch_bounds__(1024) void lsq_k2(bsls_panels M, int64_t n,
     }
 }
 
+// The residual on a tile image of A (op->At.ent set: the dealt walk of the
+// z-space engine's K1, csrc/tiles.hpp): workgroup (rb, g) sums its rows over
+// group g's columns of x in LDS and stores them as rpart[g][row]; lsq_t_sum
+// (next in the stream) adds the groups in group order (+ add) and reduces
+// ||r||^2 -- the split finish of bb_k1t / bb_k1_sum.  LDS atomic sums: the
+// same sums to rounding, not run-to-run bit-identical (the panels are).
+template <int MODE>
+__global__ __launch_bounds__(1024) void lsq_k1t(bsls_tiles T, int64_t m,
+                                                const double *__restrict__ x,
+                                                double *__restrict__ rpart) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    int64_t rb, g;
+    tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, g);
+    const int HR = (int)tile_lds_doubles(T, false);
+    for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;
+    __syncthreads();
+    tile_walk_any<MODE>(T, rb, g, x, lds, nullptr);
+    __syncthreads();
+    const int64_t r0 = rb * T.H, r1 = (r0 + T.H < m) ? r0 + T.H : m;
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+        rpart[g * m + row] = lds[row - r0];
+}
+
+__global__ __launch_bounds__(256) void lsq_t_sum(int64_t m, int64_t G, const double *rpart,
+                                                 const double *__restrict__ add,
+                                                 double *__restrict__ r, double *sq_out,
+                                                 double *part, unsigned *ticket) {
+    __shared__ double red[4];
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    double sq[1] = {0.0};
+    for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < m; row += gs) {
+        double o = rpart[row];
+        for (int64_t c = 1; c < G; ++c) o += rpart[c * m + row];
+        if (add) o += add[row];
+        r[row] = o;
+        sq[0] += o * o;
+    }
+    if (!sq_out) return;
+    block_sum<1>(sq, red);
+    double tot[1];
+    if (last_block_sum<1>(sq, part, ticket, tot, red) && threadIdx.x == 0) *sq_out = tot[0];
+}
+constexpr int LSQ_SUM_GRID = 1024;
+
 constexpr int LSQ_LDS_MAX = 163840 - 512;
 template <typename K>
 static void lsq_allow_lds(K kernel) {
@@ -155,12 +200,22 @@ static void lsq_allow_lds(K kernel) {
 static bool lsq_ok(const bsls_lsq_op *op) {
     if (!op || op->m <= 0 || op->n <= 0) return false;
     const bsls_panels &A = op->A, &T = op->AT;
-    if (A.rows != op->m || A.cols != op->n || T.rows != op->n || T.cols != op->m) return false;
-    if (T.halo != 0 || T.ngroups != 1 || A.halo != 0 || A.ngroups < 1) return false;
-    if (A.prow < 1 || A.prow > BSLS_PANEL_ROWS || T.prow < 1 || T.prow > BSLS_PANEL_ROWS)
-        return false;
+    if (T.rows != op->n || T.cols != op->m || T.halo != 0 || T.ngroups != 1) return false;
+    if (T.prow < 1 || T.prow > BSLS_PANEL_ROWS) return false;
+    if (op->At.ent) {
+        const bsls_tiles &K = op->At;
+        if (K.rows != op->m || K.cols != op->n || K.halo != 0 || K.ngroups < 1 ||
+            K.nrb < 1 || !K.group_col || !K.wave_off || (K.layout & 3) == 0 || !K.base)
+            return false;
+        if ((op->colv == nullptr) != (K.val != nullptr)) return false;
+        if (tile_lds_doubles(K, false) * 8 > (size_t)LSQ_LDS_MAX) return false;
+    } else {
+        if (A.rows != op->m || A.cols != op->n || A.halo != 0 || A.ngroups < 1) return false;
+        if (A.prow < 1 || A.prow > BSLS_PANEL_ROWS) return false;
+    }
     if (!op->rpart || !op->work) return false;
-    if (op->colv ? (!op->xs || A.val || T.val) : (!A.val || !T.val)) return false;
+    if (op->colv ? (!op->xs || T.val) : !T.val) return false;
+    if (!op->At.ent && (op->colv ? A.val != nullptr : !A.val)) return false;
     return true;
 }
 
@@ -170,15 +225,42 @@ using namespace bsls;
 
 extern "C" size_t bsls_lsq_workspace_size(int64_t m, int64_t A_npanels) {
     (void)m;
-    return lsq_layout(nullptr, A_npanels).bytes;
+    // (the tile residual's reduction uses part's first LSQ_SUM_GRID slots)
+    const int64_t np = A_npanels > LSQ_SUM_GRID * PANEL_WAVES ? A_npanels : LSQ_SUM_GRID * PANEL_WAVES;
+    return lsq_layout(nullptr, np).bytes;
 }
 
 extern "C" int bsls_lsq_residual(const bsls_lsq_op *op, const double *d_x, const double *d_add,
                                  double *d_r, double *d_sq_out, void *stream) {
     if (!lsq_ok(op) || !d_x || !d_r) return BSLS_E_ARG;
-    LsqWork w = lsq_layout(op->work, op->A.npanels);
+    LsqWork w = lsq_layout(op->work, op->At.ent ? LSQ_SUM_GRID * PANEL_WAVES : op->A.npanels);
     if (op->work_bytes < w.bytes) return BSLS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
+    if (op->At.ent) {
+        const bsls_tiles &K = op->At;
+        const double *xin = d_x;
+        if (op->colv) {
+            lsq_scale_kernel<<<grid_for(op->n < 262144 ? op->n : 262144, 256), 256, 0, st>>>(
+                op->xs, op->colv, d_x, op->n);
+            BSLS_LAUNCH_CHECK();
+            xin = op->xs;
+        }
+        const int grid = (int)(K.nrb * K.ngroups);
+        const size_t lds = tile_lds_doubles(K, false) * 8;
+        if (op->colv) {
+            lsq_allow_lds(lsq_k1t<0>);
+            lsq_k1t<0><<<grid, BSLS_TILE_THREADS, lds, st>>>(K, op->m, xin, op->rpart);
+        } else {
+            lsq_allow_lds(lsq_k1t<1>);
+            lsq_k1t<1><<<grid, BSLS_TILE_THREADS, lds, st>>>(K, op->m, xin, op->rpart);
+        }
+        BSLS_LAUNCH_CHECK();
+        const int gk = grid_for(op->m, 256);
+        lsq_t_sum<<<gk < LSQ_SUM_GRID ? gk : LSQ_SUM_GRID, 256, 0, st>>>(
+            op->m, K.ngroups, op->rpart, d_add, d_r, d_sq_out, w.part, w.tk);
+        BSLS_LAUNCH_CHECK();
+        return BSLS_OK;
+    }
     const int64_t rbs = (op->A.npanels + PANEL_WAVES - 1) / PANEL_WAVES;
     const int grid = (int)(op->A.ngroups * rbs);
     if (op->colv) {

@@ -181,6 +181,35 @@ __device__ __forceinline__ double tile_val(const double *__restrict__ val, int64
     else return val[e];
 }
 
+// a lane's four stored values of one step (entries 4 l .. 4 l + 3 of the
+// lane's quad, aligned): one or two vector loads, streaming (nt) with NT like
+// the entries, so the value stream does not evict the gathered vector's lines
+typedef double tile_d2 __attribute__((ext_vector_type(2)));
+typedef float tile_f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 tile_h4 __attribute__((ext_vector_type(4)));
+template <typename V, bool NT>
+__device__ __forceinline__ V tile_vload(const V *p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <int VT, bool NT>
+__device__ __forceinline__ void tile_vals4(const double *__restrict__ val, int64_t e,
+                                           double (&w)[4]) {
+    if constexpr (VT == 1) {
+        const tile_f4 f = tile_vload<tile_f4, NT>(reinterpret_cast<const tile_f4 *>(
+            reinterpret_cast<const float *>(val) + e));
+        w[0] = (double)f.x; w[1] = (double)f.y; w[2] = (double)f.z; w[3] = (double)f.w;
+    } else if constexpr (VT == 2) {
+        const tile_h4 h = tile_vload<tile_h4, NT>(reinterpret_cast<const tile_h4 *>(
+            reinterpret_cast<const _Float16 *>(val) + e));
+        w[0] = (double)h.x; w[1] = (double)h.y; w[2] = (double)h.z; w[3] = (double)h.w;
+    } else {
+        const tile_d2 *p = reinterpret_cast<const tile_d2 *>(val + e);
+        const tile_d2 a = tile_vload<tile_d2, NT>(p), b = tile_vload<tile_d2, NT>(p + 1);
+        w[0] = a.x; w[1] = a.y; w[2] = b.x; w[3] = b.y;
+    }
+}
+
 template <int MODE, bool NT, bool PK3 = false, int VT = 0, int P = BSLS_TILE_P, int D = BSLS_TILE_D>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
@@ -225,10 +254,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
         o[1] = xb[b.y + (ent(u, 1) & cmask)];
         o[2] = xb[b.z + (ent(u, 2) & cmask)];
         o[3] = xb[b.w + (ent(u, 3) & cmask)];
-        if (MODE == 1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = tile_val<VT>(T.val, v0 + q * 4096 + j);
-        }
+        if (MODE == 1) tile_vals4<VT, NT>(T.val, v0 + q * 4096, w);
     };
 #pragma unroll
     for (int d = 0; d < D; ++d)

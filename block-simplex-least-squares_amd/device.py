@@ -572,14 +572,19 @@ def k1_plan(m, cus=256, max_groups=10):
 
 
 class DeviceLSQ:
-    """The x-space operator pair on panel images (csrc/lsq.hip, struct
-    bsls_lsq_op): residual r = A x + add with ||r||^2, gradient g = A' r.
-    sparse_least_squares_obj's two SciPy products (algorithm_utils.py:88-94).
-    A: column groups (k1_plan), no halo; A': one group.  A scaled incidence drops
-    the values (colv * x formed once per residual, A' entries scaled by colv
-    row by row: g stays bit-identical to SciPy's csr_matvec)."""
+    """The x-space operator pair (csrc/lsq.hip, struct bsls_lsq_op): residual
+    r = A x + add with ||r||^2, gradient g = A' r -- sparse_least_squares_obj's
+    two SciPy products (algorithm_utils.py:88-94).  The residual walks column
+    groups of panels (fixed order: f repeats bit for bit at the same x, which
+    the reference's exits rely on -- BATCH.solve_LBFGS's revert stops on
+    |f_old - f| < prog_tol with delta_x = 0); k1='tiles' (or
+    BSLS_LSQ_K1=tiles) walks a dealt tile image of A instead (the z-space
+    K1's walk: LDS atomic row sums, faster, the same sums to rounding only).
+    A' is one group of panels (every row in CSR order: g bit-identical to
+    SciPy's csr_matvec).  A scaled incidence drops the values (colv * x formed
+    once per residual, A' entries scaled by colv row by row)."""
 
-    def __init__(self, A, AT=None, general=False):
+    def __init__(self, A, AT=None, general=False, k1=None):
         torch = _torch()
         L = _native.lib()
         A = sps.csr_matrix(A)
@@ -587,19 +592,31 @@ class DeviceLSQ:
         self.m, self.n = A.shape
         colv = None if general else scaled_incidence_scale(A)
         self.scaled = colv is not None
-        prow, groups = k1_plan(self.m)
-        self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
+        k1 = k1 or os.environ.get('BSLS_LSQ_K1', 'panels')
+        self.A_pan = self.A_til = None
+        if k1 == 'tiles':
+            self.A_til = DeviceTiles(A, 0, values=not self.scaled, layout=2)
+            groups, npanels = self.A_til.img['ngroups'], 0
+        else:
+            prow, groups = k1_plan(self.m)
+            self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
+            groups, npanels = self.A_pan.img['ngroups'], self.A_pan.img['npanels']
+        self.k1 = k1
         self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), False, 1,
                                    values=not self.scaled)
         dev = dict(dtype=torch.float64, device='cuda')
         self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
         self.xs = torch.empty(self.n, **dev) if self.scaled else None
-        self.rpart = torch.zeros(self.A_pan.img['ngroups'] * self.m, **dev)
-        self.work = torch.zeros(L.bsls_lsq_workspace_size(self.m, self.A_pan.img['npanels']),
+        self.rpart = torch.zeros(groups * self.m, **dev)
+        self.work = torch.zeros(L.bsls_lsq_workspace_size(self.m, npanels),
                                 dtype=torch.uint8, device='cuda')
         op = _native.LsqOp()
         op.m, op.n = self.m, self.n
-        op.A, op.AT = self.A_pan.struct, self.AT_pan.struct
+        if self.A_pan is not None:
+            op.A = self.A_pan.struct
+        else:
+            op.At = self.A_til.struct
+        op.AT = self.AT_pan.struct
         op.colv = ptr(self.colv)
         op.rpart = self.rpart.data_ptr()
         op.xs = ptr(self.xs)
@@ -617,11 +634,12 @@ class DeviceLSQ:
         return out
 
 
-def lsq_operator(A, AT=None, general=False):
-    """DeviceLSQ on the panel images, or None (the caller keeps the general CSR
-    kernels) when the panel format cannot hold the matrix (dense rows)."""
+def lsq_operator(A, AT=None, general=False, k1=None):
+    """DeviceLSQ (residual walk `k1`: 'panels' or 'tiles', see DeviceLSQ), or
+    None (the caller keeps the general CSR kernels) when the panel format
+    cannot hold the matrix (dense rows)."""
     try:
-        return DeviceLSQ(A, AT, general=general)
+        return DeviceLSQ(A, AT, general=general, k1=k1)
     except PanelOverflow:
         return None
 

@@ -10,6 +10,8 @@ normalisation, ||x_new - x||_inf and the stopping test.  Lf = sigma_max(A) from 
 driving device matvecs.  The reference's ragged np.array at :10-11 (which
 NumPy >= 1.24 rejects) is not reproduced: blocks of any sizes work.
 """
+import os
+
 import numpy as np
 import scipy.sparse as sps
 import scipy.sparse.linalg as sla
@@ -44,9 +46,13 @@ def pack_blocks(sizes):
 
 
 class MirrorDescent:
-    """Device state of mirror_descent.least_squares: A (panel images from 2^20
-    nonzeros up -- `panels` overrides -- else CSR), b, the block starts, x, and
-    Lf = sigma_max(A) from ARPACK driving device mat-vecs."""
+    """Device state of mirror_descent.least_squares: A (the x-space operator
+    from 2^20 nonzeros up -- `panels` overrides -- else CSR), b, the block
+    starts, x, and Lf = sigma_max(A) from ARPACK driving device mat-vecs.
+    The operator's residual walks the dealt tile image (BSLS_LSQ_K1 overrides):
+    the loop's only test is ||x_new - x||_inf < tolerance (mirror_descent.py:
+    50), which never asks f to repeat bit for bit, so the faster walk with
+    LDS atomic row sums is safe here (BATCH's solvers keep the panels)."""
 
     def __init__(self, A, b, blocks, panels=None):
         import torch
@@ -62,7 +68,8 @@ class MirrorDescent:
         self.Ad, self.ATd = DeviceCSR(A), DeviceCSR(AT)
         if panels is None:
             panels = A.nnz >= (1 << 20)
-        self.lsq = lsq_operator(A, AT) if panels else None
+        self.lsq = (lsq_operator(A, AT, k1=os.environ.get('BSLS_LSQ_K1', 'tiles'))
+                    if panels else None)
         self.starts = torch.from_numpy(
             np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)).cuda()
         bd = torch.from_numpy(np.asarray(b, dtype=np.float64).ravel()).cuda()

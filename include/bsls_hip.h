@@ -447,6 +447,10 @@ typedef struct bsls_lsq_op {
     double *xs;                     /* n scratch (scaled only) */
     void *work;                     /* bsls_lsq_workspace_size() bytes, zeroed once */
     size_t work_bytes;
+    /* Optional dealt tile image of A (layout 1 / 2, halo 0): when At.ent is set
+     * the residual walks it instead of the A panels (LDS atomic row sums, the
+     * z-space K1's walk; rpart then holds At.ngroups x m) and op->A is unused. */
+    bsls_tiles At;
 } bsls_lsq_op;
 
 size_t bsls_lsq_workspace_size(int64_t m, int64_t A_npanels);
