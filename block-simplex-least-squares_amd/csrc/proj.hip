@@ -15,7 +15,9 @@
 //                registers with a flip-bitonic network pruned at compile time
 //                to the wave's largest block, runs the S_i chain (division-
 //                free test, the reference's division only within ulps) and
-//                writes back through LDS -- all straight-line code;
+//                writes back through LDS -- all straight-line code; two such
+//                waves per workgroup, the second loading once the first's
+//                loads have landed (lds_group);
 //   64 < k <= 8192   one WORKGROUP per block: LDS bitonic sort, S_i by one
 //                thread into LDS, conditions + last-index search in parallel;
 //   k > 8192     one workgroup, sort in a global workspace (rare: the
@@ -352,22 +354,32 @@ __device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int 
     }
 }
 
-// (64, 2): at most 256 VGPRs so two waves fit per SIMD -- the whole C2 grid
-// (~6 waves per CU) is then resident at once.
-template <bool BALL>
-__global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
-                                                      const int64_t *__restrict__ starts,
-                                                      int64_t nb, int64_t n,
-                                                      int64_t *__restrict__ big_list,
-                                                      unsigned *__restrict__ big_count,
-                                                      int allow_big,
-                                                      const double *__restrict__ gate) {
-    __shared__ __attribute__((aligned(16))) double buf[PBUF];
-    // gated launch (the x-space BB engine, xbb.hip): run only when *gate == 1
-    // (its STEP mode); the big-block kernels then find an empty list too
-    if (gate && *gate != 1.0) return;
-    const int lane = threadIdx.x;
-    const int64_t b0 = (int64_t)blockIdx.x * WAVE;
+// One wave's group of 64 consecutive blocks (one lane each), staged in its
+// own LDS buffer.  W > 1 (proj_lds_kernel<BALL, W>, W waves per workgroup):
+// wave w issues its range's loads only once wave w - 1's have landed
+// (`landed`, an LDS counter), so the waves of a CU pass through the load /
+// sort / store phases staggered instead of all together -- wave w's loads
+// stream while wave w - 1 sorts.  Every wave bumps the counter exactly once,
+// whatever path it takes, so no wave waits forever.
+template <bool BALL, int W>
+__device__ __forceinline__ void lds_group(double *__restrict__ y,
+                                          const int64_t *__restrict__ starts, int64_t nb,
+                                          int64_t n, int64_t *__restrict__ big_list,
+                                          unsigned *__restrict__ big_count, int allow_big,
+                                          double *buf, int *landed, int64_t grp, int wv,
+                                          int lane) {
+    auto wait_turn = [&]() {
+        if constexpr (W > 1) {
+            if (wv > 0)
+                while (__atomic_load_n(landed, __ATOMIC_RELAXED) < wv) __builtin_amdgcn_s_sleep(1);
+        }
+    };
+    auto pass_turn = [&]() {
+        if constexpr (W > 1) {
+            if (lane == 0) __atomic_store_n(landed, wv + 1, __ATOMIC_RELAXED);
+        }
+    };
+    const int64_t b0 = grp * WAVE;
     const int64_t b = b0 + lane;
     int k = 0;
     int64_t s = 0, e = 0;
@@ -385,12 +397,18 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
         }
     }
     const int kmax = wave_max(k);
-    if (kmax == 0) return;
+    if (kmax == 0) {
+        wait_turn();
+        pass_turn();
+        return;
+    }
     const int lastl = (int)((nb - b0 < WAVE ? nb - b0 : WAVE) - 1);
     const int64_t s0 = uni64(s, 0);
     const int64_t e1 = uni64(e, lastl);
     const int64_t total = e1 - s0;
     if (total > PCAP) {
+        wait_turn();
+        pass_turn();
         if (kmax <= 8) lane_block<8, BALL>(y, s, k);
         else if (kmax <= 16) lane_block<16, BALL>(y, s, k);
         else if (kmax <= 32) lane_block<32, BALL>(y, s, k);
@@ -404,6 +422,7 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
     const double *src = y + s0;
     const int sh = (int)(((uintptr_t)src >> 3) & 1);
     const int npair = (tot - sh) >> 1;
+    wait_turn();
     {
         const char *gs = (const char *)(src + sh);
         char *ls = (char *)(buf + 2 * sh);
@@ -420,7 +439,14 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (W == 1) {
+        __syncthreads();
+    } else {
+        // the wave reads only its own buffer: its DMA writes are complete at
+        // vmcnt(0), and its own LDS accesses execute in order
+        pass_turn();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     const int off = (k > 0) ? (int)(s - s0) + sh : 0;
     if (kmax <= 8) lane_block_lds<8, 8, BALL>(buf, off, k, lane);
     else if (kmax <= 16) lane_block_lds<16, 16, BALL>(buf, off, k, lane);
@@ -429,7 +455,8 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
     else if (kmax <= 48) lane_block_lds<64, 48, BALL>(buf, off, k, lane);
     else if (kmax <= 56) lane_block_lds<64, 56, BALL>(buf, off, k, lane);
     else lane_block_lds<64, 64, BALL>(buf, off, k, lane);
-    __syncthreads();
+    if constexpr (W == 1) __syncthreads();
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // out: 16-B write-through (sc1) stores of the aligned pairs -- the bytes
     // leave L2 while other waves still compute, instead of as dirty lines at
     // the kernel's end (measured -2.8 us at C2) -- and the unaligned head /
@@ -458,6 +485,31 @@ __global__ __launch_bounds__(64, 2) void proj_lds_kernel(double *__restrict__ y,
         if (sh) y[s0] = buf[1];
         if ((tot - sh) & 1) y[s0 + tot - 1] = buf[sh + tot - 1];
     }
+}
+
+// (64 W, 2): at most 256 VGPRs so two waves fit per SIMD -- the whole C2 grid
+// (~6 waves per CU) is then resident at once.
+template <bool BALL, int W>
+__global__ __launch_bounds__(64 * W, 2) void proj_lds_kernel(double *__restrict__ y,
+                                                          const int64_t *__restrict__ starts,
+                                                          int64_t nb, int64_t n,
+                                                          int64_t *__restrict__ big_list,
+                                                          unsigned *__restrict__ big_count,
+                                                          int allow_big,
+                                                          const double *__restrict__ gate) {
+    __shared__ __attribute__((aligned(16))) double buf[W][PBUF];
+    __shared__ int landed;
+    // gated launch (the x-space BB engine, xbb.hip): run only when *gate == 1
+    // (its STEP mode); the big-block kernels then find an empty list too
+    if (gate && *gate != 1.0) return;
+    const int wv = (W == 1) ? 0 : (int)(threadIdx.x / WAVE);
+    const int lane = (W == 1) ? (int)threadIdx.x : (int)(threadIdx.x % WAVE);
+    if constexpr (W > 1) {
+        if (threadIdx.x == 0) landed = 0;
+        __syncthreads();
+    }
+    lds_group<BALL, W>(y, starts, nb, n, big_list, big_count, allow_big, buf[wv], &landed,
+                       (int64_t)blockIdx.x * W + wv, wv, lane);
 }
 
 // In-place descending bitonic sort of u[0..P) by the whole workgroup
@@ -709,8 +761,24 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
     // (max_block is the caller's bound on every block length, like the
     // workspace size derived from it): otherwise no reset launch at all
     if (max_block > SMALL_MAX) BSLS_CHECK(hipMemsetAsync(w.count, 0, 16, st));
-    proj_lds_kernel<BALL><<<grid_for(nb, WAVE), WAVE, 0, st>>>(y, starts, nb, n, w.list, w.count,
-                                                                  max_block > SMALL_MAX, gate);
+    // waves per workgroup (BSLS_PROJ_WAVES, A/B): 2, staggered, by default --
+    // C2 20.7 -> 20.2 us per launch (HBM-fed batch); 3 is slower (27.9 us:
+    // 60 KB of LDS per workgroup leave 512 slots for 521 workgroups, a tail)
+    static const int pw = [] {
+        const char *e = getenv("BSLS_PROJ_WAVES");
+        const int v = e ? atoi(e) : 2;
+        return (v == 1 || v == 3) ? v : 2;
+    }();
+    const int64_t ngrp = (nb + WAVE - 1) / WAVE;
+    if (pw == 3)
+        proj_lds_kernel<BALL, 3><<<(unsigned)((ngrp + 2) / 3), 3 * WAVE, 0, st>>>(
+            y, starts, nb, n, w.list, w.count, max_block > SMALL_MAX, gate);
+    else if (pw == 2)
+        proj_lds_kernel<BALL, 2><<<(unsigned)((ngrp + 1) / 2), 2 * WAVE, 0, st>>>(
+            y, starts, nb, n, w.list, w.count, max_block > SMALL_MAX, gate);
+    else
+        proj_lds_kernel<BALL, 1><<<grid_for(nb, WAVE), WAVE, 0, st>>>(
+            y, starts, nb, n, w.list, w.count, max_block > SMALL_MAX, gate);
     BSLS_LAUNCH_CHECK();
     if (max_block > SMALL_MAX) {
         int64_t nbig = nb < (n / (SMALL_MAX + 1) + 1) ? nb : (n / (SMALL_MAX + 1) + 1);
