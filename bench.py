@@ -426,8 +426,10 @@ def bench_dore(sh, b, iters=30):
     from ARPACK over the same operators, not timed -- proj = PAVA v1 + clip
     by K3).  `iters` iterations after 3 untimed ones, eps < 0 so the
     norm-change exit never fires.  Roofline: the algorithmic bytes of the
-    kernels an iteration launches (3 K1 general-CSR passes, 1 K2, 2
-    projections at 16 n_z + 4 (p+1) each) over the wall time; the
+    kernels an iteration launches (2 K1 general-CSR passes -- the reference's
+    third, linop(x) of the last x_select, is the Ax the previous iteration
+    formed -- 1 K2, 2 projections at 16 n_z + 4 (p+1) each) over the wall
+    time; the
     host-decided closure loop (DORE.solve) is timed beside it."""
     import torch
     import DORE
@@ -453,7 +455,9 @@ def bench_dore(sh, b, iters=30):
                tgt, proj=eng.proj, log=log, options={'max_iter': 10, 'opt_tol': -1.0})
     torch.cuda.synchronize()
     host_us = (time.perf_counter() - t1) * 1e6 / 10
-    calls = {'A': 3 * iters, 'AT': iters, 'proj': 2 * iters}
+    # linop(x) at the top of an iteration reuses the last x_select's Ax from
+    # iteration 1 on (csrc/bb.hip dore_top): 2 K1 per iteration + 1
+    calls = {'A': 2 * iters + 1, 'AT': iters, 'proj': 2 * iters}
     m, n, nz, p, nnz = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
     kb = kernel_bytes(m, n, nz, p, nnz, nnz)
     byt = (calls['A'] * kb['K1_spmv_A'] + calls['AT'] * kb['K2_spmvT_Nt_dots']

@@ -1088,11 +1088,16 @@ static int check_problem(const bsls_bb_problem *p) {
 // roundings; dot products as fixed-order block sums; every branch decided by
 // the last block of a reduction and read by the kernels after it.
 
-// Ax = scale * r (DORE's linop), err = b - Ax; norm_change = ||x - x_prev||^2
-// (la.norm(.)**2: the square of the rooted sum) and the break test
+// Ax = linop(x), err = b - Ax; norm_change = ||x - x_prev||^2 (la.norm(.)**2:
+// the square of the rooted sum) and the break test.  Ax is scale * r of this
+// launch's K1 at iteration 0 (axs == nullptr); after that x is the previous
+// iteration's x_select, whose linop the previous iteration already formed
+// (axs: its Ax, = scale * r of K1 on the same x -- the reference recomputes
+// it at DORE.py:33, here it is reused, one K1 and one z2x fewer per iteration)
 __global__ __launch_bounds__(256) void dore_top(bsls_bb_problem P, bsls_dore_state D, int64_t it,
                                                 const double *__restrict__ x,
-                                                const double *__restrict__ xp) {
+                                                const double *__restrict__ xp,
+                                                const double *__restrict__ axs) {
     __shared__ double red[4];
     if (D.S[BSLS_S_STOP] != 0.0) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1102,7 +1107,7 @@ __global__ __launch_bounds__(256) void dore_top(bsls_bb_problem P, bsls_dore_sta
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t gs = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = i0; i < P.m; i += gs) {
-        const double ax = P.r[i] * D.scale;
+        const double ax = axs ? axs[i] : P.r[i] * D.scale;
         D.err[i] = D.b[i] - ax;
     }
     double v[1] = {0.0};
@@ -1264,10 +1269,18 @@ extern "C" int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state
     for (int64_t i = first_iter; i < first_iter + count; ++i) {
         double *x = d->X[i % 3], *xp = d->X[(i + 2) % 3], *xn = d->X[(i + 1) % 3];
         double *axo = d->AX[i % 3], *axp = d->AX[(i + 2) % 3], *axpp = d->AX[(i + 1) % 3];
-        // Ax = linop(x), err, norm_change (DORE.py:31-37)
-        bb_z2x<<<grid_for(p->n, 256), 256, 0, st>>>(PS, x);
-        launch_k1<false, false, true>(PS, i, w, st);
-        dore_top<<<gb, 256, 0, st>>>(PS, D, i, x, xp);
+        // Ax = linop(x), err, norm_change (DORE.py:31-37); from iteration 1 on
+        // x is the last x_select and Ax its linop, kept in axp (dore_top)
+        static const bool recompute = [] {   // BSLS_DORE_RECOMPUTE=1: the reference's K1 (A/B)
+            const char *e = getenv("BSLS_DORE_RECOMPUTE");
+            return e && e[0] == '1';
+        }();
+        const bool top_k1 = i == 0 || recompute;
+        if (top_k1) {
+            bb_z2x<<<grid_for(p->n, 256), 256, 0, st>>>(PS, x);
+            launch_k1<false, false, true>(PS, i, w, st);
+        }
+        dore_top<<<gb, 256, 0, st>>>(PS, D, i, x, xp, top_k1 ? nullptr : axp);
         // x_new = proj(x + linop_T(err)) (DORE.py:38-40; K3 with t = -scale)
         launch_k2<false>(PE, nullptr, p->g[0], w, st);
         launch_k3(PS, i, x, p->g[0], xn, w, st);
