@@ -390,11 +390,21 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     double rr[1] = {0.0};
     if constexpr (FUSE) {
         if (ITER) {
+            // the slice's loads RR at a time, all in flight (a load-then-add
+            // loop waited out one memory latency per element, at the start of
+            // every workgroup); same left-to-right order, padding adds +0
+            constexpr int RR = 4;
             const int64_t ns = T.nrb * G, sl = rb * G + g;
             const int64_t q0 = sl * P.m / ns, q1 = (sl + 1) * P.m / ns;
-            for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
-                const double v = P.r[i];
-                rr[0] += v * v;
+            for (int64_t i0 = q0 + threadIdx.x; i0 < q1; i0 += RR * (int64_t)blockDim.x) {
+                double v[RR];
+#pragma unroll
+                for (int q = 0; q < RR; ++q) {
+                    const int64_t i = i0 + (int64_t)q * blockDim.x;
+                    v[q] = (i < q1) ? P.r[i] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < RR; ++q) rr[0] += v[q] * v[q];
             }
         }
     }
