@@ -255,9 +255,14 @@ __global__ __launch_bounds__(1024) void md_pack_kernel(double *__restrict__ x,
                                                       double *__restrict__ state, double tol,
                                                       int64_t iter) {
     __shared__ double red[MD_PACK_WAVES];
+    __shared__ double c2lk[WAVE + 1];   // sqrt(2 log k), k = 1 .. 64: blocks of a packed wave
     if (state[0] != 0.0) return;
     const int l = threadIdx.x % WAVE, wv = threadIdx.x / WAVE;
     const int64_t pk = (int64_t)blockIdx.x * MD_PACK_WAVES + wv;
+    // one log and one sqrt per size class and workgroup instead of per entry
+    // (they were ~60 of the ~150 VALU instructions an entry cost)
+    if (threadIdx.x < WAVE) c2lk[threadIdx.x + 1] = sqrt(2.0 * log((double)(threadIdx.x + 1)));
+    __syncthreads();
     double dmax = 0.0;
     if (pk < npacks) {
         const int64_t x0 = pk_x0[pk];
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(1024) void md_pack_kernel(double *__restrict__ x,
             const int en = (above ? (__ffsll((long long)above) - 1) : L) - 1;   // its last entry
             const double xo = act ? x[x0 + l] : 0.0;
             const double gv = act ? g[x0 + l] : 0.0;
-            const double t = sqrt(2.0 * log((double)(en - st + 1))) / scale;
+            const double t = c2lk[en - st + 1] / scale;
             const double v = act ? xo * exp(-(gv * t)) : 0.0;
             // segmented inclusive scan (segments = blocks)
             double acc = v;
