@@ -500,7 +500,7 @@ def bench_md(sh, b, iters=30):
     # 4 (p+1)
     byt = 24 * nnz + 4 * (m + n + 2) + 24 * m + 16 * n + 24 * n + 4 * (p + 1)
     us = ms * 1e3 / iters
-    op = ('residual %s, gradient panels' % md.lsq.k1) if md.lsq is not None else 'csr'
+    op = ('residual %s, gradient %s' % (md.lsq.k1, md.lsq.k2)) if md.lsq is not None else 'csr'
     return {'operator': op, 'scale': 0.01,
             'iterations': iters,
             'us_per_iter': us, 'iterations_per_s': iters / (ms * 1e-3),

@@ -197,11 +197,43 @@ static void lsq_allow_lds(K kernel) {
     }
 }
 
+// one dealt image of A' (layout 1 / 2, one group, halo 0): tile rb sums the
+// entries of each of its rows in LDS (atomic adds: the sums to rounding, not
+// SciPy's order) and writes g = colv_i * sum (scaled incidence, MODE 0) or
+// the sum (values stored, MODE 1) -- the z-space K2's walk without its N'
+// epilogue
+template <int MODE>
+__global__ __launch_bounds__(1024) void lsq_k2t(bsls_tiles T, int64_t n,
+                                                const double *__restrict__ r,
+                                                const double *__restrict__ colv,
+                                                double *__restrict__ g) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    int64_t rb, gg;
+    tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, gg);
+    const int HR = (int)tile_lds_doubles(T, false);
+    for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;
+    __syncthreads();
+    tile_walk_any<MODE>(T, rb, gg, r, lds, nullptr);
+    __syncthreads();
+    const int64_t r0 = rb * T.H, r1 = (r0 + T.H < n) ? r0 + T.H : n;
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+        g[row] = (MODE == 0) ? colv[row] * lds[row - r0] : lds[row - r0];
+}
+
 static bool lsq_ok(const bsls_lsq_op *op) {
     if (!op || op->m <= 0 || op->n <= 0) return false;
     const bsls_panels &A = op->A, &T = op->AT;
-    if (T.rows != op->n || T.cols != op->m || T.halo != 0 || T.ngroups != 1) return false;
-    if (T.prow < 1 || T.prow > BSLS_PANEL_ROWS) return false;
+    if (op->ATt.ent) {
+        const bsls_tiles &K = op->ATt;
+        if (K.rows != op->n || K.cols != op->m || K.halo != 0 || K.ngroups != 1 ||
+            K.nrb < 1 || !K.group_col || !K.wave_off || (K.layout & 3) == 0 || !K.base)
+            return false;
+        if ((op->colv == nullptr) != (K.val != nullptr)) return false;
+        if (tile_lds_doubles(K, false) * 8 > (size_t)LSQ_LDS_MAX) return false;
+    } else {
+        if (T.rows != op->n || T.cols != op->m || T.halo != 0 || T.ngroups != 1) return false;
+        if (T.prow < 1 || T.prow > BSLS_PANEL_ROWS) return false;
+    }
     if (op->At.ent) {
         const bsls_tiles &K = op->At;
         if (K.rows != op->m || K.cols != op->n || K.halo != 0 || K.ngroups < 1 ||
@@ -214,7 +246,8 @@ static bool lsq_ok(const bsls_lsq_op *op) {
         if (A.prow < 1 || A.prow > BSLS_PANEL_ROWS) return false;
     }
     if (!op->rpart || !op->work) return false;
-    if (op->colv ? (!op->xs || T.val) : !T.val) return false;
+    if (op->colv && !op->xs) return false;
+    if (!op->ATt.ent && (op->colv ? T.val != nullptr : !T.val)) return false;
     if (!op->At.ent && (op->colv ? A.val != nullptr : !A.val)) return false;
     return true;
 }
@@ -285,6 +318,19 @@ extern "C" int bsls_lsq_gradient(const bsls_lsq_op *op, const double *d_r, doubl
                                  void *stream) {
     if (!lsq_ok(op) || !d_r || !d_g) return BSLS_E_ARG;
     hipStream_t st = (hipStream_t)stream;
+    if (op->ATt.ent) {
+        const bsls_tiles &K = op->ATt;
+        const size_t lds = tile_lds_doubles(K, false) * 8;
+        if (op->colv) {
+            lsq_allow_lds(lsq_k2t<0>);
+            lsq_k2t<0><<<(int)K.nrb, BSLS_TILE_THREADS, lds, st>>>(K, op->n, d_r, op->colv, d_g);
+        } else {
+            lsq_allow_lds(lsq_k2t<1>);
+            lsq_k2t<1><<<(int)K.nrb, BSLS_TILE_THREADS, lds, st>>>(K, op->n, d_r, nullptr, d_g);
+        }
+        BSLS_LAUNCH_CHECK();
+        return BSLS_OK;
+    }
     const int grid = grid_for(op->AT.npanels, PANEL_WAVES);
     if (op->colv) {
         lsq_allow_lds(lsq_k2<2>);

@@ -581,10 +581,12 @@ class DeviceLSQ:
     BSLS_LSQ_K1=tiles) walks a dealt tile image of A instead (the z-space
     K1's walk: LDS atomic row sums, faster, the same sums to rounding only).
     A' is one group of panels (every row in CSR order: g bit-identical to
-    SciPy's csr_matvec).  A scaled incidence drops the values (colv * x formed
-    once per residual, A' entries scaled by colv row by row)."""
+    SciPy's csr_matvec); k2='tiles' (or BSLS_LSQ_K2=tiles) walks a dealt tile
+    image of A' instead (one group, LDS atomic row sums scaled by colv once per
+    row: the same sums to rounding).  A scaled incidence drops the values
+    (colv * x formed once per residual, A' entries scaled by colv row by row)."""
 
-    def __init__(self, A, AT=None, general=False, k1=None):
+    def __init__(self, A, AT=None, general=False, k1=None, k2=None):
         torch = _torch()
         L = _native.lib()
         A = sps.csr_matrix(A)
@@ -602,8 +604,20 @@ class DeviceLSQ:
             self.A_pan = DevicePanels(A, prow, False, groups, values=not self.scaled)
             groups, npanels = self.A_pan.img['ngroups'], self.A_pan.img['npanels']
         self.k1 = k1
-        self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), False, 1,
-                                   values=not self.scaled)
+        k2 = k2 or os.environ.get('BSLS_LSQ_K2', 'panels')
+        self.AT_pan = self.AT_til = None
+        if k2 == 'tiles':
+            # one group of row blocks as tall as the LDS holds, whole rounds of
+            # 256 workgroups (the z-space K2's plan)
+            hmax = _native.TILE_LDS_BYTES // 8 - 1
+            nrb = -(-max(256, -(-self.n // hmax)) // 256) * 256
+            # (a tile holds at least 64 rows: bsls_tiles_build_dealt3)
+            self.AT_til = DeviceTiles(AT, 0, values=not self.scaled,
+                                      plan=(max(64, -(-self.n // nrb)), 1, 0), layout=2)
+        else:
+            self.AT_pan = DevicePanels(AT, panel_rows(self.n, 256), False, 1,
+                                       values=not self.scaled)
+        self.k2 = k2
         dev = dict(dtype=torch.float64, device='cuda')
         self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
         self.xs = torch.empty(self.n, **dev) if self.scaled else None
@@ -616,7 +630,10 @@ class DeviceLSQ:
             op.A = self.A_pan.struct
         else:
             op.At = self.A_til.struct
-        op.AT = self.AT_pan.struct
+        if self.AT_pan is not None:
+            op.AT = self.AT_pan.struct
+        else:
+            op.ATt = self.AT_til.struct
         op.colv = ptr(self.colv)
         op.rpart = self.rpart.data_ptr()
         op.xs = ptr(self.xs)
@@ -634,12 +651,12 @@ class DeviceLSQ:
         return out
 
 
-def lsq_operator(A, AT=None, general=False, k1=None):
-    """DeviceLSQ (residual walk `k1`: 'panels' or 'tiles', see DeviceLSQ), or
-    None (the caller keeps the general CSR kernels) when the panel format
-    cannot hold the matrix (dense rows)."""
+def lsq_operator(A, AT=None, general=False, k1=None, k2=None):
+    """DeviceLSQ (residual walk `k1`, gradient walk `k2`: 'panels' or 'tiles',
+    see DeviceLSQ), or None (the caller keeps the general CSR kernels) when the
+    panel format cannot hold the matrix (dense rows)."""
     try:
-        return DeviceLSQ(A, AT, general=general, k1=k1)
+        return DeviceLSQ(A, AT, general=general, k1=k1, k2=k2)
     except PanelOverflow:
         return None
 

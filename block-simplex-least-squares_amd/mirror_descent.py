@@ -49,10 +49,11 @@ class MirrorDescent:
     """Device state of mirror_descent.least_squares: A (the x-space operator
     from 2^20 nonzeros up -- `panels` overrides -- else CSR), b, the block
     starts, x, and Lf = sigma_max(A) from ARPACK driving device mat-vecs.
-    The operator's residual walks the dealt tile image (BSLS_LSQ_K1 overrides):
-    the loop's only test is ||x_new - x||_inf < tolerance (mirror_descent.py:
-    50), which never asks f to repeat bit for bit, so the faster walk with
-    LDS atomic row sums is safe here (BATCH's solvers keep the panels)."""
+    The operator's residual and gradient walk dealt tile images (BSLS_LSQ_K1 /
+    BSLS_LSQ_K2 override): the loop's only test is ||x_new - x||_inf <
+    tolerance (mirror_descent.py:50), which never asks f or g to repeat bit for
+    bit, so the faster walks with LDS atomic row sums are safe here (BATCH's
+    solvers keep the panels)."""
 
     def __init__(self, A, b, blocks, panels=None):
         import torch
@@ -68,7 +69,8 @@ class MirrorDescent:
         self.Ad, self.ATd = DeviceCSR(A), DeviceCSR(AT)
         if panels is None:
             panels = A.nnz >= (1 << 20)
-        self.lsq = (lsq_operator(A, AT, k1=os.environ.get('BSLS_LSQ_K1', 'tiles'))
+        self.lsq = (lsq_operator(A, AT, k1=os.environ.get('BSLS_LSQ_K1', 'tiles'),
+                                 k2=os.environ.get('BSLS_LSQ_K2', 'tiles'))
                     if panels else None)
         self.starts = torch.from_numpy(
             np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)).cuda()

@@ -451,6 +451,11 @@ typedef struct bsls_lsq_op {
      * the residual walks it instead of the A panels (LDS atomic row sums, the
      * z-space K1's walk; rpart then holds At.ngroups x m) and op->A is unused. */
     bsls_tiles At;
+    /* Optional dealt tile image of A' (layout 1 / 2, one group, halo 0): when
+     * ATt.ent is set the gradient walks it instead of the AT panels (LDS
+     * atomic row sums scaled by colv once per row: g to rounding, not SciPy's
+     * order; mirror descent) and op->AT is unused. */
+    bsls_tiles ATt;
 } bsls_lsq_op;
 
 size_t bsls_lsq_workspace_size(int64_t m, int64_t A_npanels);

@@ -34,8 +34,8 @@ def _scaled(m, n, per_col, rs):
 @pytest.mark.parametrize('m,n,per_col', [(1000, 9001, 5), (37, 300, 3), (20000, 150000, 12),
                                          (4096, 64, 40)])
 @pytest.mark.parametrize('scaled', [True, False])
-@pytest.mark.parametrize('k1', ['tiles', 'panels'])
-def test_lsq_operator(cuda, m, n, per_col, scaled, k1):
+@pytest.mark.parametrize('k1,k2', [('tiles', 'panels'), ('panels', 'panels'), ('tiles', 'tiles')])
+def test_lsq_operator(cuda, m, n, per_col, scaled, k1, k2):
     import torch
     from device import DeviceLSQ, panels_matvec
     rs = np.random.RandomState(SEED + m)
@@ -47,8 +47,8 @@ def test_lsq_operator(cuda, m, n, per_col, scaled, k1):
                        sps.diags((rs.rand(n) > 0.05).astype(float)))
     A.eliminate_zeros()
     AT = A.T.tocsr()
-    op = DeviceLSQ(A, AT, general=not scaled, k1=k1)
-    assert op.scaled == scaled and op.k1 == k1
+    op = DeviceLSQ(A, AT, general=not scaled, k1=k1, k2=k2)
+    assert op.scaled == scaled and op.k1 == k1 and op.k2 == k2
     x = rs.randn(n)
     add = rs.randn(m)
     xd, ad = torch.from_numpy(x).cuda(), torch.from_numpy(add).cuda()
@@ -73,7 +73,13 @@ def test_lsq_operator(cuda, m, n, per_col, scaled, k1):
                                atol=1e-12 * np.abs(ref).max())
     g = torch.empty(n, dtype=torch.float64, device='cuda')
     op.gradient(r, g)
-    assert exact(g.cpu().numpy(), AT.dot(rh))
+    gref = AT.dot(rh)
+    if k2 == 'panels':
+        assert exact(g.cpu().numpy(), gref)
+    else:
+        # dealt tiles: LDS atomic row sums (scaled: colv times the row's sum)
+        np.testing.assert_allclose(g.cpu().numpy(), gref, rtol=1e-12,
+                                   atol=1e-12 * max(np.abs(gref).max(), 1.0))
     # repeated calls (tickets re-armed): bit for bit on the panels, to
     # rounding on the dealt tiles
     r3 = torch.empty(m, dtype=torch.float64, device='cuda')

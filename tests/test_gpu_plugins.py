@@ -286,7 +286,7 @@ def test_lbfgs_60_iterations_vs_reference(cuda, golden):
     assert rel(states[-1], G['gd_states'][-1]) < 1e-6
 
 
-@pytest.mark.parametrize('m,pushes', [(1, 3), (5, 3), (5, 12), (50, 70), (64, 66), (70, 75)])
+@pytest.mark.parametrize('m,pushes', [(1, 3), (5, 3), (5, 12), (50, 70), (64, 66), (70, 75), (100, 103)])
 def test_lbfgs_device_history_direction(cuda, m, pushes):
     """_DeviceHistory.direction / push (csrc/lbfgs.hip: multi-dot, one-wave
     recursion on the Gram matrices, combine) against the reference's vector
