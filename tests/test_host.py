@@ -372,3 +372,31 @@ def test_tile_images_restate_scipy(layout, halo, values):
         live = int(np.sum((e >> cb) != H + halo))
         extra = sum(int(A.indptr[r + 1] - A.indptr[r]) for r in range(H, m, H)) if halo else 0
         assert live == A.nnz + extra
+
+
+def test_iso_plan_cache_by_content(monkeypatch):
+    """device.iso_plan's cache (the pack plan of a block layout, made once):
+    a fresh array with the same starts finds the cached plan, other starts or
+    another length make a new one, and changing the caller's array in place
+    after caching does not alias the cached entry (the cache keeps a copy)."""
+    import device
+    made = []
+
+    class Stub:
+        def __init__(self, st, n):
+            made.append((st.copy(), n))
+    monkeypatch.setattr(device, 'IsoPlan', Stub)
+    monkeypatch.setattr(device, '_iso_plans', {})
+    a = np.array([0, 3, 7, 12], dtype=np.int64)
+    p1 = device.iso_plan(a, 20)
+    assert device.iso_plan(a.copy(), 20) is p1
+    assert device.iso_plan(list(a), 20) is p1            # converted, same content
+    p2 = device.iso_plan(a, 21)                         # another length
+    b = a.copy()
+    b[2] = 8
+    p3 = device.iso_plan(b, 20)                         # other starts, same count
+    assert len({id(p1), id(p2), id(p3)}) == 3 and len(made) == 3
+    a[1] = 4                                            # the caller mutates its array
+    p4 = device.iso_plan(a, 20)
+    assert p4 is not p1 and len(made) == 4
+    assert device.iso_plan(np.array([0, 3, 7, 12]), 20) is p1
