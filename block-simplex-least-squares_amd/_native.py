@@ -128,6 +128,8 @@ _SIGS = {
     'bsls_proj_workspace_size': (_sz, [_i64, _i64, _i64]),
     'bsls_proj_multi_simplex': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
     'bsls_proj_multi_ball': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
+    'bsls_proj_multi_simplex_fast': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
+    'bsls_proj_multi_ball_fast': (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
     'bsls_isotonic_workspace_size': (_sz, [_i64]),
     'bsls_isotonic_multi': (_int, [_int, _vp, _vp, _i64, _i64, _vp, _int, _i64, _vp, _sz, _vp,
                                    _vp]),

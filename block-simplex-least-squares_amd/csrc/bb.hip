@@ -529,7 +529,13 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
                                : last_of_sum<NS>(sums, part, (unsigned)rb, (unsigned)T.nrb, ticket,
                                                  tot, red);
     if (last && threadIdx.x == 0) {
-        if constexpr (FUSE) bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
+        if constexpr (FUSE) {
+            bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
+            // stopped at iter - 1: keep that iteration's sums (what the
+            // unfused schedule leaves in scal); g[iter & 1], written above,
+            // is the other buffer -- the stopping iterate's g is untouched
+            if (P.scal[BSLS_S_STOP] != 0.0) return;
+        }
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
@@ -656,7 +662,10 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
     block_sum<NS>(sums, lds);
     double tot[NS];
     if (last_block_sum<NS>(sums, part, ticket, tot, lds) && threadIdx.x == 0) {
-        if constexpr (FUSE) bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
+        if constexpr (FUSE) {
+            bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
+            if (P.scal[BSLS_S_STOP] != 0.0) return;   // as bb_k2t
+        }
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
@@ -1048,21 +1057,6 @@ static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t 
     return need_val ? M.val != nullptr : true;
 }
 
-static bool tiles_ok(const bsls_tiles &T, int64_t rows, int64_t cols, int64_t halo,
-                     bool need_val, bool colv_lds) {
-    if (T.rows != rows || T.cols != cols || T.halo != halo || T.H < 64) return false;
-    if (T.nrb != (rows + T.H - 1) / T.H || T.ngroups < 1 || T.nquads < 0) return false;
-    if (T.order != 0 && !(T.order == 1 && T.ngroups % 8 == 0)) return false;
-    if (tile_lds_doubles(T, colv_lds) * 8 > (size_t)PANEL_LDS_MAX) return false;
-    if (!T.group_col || !T.wave_off || !T.ent) return false;
-    const int64_t lay = T.layout & ~(int64_t)(BSLS_TILE_NT | BSLS_TILE_VAL32 | BSLS_TILE_VAL16);
-    if (T.layout != 0 && !((lay == 1 || lay == 2) && T.base && T.H + T.halo < 65536))
-        return false;
-    if ((T.layout & BSLS_TILE_VAL32) && (T.layout & BSLS_TILE_VAL16)) return false;
-    if (lay == 2 && T.H + T.halo >= (1 << 18)) return false;   // >= 6 column bits
-    return need_val ? T.val != nullptr : true;
-}
-
 static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
     if (p->shard_role < 0 || p->shard_role > 2) return BSLS_E_ARG;
@@ -1070,14 +1064,14 @@ static int check_problem(const bsls_bb_problem *p) {
         return BSLS_E_ARG;
     const bool general = p->colv == nullptr;
     if (p->At.ent) {
-        if (!tiles_ok(p->At, p->m, p->n, 0, general, false)) return BSLS_E_ARG;
+        if (!tiles_valid(p->At, p->m, p->n, 0, general, false, PANEL_LDS_MAX)) return BSLS_E_ARG;
         if (p->At.ngroups > 1 && !p->rpart) return BSLS_E_ARG;
     } else if (!panels_ok(p->A, p->m, p->n, 0, general) || !p->rpart) {
         return BSLS_E_ARG;
     }
     if (p->ATt.ent) {
-        if (!tiles_ok(p->ATt, p->n, p->m, 1, general,
-                      !general && p->ATt.ngroups == 1 && p->ATt.layout == 0))
+        if (!tiles_valid(p->ATt, p->n, p->m, 1, general,
+                         !general && p->ATt.ngroups == 1 && p->ATt.layout == 0, PANEL_LDS_MAX))
             return BSLS_E_ARG;
         if (p->ATt.ngroups > 1 && !p->wpart) return BSLS_E_ARG;
     } else if (!panels_ok(p->AT, p->n, p->m, 1, general) || p->AT.ngroups != 1) {

@@ -225,22 +225,20 @@ static bool lsq_ok(const bsls_lsq_op *op) {
     const bsls_panels &A = op->A, &T = op->AT;
     if (op->ATt.ent) {
         const bsls_tiles &K = op->ATt;
-        if (K.rows != op->n || K.cols != op->m || K.halo != 0 || K.ngroups != 1 ||
-            K.nrb < 1 || !K.group_col || !K.wave_off || (K.layout & 3) == 0 || !K.base)
-            return false;
+        // the shared validator (bb.hip's) plus what lsq_k2t assumes: one group,
+        // a dealt layout, values iff the matrix is not a scaled incidence
+        if (!tiles_valid(K, op->n, op->m, 0, op->colv == nullptr, false, LSQ_LDS_MAX)) return false;
+        if (K.ngroups != 1 || (K.layout & 3) == 0) return false;
         if ((op->colv == nullptr) != (K.val != nullptr)) return false;
-        if (tile_lds_doubles(K, false) * 8 > (size_t)LSQ_LDS_MAX) return false;
     } else {
         if (T.rows != op->n || T.cols != op->m || T.halo != 0 || T.ngroups != 1) return false;
         if (T.prow < 1 || T.prow > BSLS_PANEL_ROWS) return false;
     }
     if (op->At.ent) {
         const bsls_tiles &K = op->At;
-        if (K.rows != op->m || K.cols != op->n || K.halo != 0 || K.ngroups < 1 ||
-            K.nrb < 1 || !K.group_col || !K.wave_off || (K.layout & 3) == 0 || !K.base)
-            return false;
+        if (!tiles_valid(K, op->m, op->n, 0, op->colv == nullptr, false, LSQ_LDS_MAX)) return false;
+        if ((K.layout & 3) == 0) return false;
         if ((op->colv == nullptr) != (K.val != nullptr)) return false;
-        if (tile_lds_doubles(K, false) * 8 > (size_t)LSQ_LDS_MAX) return false;
     } else {
         if (A.rows != op->m || A.cols != op->n || A.halo != 0 || A.ngroups < 1) return false;
         if (A.prow < 1 || A.prow > BSLS_PANEL_ROWS) return false;

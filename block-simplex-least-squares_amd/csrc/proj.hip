@@ -711,6 +711,200 @@ __global__ __launch_bounds__(HUGE_THREADS) void proj_huge_apply(
     }
 }
 
+// ---- sort-free path (bsls_proj_multi_*_fast: 1e-12 contract, not bit-identical) ----
+//
+// With tau = -lambda the reference's result solves sum_j max(y_j - tau, 0) = 1,
+// and for ANY subset A of the block tau >= (sum_A y - 1)/|A| (since
+// sum_A (y - tau) <= sum max(y - tau, 0) = 1), with equality at the
+// reference's top-(rho + 1) set.  Newton from the left on that convex,
+// piecewise-linear function: tau_0 = max - 1 (the set {max}),
+// A_{t+1} = {y in A_t : y > tau_t} (the max always stays),
+// tau_{t+1} = (sum_{A_{t+1}} y - 1)/|A_{t+1}|.  The sets only shrink and tau
+// never overshoots, so the first pass that removes nothing has the
+// reference's set: lambda = (1 - sum_A y)/|A|, the reference's expression at
+// rho = |A| - 1 (proj_simplex.h:27-31), its members summed in another order
+// (per lane, then a DPP tree) -- ulps of the sum, no sort, no S_i chain.
+// Passes (C2): 5 * N(0,1) blocks 1-2 (tau_0 is usually exact), U[0,1) ~5.
+// A set of one element (rho = 0) reproduces 1 - u_0 bit for bit.
+//
+// Lane mapping: LPB lanes per block, 64 / LPB consecutive blocks per wave;
+// lane (g, j) holds entries j, j + LPB, ... of block g in registers (EB
+// slots, the wave's bucket), so the reductions are DPP steps inside a quad /
+// half-row and a C2 wave (16 blocks) is ~4 KB of contiguous input: 6250 waves,
+// one resident round at <= 64 VGPRs.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    return __hiloint2double(dpp_i<CTRL>(__double2hiint(v)), dpp_i<CTRL>(__double2loint(v)));
+}
+// sum / max over the LPB lanes of a group (xor 1, xor 2 in the quad, then the
+// half-row mirror); every lane ends with the same bits (a + b == b + a)
+template <int LPB>
+__device__ __forceinline__ double grp_sum_d(double v) {
+    if constexpr (LPB >= 2) v += dpp_d<0xB1>(v);
+    if constexpr (LPB >= 4) v += dpp_d<0x4E>(v);
+    if constexpr (LPB >= 8) v += dpp_d<0x141>(v);
+    return v;
+}
+template <int LPB>
+__device__ __forceinline__ int grp_sum_i(int v) {
+    if constexpr (LPB >= 2) v += dpp_i<0xB1>(v);
+    if constexpr (LPB >= 4) v += dpp_i<0x4E>(v);
+    if constexpr (LPB >= 8) v += dpp_i<0x141>(v);
+    return v;
+}
+template <int LPB>
+__device__ __forceinline__ double grp_max_d(double v) {
+    double u;
+    if constexpr (LPB >= 2) { u = dpp_d<0xB1>(v); v = (u > v) ? u : v; }
+    if constexpr (LPB >= 4) { u = dpp_d<0x4E>(v); v = (u > v) ? u : v; }
+    if constexpr (LPB >= 8) { u = dpp_d<0x141>(v); v = (u > v) ? u : v; }
+    return v;
+}
+
+// the largest double below x (finite x)
+__device__ __forceinline__ double next_down(double x) {
+    const long long b = __double_as_longlong(x);
+    if (x == 0.0) return -4.9406564584124654e-324;
+    return __longlong_as_double(x > 0.0 ? b - 1 : b + 1);
+}
+
+template <int LPB, int EB, bool BALL>
+__device__ __forceinline__ void thr_solve(double *__restrict__ y, int64_t s, int64_t s0, int k,
+                                          int j, const __amdgpu_buffer_rsrc_t &rs) {
+    constexpr double PAD = -1.7976931348623157e308;   // below every entry, finite
+    const double *blk = y + (k > 0 ? s : 0);
+    const int off0 = (int)(s - s0) * 8;                 // byte offset of the block in rs
+    double v[EB];
+    // unconditional loads at clamped offsets: all EB in flight at once
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+        const int i = j + LPB * e;
+        const double t = blk[i < k ? i : 0];
+        v[e] = (i < k) ? t : PAD;
+    }
+    bool need = true;
+    if constexpr (BALL) {
+        // proj_simplex.h:56-64: clamp the negatives, project iff the rest sums > 1
+        double acc = 0.0;
+#pragma unroll
+        for (int e = 0; e < EB; ++e) {
+            const bool ok = j + LPB * e < k;
+            v[e] = (ok & (v[e] < 0.0)) ? 0.0 : v[e];
+            acc += ok ? v[e] : 0.0;
+        }
+        need = grp_sum_d<LPB>(acc) > 1.0;
+    }
+    double lam = 0.0;
+    if (!BALL || __builtin_amdgcn_ballot_w64(need && k > 0)) {
+        double M = v[0];
+#pragma unroll
+        for (int e = 1; e < EB; ++e) M = (v[e] > M) ? v[e] : M;
+        M = grp_max_d<LPB>(M);
+        // tau stays below the max (clamped to the next double down: only a
+        // |y| ~ 1e12+ rounding could reach it), so the max never leaves the set
+        const double Mdn = next_down(M);
+        double tau = fmin(M - 1.0, Mdn);
+        // active flags: padding never passes (PAD < tau of a live block)
+        bool a[EB];
+#pragma unroll
+        for (int e = 0; e < EB; ++e) a[e] = true;
+        double cprev = 1.0;   // tau_0 is the tau of the set {max}
+        double S = M, c = 1.0;
+        for (int pass = 0; pass <= LPB * EB; ++pass) {
+            double sl = 0.0, cl = 0.0;
+#pragma unroll
+            for (int e = 0; e < EB; ++e) {
+                // branch-free: the set only shrinks (& with the old flag); sum
+                // and count by a 0 / 1 factor (fma: one rounding, = the add;
+                // the count is exact in a double)
+                a[e] = a[e] & (v[e] > tau);
+                const double f = a[e] ? 1.0 : 0.0;
+                sl = __builtin_fma(f, v[e], sl);
+                cl += f;
+            }
+            S = grp_sum_d<LPB>(sl);
+            c = grp_sum_d<LPB>(cl);
+            const bool more = (k > 0) & need & (c != cprev);
+            cprev = c;
+            tau = fmin((S - 1.0) / c, Mdn);
+            if (!__builtin_amdgcn_ballot_w64(more)) break;
+        }
+        lam = (1. - S) / c;
+    }
+    // out through the wave's buffer resource: offsets of padding slots are
+    // past its end, so the hardware drops them (no per-slot branch)
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+        const int i = j + LPB * e;
+        const double r = need ? relu_ref(lam + v[e]) : v[e];
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, r), rs,
+            (i < k) ? off0 + 8 * i : 0x7FFFFFF0, 0, 0);
+    }
+}
+
+// One wave: blocks b0 .. b0 + 64/LPB - 1 (block ends from the same coalesced
+// read of starts); blocks > SMALL_MAX go to the big list as in lds_group.
+template <bool BALL, int LPB>
+__global__ __launch_bounds__(256) void proj_thr_kernel(double *__restrict__ y,
+                                                      const int64_t *__restrict__ starts,
+                                                      int64_t nb, int64_t n,
+                                                      int64_t *__restrict__ big_list,
+                                                      unsigned *__restrict__ big_count,
+                                                      int allow_big,
+                                                      const double *__restrict__ gate) {
+    static_assert(LPB == 2 || LPB == 4 || LPB == 8, "lanes per block");
+    constexpr int BPW = WAVE / LPB;
+    if (gate && *gate != 1.0) return;
+    const int lane = lane_id();
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    const int64_t b0 = wave * BPW;
+    if (b0 >= nb) return;
+    const int g = lane / LPB, j = lane % LPB;
+    long long st = (long long)n;
+    if (lane <= BPW && b0 + lane < nb) st = (long long)starts[b0 + lane];
+    const int64_t s = (int64_t)__shfl(st, g, WAVE);
+    const int64_t e = (int64_t)__shfl(st, g + 1, WAVE);
+    const int64_t b = b0 + g;
+    int k = 0;
+    if (b < nb) {
+        const int64_t kk = e - s;
+        if (kk > SMALL_MAX) {
+            if (allow_big && j == 0) {   // (a block > max_block breaks the contract: left as is)
+                const unsigned slot = atomicAdd(big_count, 1u);
+                big_list[slot] = b;
+            }
+        } else {
+            k = (int)kk;
+        }
+    }
+    const int kmax = wave_max(k);
+    if (kmax == 0) return;
+    // the wave's range [s0, e1): its first block's start to its last block's end
+    // (read into scalar registers: a buffer resource built from VGPRs becomes
+    // a waterfall loop around every store)
+    const int64_t s0 = uni64((int64_t)st, 0);
+    const int nbw = __builtin_amdgcn_readfirstlane((int)((nb - b0 < BPW) ? nb - b0 : BPW));
+    const int64_t e1 = uni64((int64_t)st, nbw);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(y + s0, 0, (int)((e1 - s0) * 8), 0x00020000);
+    const int E = (kmax + LPB - 1) / LPB;
+    if (E <= 4) thr_solve<LPB, 4, BALL>(y, s, s0, k, j, rs);
+    else if (E <= 8) thr_solve<LPB, 8, BALL>(y, s, s0, k, j, rs);
+    else if constexpr (LPB <= 4) {
+        if (E <= 12) thr_solve<LPB, 12, BALL>(y, s, s0, k, j, rs);
+        else if (E <= 16) thr_solve<LPB, 16, BALL>(y, s, s0, k, j, rs);
+        else if constexpr (LPB == 2) {
+            if (E <= 24) thr_solve<LPB, 24, BALL>(y, s, s0, k, j, rs);
+            else thr_solve<LPB, 32, BALL>(y, s, s0, k, j, rs);
+        }
+    }
+}
+
 struct ProjWork {
     unsigned *count;
     int64_t *list;
@@ -752,7 +946,7 @@ static ProjWork proj_layout(void *base, int64_t n, int64_t nb, int64_t max_block
 template <bool BALL>
 static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
                        int64_t max_block, void *work, size_t work_bytes, hipStream_t st,
-                       const double *gate = nullptr) {
+                       const double *gate = nullptr, bool fast = false) {
     if (nb <= 0 || n <= 0 || y == nullptr || starts == nullptr) return BSLS_E_ARG;
     if (max_block < 1) return BSLS_E_ARG;
     ProjWork w = proj_layout(work, n, nb, max_block);
@@ -769,8 +963,26 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
         const int v = e ? atoi(e) : 2;
         return (v == 1 || v == 3) ? v : 2;
     }();
+    // the sort-free path: lanes per block (BSLS_PROJ_LPB, A/B), 4 by default
+    static const int lpb = [] {
+        const char *e = getenv("BSLS_PROJ_LPB");
+        const int v = e ? atoi(e) : 4;
+        return (v == 2 || v == 8) ? v : 4;
+    }();
     const int64_t ngrp = (nb + WAVE - 1) / WAVE;
-    if (pw == 3)
+    if (fast) {
+        const int64_t waves = (nb + WAVE / lpb - 1) / (WAVE / lpb);
+        const unsigned grid = (unsigned)((waves + 3) / 4);
+        if (lpb == 2)
+            proj_thr_kernel<BALL, 2><<<grid, 256, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                          max_block > SMALL_MAX, gate);
+        else if (lpb == 8)
+            proj_thr_kernel<BALL, 8><<<grid, 256, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                          max_block > SMALL_MAX, gate);
+        else
+            proj_thr_kernel<BALL, 4><<<grid, 256, 0, st>>>(y, starts, nb, n, w.list, w.count,
+                                                          max_block > SMALL_MAX, gate);
+    } else if (pw == 3)
         proj_lds_kernel<BALL, 3><<<(unsigned)((ngrp + 2) / 3), 3 * WAVE, 0, st>>>(
             y, starts, nb, n, w.list, w.count, max_block > SMALL_MAX, gate);
     else if (pw == 2)
@@ -823,9 +1035,9 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
 
 int proj_launch_gated(bool ball, double *y, const int64_t *starts, int64_t nb, int64_t n,
                       int64_t max_block, void *work, size_t work_bytes, hipStream_t st,
-                      const double *gate) {
-    return ball ? proj_launch<true>(y, starts, nb, n, max_block, work, work_bytes, st, gate)
-                : proj_launch<false>(y, starts, nb, n, max_block, work, work_bytes, st, gate);
+                      const double *gate, bool fast) {
+    return ball ? proj_launch<true>(y, starts, nb, n, max_block, work, work_bytes, st, gate, fast)
+                : proj_launch<false>(y, starts, nb, n, max_block, work, work_bytes, st, gate, fast);
 }
 
 }  // namespace bsls
@@ -848,4 +1060,18 @@ extern "C" int bsls_proj_multi_ball(double *d_y, const int64_t *d_starts, int64_
                                     size_t work_bytes, void *stream) {
     return proj_launch<true>(d_y, d_starts, nblocks, n, max_block, d_work, work_bytes,
                              (hipStream_t)stream);
+}
+
+extern "C" int bsls_proj_multi_simplex_fast(double *d_y, const int64_t *d_starts, int64_t nblocks,
+                                            int64_t n, int64_t max_block, void *d_work,
+                                            size_t work_bytes, void *stream) {
+    return proj_launch<false>(d_y, d_starts, nblocks, n, max_block, d_work, work_bytes,
+                              (hipStream_t)stream, nullptr, true);
+}
+
+extern "C" int bsls_proj_multi_ball_fast(double *d_y, const int64_t *d_starts, int64_t nblocks,
+                                         int64_t n, int64_t max_block, void *d_work,
+                                         size_t work_bytes, void *stream) {
+    return proj_launch<true>(d_y, d_starts, nblocks, n, max_block, d_work, work_bytes,
+                             (hipStream_t)stream, nullptr, true);
 }

@@ -326,4 +326,22 @@ __device__ __forceinline__ void tile_walk_any(const bsls_tiles &T, int64_t rb, i
     else tile_walk<MODE>(T, rb, g, src, rows, rcol);
 }
 
+// Host-side validation of a tile image against the matrix it claims to hold
+// (bb.hip's K1 / K2 images, lsq.hip's x-space operator): shape, plan, LDS
+// budget, layout flags and the bit widths the dealt entries assume.
+inline bool tiles_valid(const bsls_tiles &T, int64_t rows, int64_t cols, int64_t halo,
+                        bool need_val, bool colv_lds, int64_t lds_max) {
+    if (T.rows != rows || T.cols != cols || T.halo != halo || T.H < 64) return false;
+    if (T.nrb != (rows + T.H - 1) / T.H || T.ngroups < 1 || T.nquads < 0) return false;
+    if (T.order != 0 && !(T.order == 1 && T.ngroups % 8 == 0)) return false;
+    if (tile_lds_doubles(T, colv_lds) * 8 > (size_t)lds_max) return false;
+    if (!T.group_col || !T.wave_off || !T.ent) return false;
+    const int64_t lay = T.layout & ~(int64_t)(BSLS_TILE_NT | BSLS_TILE_VAL32 | BSLS_TILE_VAL16);
+    if (T.layout != 0 && !((lay == 1 || lay == 2) && T.base && T.H + T.halo < 65536))
+        return false;
+    if ((T.layout & BSLS_TILE_VAL32) && (T.layout & BSLS_TILE_VAL16)) return false;
+    if (lay == 2 && T.H + T.halo >= (1 << 18)) return false;   // >= 6 column bits
+    return need_val ? T.val != nullptr : true;
+}
+
 }  // namespace bsls

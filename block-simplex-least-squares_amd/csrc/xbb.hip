@@ -33,7 +33,7 @@ namespace bsls {
 
 int proj_launch_gated(bool ball, double *y, const int64_t *starts, int64_t nb, int64_t n,
                       int64_t max_block, void *work, size_t work_bytes, hipStream_t st,
-                      const double *gate);
+                      const double *gate, bool fast);
 
 constexpr int XT = 256;
 constexpr int XGRID = 1024;   // finish: partials per launch (one slot per workgroup)
@@ -373,8 +373,9 @@ extern "C" int bsls_xbb_rounds(const bsls_xbb_problem *p, int64_t count, void *s
             xbb_step_kernel<<<gs, XT, 0, st>>>(p->x, p->g, p->xn, p->gn, p->n, p->scal);
         }
         BSLS_LAUNCH_CHECK();
-        int rc = proj_launch_gated(p->ball != 0, p->xn, p->starts, p->nblocks, p->n, p->max_block,
-                                   p->proj_work, p->proj_work_bytes, st, p->scal + BSLS_XS_MODE);
+        int rc = proj_launch_gated((p->ball & 1) != 0, p->xn, p->starts, p->nblocks, p->n,
+                                   p->max_block, p->proj_work, p->proj_work_bytes, st,
+                                   p->scal + BSLS_XS_MODE, (p->ball & 2) != 0);
         if (rc != BSLS_OK) return rc;
         if (p->lsq) {
             rc = bsls_lsq_residual(p->lsq, p->xn, p->neg_b, p->r, p->scal + BSLS_XS_SQ, stream);

@@ -670,6 +670,7 @@ class IsoPlan:
         torch = _torch()
         L = _native.lib()
         P = _native.pack_plan(starts, n)
+        self.device = _cur_dev()                      # the plan's arrays live there
         self.n = int(n)
         self.npacks = int(P['start'].shape[0])
         self.nlong = int(P['longs'].shape[0])
@@ -684,6 +685,9 @@ class IsoPlan:
     def apply(self, y, stream=None):
         """PAVA v1 (expanded) of every block of y[:n], in place."""
         L = _native.lib()
+        if y.device.index != self.device:
+            raise ValueError('IsoPlan built on cuda:%d applied to a tensor on %s'
+                             % (self.device, y.device))
         check(L.bsls_isotonic_packs(ptr(y), ptr(self.start), ptr(self.mask), ptr(self.len),
                                     self.npacks, ptr(self.longs), self.nlong, self.n,
                                     ptr(self.work), self.work.numel() if self.work is not None
@@ -694,6 +698,12 @@ class IsoPlan:
 _iso_plans = {}
 
 
+def _cur_dev():
+    """Index of the current GPU (-1 without one: host-only tests of the cache)."""
+    torch = _torch()
+    return torch.cuda.current_device() if torch.cuda.is_available() else -1
+
+
 def iso_plan(starts_h, n):
     """IsoPlan of a host block-start array, cached by content (a few layouts):
     an entry matches when its own copy of the starts equals these (a compare
@@ -701,15 +711,16 @@ def iso_plan(starts_h, n):
     call, more than the projection it planned)."""
     st = np.ascontiguousarray(starts_h, dtype=np.int64)
     n = int(n)
+    dev = _cur_dev()                         # a plan's arrays belong to one GPU
     for key, (ref, plan) in _iso_plans.items():
-        if key[:2] == (st.shape[0], n) and (ref is st or np.array_equal(ref, st)):
+        if key[:3] == (st.shape[0], n, dev) and (ref is st or np.array_equal(ref, st)):
             return plan
     if len(_iso_plans) >= 8:
         _iso_plans.pop(next(iter(_iso_plans)))
     plan = IsoPlan(st, n)
     # keyed by (count, n) plus insertion order; the copy guards against a
     # caller that changes its array in place later
-    k = (st.shape[0], n)
+    k = (st.shape[0], n, dev)
     while k in _iso_plans:
         k = k + (len(_iso_plans),)
     _iso_plans[k] = (st.copy(), plan)
@@ -763,7 +774,7 @@ class BlockLayout:
         array (C3: 400 KB, ~0.3 ms a call -- most of an LBFGS.solve iteration,
         whose line search projects ~20 times)."""
         plan = getattr(self, '_iso', None)
-        if plan is None:
+        if plan is None or getattr(plan, 'device', None) != _cur_dev():
             plan = self._iso = iso_plan(self.zstarts_h, self.nz)
         return plan
 

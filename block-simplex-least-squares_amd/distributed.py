@@ -57,6 +57,22 @@ def row_parts(nblocks, parts):
     return [int(v) for v in np.round(np.linspace(0, nblocks, parts + 1)).astype(np.int64)]
 
 
+def _shard_rank(rank):
+    """The rank that decides the shard role: the caller's, else the initialized
+    default process group's.  Without either there is no safe default -- every
+    rank taking role 1 would add target world times over -- so it raises."""
+    if rank is not None:
+        return int(rank)
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank()
+    except ImportError:
+        pass
+    raise ValueError('ShardedBB needs rank= (no torch.distributed process group is '
+                     'initialized to take it from)')
+
+
 class ShardedBB:
     """Drive one rank's stages with the all-reduces between them.
 
@@ -75,8 +91,10 @@ class ShardedBB:
 
     SUMS = slice(5, 9)   # scal[SUMDG..GG]
 
-    def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None, rank=0, fuse=None):
+    def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None, rank=None,
+                 fuse=None):
         self.e = engine
+        rank = _shard_rank(rank)
         # fuse: K2 folds in the previous iteration's ||r||^2 / f / stopping test
         # (stage 8, one stage-9 launch per call); else stage 3 and a stage-9
         # launch after every residual exchange.  BSLS_SHARD_FUSE=0|1 (A/B).

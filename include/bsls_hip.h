@@ -46,6 +46,17 @@ int bsls_proj_multi_simplex(double *d_y, const int64_t *d_starts, int64_t nblock
                             int64_t max_block, void *d_work, size_t work_bytes, void *stream);
 int bsls_proj_multi_ball(double *d_y, const int64_t *d_starts, int64_t nblocks, int64_t n,
                          int64_t max_block, void *d_work, size_t work_bytes, void *stream);
+/* The same two calls (same arguments, workspace and errors) without sorting:
+ * lambda from Newton's method on sum_j max(y_j + lambda, 0) = 1 started at the
+ * block maximum (the active set only shrinks; the first pass that removes
+ * nothing has the reference's set, proj_simplex.h:27-31), the set's sum in a
+ * fixed lane order instead of the sorted prefix chain.  Within 1e-12 *
+ * max(1, |reference|) of the reference on every tested input (the north
+ * star's projection contract), deterministic, not bit-identical. */
+int bsls_proj_multi_simplex_fast(double *d_y, const int64_t *d_starts, int64_t nblocks, int64_t n,
+                                 int64_t max_block, void *d_work, size_t work_bytes, void *stream);
+int bsls_proj_multi_ball_fast(double *d_y, const int64_t *d_starts, int64_t nblocks, int64_t n,
+                              int64_t max_block, void *d_work, size_t work_bytes, void *stream);
 
 /* ---- isotonic regression (PAVA) ---------------------------------------------
  * Replaces isotonic_regression_multi_c{,_2,_3} (c_extensions.pyx:76-138) ->
@@ -509,7 +520,8 @@ typedef struct bsls_csr {           /* a CSR matrix for bsls_csr_spmv */
 
 typedef struct bsls_xbb_problem {
     int64_t m, n, nblocks, max_block;
-    int64_t ball;                   /* 0: proj_multi_simplex, 1: proj_multi_ball */
+    int64_t ball;                   /* bit 0: proj_multi_ball (else proj_multi_simplex);
+                                       bit 1: the sort-free _fast form */
     bsls_csr A, AT;                 /* A (m x n) and A' (n x m), explicit */
     const double *neg_b;            /* m: -b */
     const int64_t *starts;          /* nblocks block starts (strictly increasing) */
@@ -536,10 +548,11 @@ typedef struct bsls_xbb_problem {
      * iteration, one pass; then x_new = x + d, one pass).  0: BB. */
     int64_t lbfgs;
     double *s, *y;                  /* n each: delta_x, delta_g of the last accepted step */
-    double *lb;                     /* bsls_xbb_lbfgs_size(lbfgs) doubles: rho ring, alpha, coefficients */
+    double *lb;                     /* bsls_xbb_lbfgs_size(lbfgs) BYTES: rho ring, alpha, coefficients */
 } bsls_xbb_problem;
 
 size_t bsls_xbb_workspace_size(int64_t m, int64_t n, int64_t A_ntiles, int64_t AT_ntiles);
+/* Bytes of the L-BFGS scratch `lb` for `corrections` (0: none). */
 size_t bsls_xbb_lbfgs_size(int64_t corrections);
 /* x must hold x_init; resets scal (mode INIT) and the reduction tickets. */
 int bsls_xbb_init(const bsls_xbb_problem *p, void *stream);

@@ -400,3 +400,10 @@ def test_iso_plan_cache_by_content(monkeypatch):
     p4 = device.iso_plan(a, 20)
     assert p4 is not p1 and len(made) == 4
     assert device.iso_plan(np.array([0, 3, 7, 12]), 20) is p1
+    # a plan's arrays live on one GPU: the same layout on another device is
+    # planned again, and the first device still finds its own
+    monkeypatch.setattr(device, '_cur_dev', lambda: 5)
+    p5 = device.iso_plan(np.array([0, 3, 7, 12]), 20)
+    assert p5 is not p1 and len(made) == 5
+    monkeypatch.setattr(device, '_cur_dev', lambda: -1)
+    assert device.iso_plan(np.array([0, 3, 7, 12]), 20) is p1
