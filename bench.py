@@ -1,23 +1,24 @@
 #!/usr/bin/env python
-"""Benchmark: BB solver iterations/sec + proj_simplex HBM GB/s on MI355X.
-One JSON line on rank 0.
+"""Benchmark: BB solver iterations/sec (1M-route block-LSQ) + proj_simplex HBM
+GB/s on MI355X.  One JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C5|C3]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C3|C5]
 
 A step = one full projected-BB iteration (python/BB.py:17-41 semantics, fused
 K2 -> K3 -> K1 on the device) over the whole problem, inputs resident in HBM.
 
-Default workload C5 (BASELINE.json configs[4]): ONE synthetic problem of 10M
-routes / 500k blocks / 1M links / 160M nnz, the same for every N
-(synthetic.make_partitioned), column-sharded by whole blocks over the N ranks
-(one process per GPU, torchrun); strong scaling: value = iterations/s of the
-whole job, the 1-GPU run being the N = 1 point.  Per iteration one RCCL
-all-reduce of the four BB sums and one of the residual r (8 MB) after K1
-(distributed.ShardedBB; --parts > 1 pipelines it behind K1 by row parts).
-At N = 1 the line also carries "c3": the BASELINE metric's 1M-route problem
-(C3: 1M routes / 50k blocks / 100k links / 16M nnz) with its kernels and
-roofline, the C2 projection, the x-space BB, mirror descent and the standalone
-PAVA legs, and the CPU baselines.
+Headline (BASELINE.json's metric and configs[2]): C3, 1M routes / 50k blocks /
+100k links / 16M nnz.  At N = 1 `value` is C3's iterations/s on one GPU.  At
+N > 1 every rank holds one C3-sized column shard (synthetic.make_shard with the
+rank in its seed; rank 0's shard IS the C3 problem) of one N x 1M-route problem
+over the same 100k links: weak scaling, per-GPU work fixed, one RCCL all-reduce
+of the residual (800 KB) and of the four BB sums per iteration
+(distributed.ShardedBB), `value` = N x iterations/s = 1M-route iterations/s of
+the whole job.  The north star's strong-scaling problem (BASELINE configs[4],
+C5: 10M routes / 500k blocks / 1M links, ONE problem column-sharded over the N
+ranks) is timed beside it at every N as "c5".  At N = 1 the line also carries
+the C2 projection, the standalone PAVA, the x-space / mirror-descent / DORE /
+L-BFGS legs and the CPU baselines (C3).
 
 Early exits are disabled for timing: exactly K iterations run.
 """
@@ -39,12 +40,9 @@ for _p in (ROOT, PKG):
 
 import numpy as np  # noqa: E402
 
-# BASELINE.json's metric names the 1M-route problem (C3); the headline `value`
-# here is the north star's 10M-route problem (C5, BASELINE configs[4]), the one
-# its 8-GPU target is quoted on and the one bench.py scales over N GPUs, so the
-# metric text says which; the C3 rate is the line's "c3" entry (N = 1).
-METRIC = ('BB solver iterations/sec (10M-route block-LSQ, BASELINE configs[4]; '
-          '1M-route rate in "c3") + proj_simplex HBM GB/s')
+# BASELINE.json's metric text, verbatim; `value` is its 1M-route (C3) rate
+METRIC = 'BB solver iterations/sec (1M-route block-LSQ) + proj_simplex HBM GB/s'
+ROUND = 'r04'
 HBM_PEAK = 8.0e12   # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -166,18 +164,22 @@ def bench_stored_values(sh, b, steps, warmup, codec=None):
                                    'frac': ib * its / HBM_PEAK}}
 
 
-def bench_proj(reps=30, batch=16):
+def bench_proj(reps=30, batch=16, fast=True):
     """C2 proj_multi_simplex (100k blocks x mean 32, 3.2M fp64) on the device,
-    every launch on fresh input.  avg_us: `batch` launches back to back on
-    `batch` distinct copies of the input between two events on the launch
-    stream (the stream held by a spin kernel while the host enqueues) -- the
-    kernel time rocprofv3 reports, dispatch gaps amortised; isolated_*: one
-    launch per event pair (adds the launch latency)."""
+    every launch on fresh input: the sort-free path (bsls_proj_multi_simplex_fast,
+    the north star's 1e-12 contract) or, fast=False, the bit-identical sorting
+    path.  avg_us: `batch` launches back to back on `batch` distinct copies of
+    the input between two events on the launch stream (the stream held by a
+    spin kernel while the host enqueues) -- the kernel time rocprofv3 reports,
+    HBM-fed, dispatch gaps amortised; isolated_*: one launch per event pair
+    (adds the launch latency)."""
     import torch
     import _native
     from _native import ptr, stream_handle, check
     from synthetic import proj_input
     L = _native.lib()
+    name = 'bsls_proj_multi_simplex_fast' if fast else 'bsls_proj_multi_simplex'
+    fn = getattr(L, name)
     y_h, starts_h = proj_input()
     n, p = y_h.shape[0], starts_h.shape[0]
     mb = int(np.max(np.diff(np.append(starts_h, n))))
@@ -186,13 +188,12 @@ def bench_proj(reps=30, batch=16):
     ws = torch.zeros(L.bsls_proj_workspace_size(n, p, mb), dtype=torch.uint8, device='cuda')
 
     def proj(t):
-        check(L.bsls_proj_multi_simplex(ptr(t), ptr(st), p, n, mb, ptr(ws), ws.numel(),
-                                        stream_handle()), 'proj')
+        check(fn(ptr(t), ptr(st), p, n, mb, ptr(ws), ws.numel(), stream_handle()), name)
     ys = [y0.clone() for _ in range(batch)]
     for t in ys[:3]:
         proj(t)
     avg = []
-    for _ in range(3):
+    for _ in range(5):
         for t in ys:
             t.copy_(y0)
         torch.cuda.synchronize()
@@ -204,7 +205,7 @@ def bench_proj(reps=30, batch=16):
         e1.record()
         torch.cuda.synchronize()
         avg.append(e0.elapsed_time(e1) / batch)
-    us = sorted(avg)[1] * 1e3
+    us = sorted(avg)[2] * 1e3
     y = ys[0]
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(reps)]
@@ -219,17 +220,21 @@ def bench_proj(reps=30, batch=16):
     med = ms[len(ms) // 2]
     byt = 16 * n + 4 * (p + 1)
     del ys
-    # CPU baseline for the same call: the oracle (1 thread)
+    # CPU baseline for the same call: the oracle (1 thread), and the check
     from oracle import oracle as orc
     yc = y_h.copy()
     t0 = time.perf_counter()
     orc.proj_multi_simplex_c(yc, starts_h)
     cpu_s = time.perf_counter() - t0
-    ok = bool(np.array_equal(yc.view(np.int64), y.cpu().numpy().view(np.int64)))
-    return {'n': n, 'blocks': p, 'avg_us': us, 'GB_s': byt / (us * 1e-6) / 1e9,
+    out = y.cpu().numpy()
+    rel = float(np.max(np.abs(out - yc) / np.maximum(1.0, np.abs(yc))))
+    return {'entry': name, 'n': n, 'blocks': p, 'avg_us': us, 'GB_s': byt / (us * 1e-6) / 1e9,
             'alg_bytes': byt, 'frac_hbm_peak': byt / (us * 1e-6) / HBM_PEAK,
+            'rocprof_kernels': ['proj_thr_kernel' if fast else 'proj_lds_kernel'],
             'isolated_median_us': med * 1e3, 'isolated_min_us': ms[0] * 1e3,
-            'cpu_oracle_ms_1thread': cpu_s * 1e3, 'bit_exact_vs_oracle': ok}
+            'cpu_oracle_ms_1thread': cpu_s * 1e3,
+            'max_rel_diff_vs_oracle': rel, 'within_1e-12': rel <= 1e-12,
+            'bit_exact_vs_oracle': bool(np.array_equal(yc.view(np.int64), out.view(np.int64)))}
 
 
 def bench_xspace(sh, b, rounds=40, reps=5, k1=None):
@@ -587,8 +592,11 @@ T0 = time.perf_counter()
 def build_problem(name, world, rank, dist, shard_of=None):
     """The rank's column shard of workload `name` and the full b (SURVEY §8(d)
     recipe, 2 % multiplicative noise so the exact-zero exit never fires).
-    shard_of (rehearsal on one GPU): rank 0's shard of that many ranks, b its
-    own A x (the timing does not depend on b)."""
+    C5: rank's share of the one 10M-route problem (strong scaling).  C3: one
+    C3-sized shard per rank, seeded by the rank (rank 0's is the C3 problem
+    itself), all over the same 100k links (weak scaling).  shard_of
+    (rehearsal on one GPU): rank 0's C5 shard of that many ranks, b its own
+    A x (the timing does not depend on b)."""
     import torch
     from synthetic import make_partitioned, make_shard, add_noise, CONFIGS, SEED
     c = CONFIGS[name]
@@ -596,11 +604,9 @@ def build_problem(name, world, rank, dist, shard_of=None):
         sh = make_partitioned(c['n'], c['p'], c['m'], c['per_col'], rank=rank,
                               world=shard_of or world)
     else:
-        if world != 1:
-            raise SystemExit('workload %s is a single-GPU configuration' % name)
-        sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+        sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED, rank=rank)
         sh['colv'] = None
-        sh['n_total'], sh['p_total'] = c['n'], c['p']
+        sh['n_total'], sh['p_total'] = world * c['n'], world * c['p']
     Ax = torch.from_numpy(sh['Ax']).cuda()
     if dist:
         dist.all_reduce(Ax)
@@ -632,10 +638,17 @@ def build_engine(sh, b, world, dist, parts, sharded=False):
     dist.all_reduce(eng.r)
     eng.target.copy_(eng.r - torch.from_numpy(b).cuda())
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    # the schedule enqueued from C++ with RCCL in the loop (BSLS_SHARD_NATIVE=0:
+    # the Python loop over torch.distributed, for A/B)
+    comm = None
+    if os.environ.get('BSLS_SHARD_NATIVE', '1') != '0' and dist.get_backend() == 'nccl':
+        from distributed import RcclComm
+        comm = RcclComm()
     drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
                     all_reduce_async=torch_all_reduce_async(),
-                    rank=dist.get_rank() if dist else 0)
+                    rank=dist.get_rank(), native=comm)
     drv.prologue()
+    eng._comm = comm            # kept alive with the engine
     return eng, drv.iterate
 
 
@@ -752,7 +765,7 @@ def host_info(threads):
             'OPENBLAS_NUM_THREADS': os.environ.get('OPENBLAS_NUM_THREADS')}
 
 
-LEGS = ('main', 'c3', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'gdlbfgs', 'c1',
+LEGS = ('main', 'c5', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'gdlbfgs', 'c1',
         'cpu')
 
 
@@ -768,7 +781,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
-    ap.add_argument('--workload', default='C5', choices=['C5', 'C3'])
+    ap.add_argument('--workload', default='C3', choices=['C3', 'C5'])
     ap.add_argument('--parts', type=int, default=1,
                     help='row parts of the pipelined residual all-reduce (N > 1)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -795,8 +808,10 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
-    if world > 1 or args.rehearse_shard:
-        legs = {'main'}
+    if args.rehearse_shard:
+        legs, args.workload = {'main'}, 'C5'
+    elif world > 1:
+        legs &= {'main', 'c5'}
     # (modulo: the gloo rehearsal puts several ranks on one GPU)
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -817,60 +832,20 @@ def main():
     out = {} if rank == 0 else None
     wl = args.workload
     if 'main' in legs:
-        sh, b = build_problem(wl, world, rank, dist, shard_of=args.rehearse_shard or None)
-        log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
-            % (wl, rank, world, sh['n'], sh['p'], sh['m'],
-               sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
-        eng, run = build_engine(sh, b, world, dist, args.parts,
-                                sharded=bool(args.rehearse_shard))
-        log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
-        el = time_run(run, args.steps, args.warmup, dist)
-        it_s = args.steps / el
-        finite = bool(np.isfinite(eng.scalars()[4]))
-        log('%d iterations in %.3f s: %.1f it/s' % (args.steps, el, it_s))
-        m, n_g, nz_g, p_g, nnz_g = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
-        kern = {}
-        if args.profile_iters > 0 and rank == 0:
-            kern = kernel_table(eng, 1 + args.warmup + args.steps, args.profile_iters, world,
-                                m, n_g, nz_g, p_g, nnz_g)
-            log('kernel table done')
-        if dist:
-            dist.barrier()
+        res = bench_workload(wl, args, world, rank, dist, tfile, args.steps,
+                             shard_of=args.rehearse_shard or None)
         if rank == 0:
-            n_tot, p_tot = sh['n_total'], sh['p_total']
-            nnz_tot = 16 * n_tot
-            ib = survey_iter_bytes(m, n_tot, n_tot - p_tot, nnz_tot)
-            key = ('%s_x%d' % (wl, args.rehearse_shard)) if args.rehearse_shard else wl
-            out.update({
-                'metric': METRIC, 'value': it_s,
-                'unit': 'BB iterations/s of the whole job (%s: %d routes / %d blocks / %d links)'
-                        % (wl, n_tot, p_tot, m),
-                'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-                'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
-                'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-                'config': {'workload': '%s: BB (z-space, PAVA projection) on %d routes / %d '
-                                       'blocks / %d links / %d nnz, column-sharded over %d GPU(s)'
-                                       % (wl, n_tot, p_tot, m, nnz_tot, world),
-                           'routes': n_tot, 'blocks': p_tot, 'links': m, 'nnz': nnz_tot,
-                           'routes_rank0': n_g, 'nnz_rank0': nnz_g,
-                           'parallelism': 'column-shard x%d' % world,
-                           'residual_allreduce_parts': args.parts if world > 1 else None},
-                'roofline': roofline_of(kern, tfile, key) if kern else None,
-                'iteration_roofline': {'survey_bytes_per_iter': ib,
-                                       'achieved_GB_s': ib * it_s / 1e9,
-                                       'frac': ib * it_s / HBM_PEAK,
-                                       'note': 'whole job over all GPUs; peak is one GPU'},
-                'kernels': kern, 'finite': finite,
-                'profiles': 'profiles/r03_%s_kernel_stats.csv' % key,
-            })
-            if args.rehearse_shard:
-                out['config']['rehearsal'] = ('rank 0 of a %d-way C5 partition on one GPU through '
-                                              'the sharded driver (RCCL with one rank: no fabric)'
-                                              % args.rehearse_shard)
-        del eng, run
-        torch.cuda.empty_cache()
-    # --- N = 1 legs: the BASELINE metric's C3 problem and the other paths -----------
-    if world == 1 and not args.rehearse_shard and legs - {'main'}:
+            out.update({'metric': METRIC, 'n_gpus': world, 'steps': args.steps,
+                        'warmup': args.warmup, 'higher_is_better': True,
+                        'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic'})
+            out.update(res)
+    # the north star's strong-scaling problem beside the headline, at every N
+    if 'c5' in legs and wl != 'C5':
+        res = bench_workload('C5', args, world, rank, dist, tfile, max(args.steps, 100))
+        if rank == 0:
+            out['c5'] = res
+    # --- N = 1 legs: the other paths -------------------------------------------------
+    if world == 1 and not args.rehearse_shard and legs - {'main', 'c5'}:
         extras(args, legs, out, tfile)
     if out is not None:
         print(json.dumps(out), flush=True)
@@ -879,31 +854,85 @@ def main():
         dist.destroy_process_group()
 
 
+def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
+    """Build workload `wl` on this rank, time `steps` iterations after the
+    warmup (max over ranks), and on rank 0 return the line's fields: value
+    (whole-job rate in the workload's unit), kernels (HIP-event table of the
+    rank-0 stages) and their roofline."""
+    import torch
+    sh, b = build_problem(wl, world, rank, dist, shard_of=shard_of)
+    log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
+        % (wl, rank, world, sh['n'], sh['p'], sh['m'],
+           sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
+    eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(shard_of))
+    log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
+    el = time_run(run, steps, args.warmup, dist)
+    it_s = steps / el
+    finite = bool(np.isfinite(eng.scalars()[4]))
+    log('%s: %d iterations in %.3f s: %.1f it/s' % (wl, steps, el, it_s))
+    m, n_g, nz_g, p_g, nnz_g = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
+    kern = {}
+    if args.profile_iters > 0 and rank == 0:
+        kern = kernel_table(eng, 1 + args.warmup + steps, args.profile_iters,
+                            world if not shard_of else 2, m, n_g, nz_g, p_g, nnz_g)
+        log('kernel table done')
+    if dist:
+        dist.barrier()
+    res = None
+    if rank == 0:
+        n_tot, p_tot = sh['n_total'], sh['p_total']
+        nnz_tot = 16 * n_tot
+        key = ('%s_x%d' % (wl, shard_of)) if shard_of else wl
+        weak = wl == 'C3'
+        # weak: the job is world C3-sized shards; its unit is the 1M-route
+        # iteration, so the rate is world x iterations/s of the whole problem
+        value = it_s * world if weak else it_s
+        ib = survey_iter_bytes(m, n_tot, n_tot - p_tot, nnz_tot)
+        res = {
+            'value': value,
+            'unit': ('1M-route BB iterations/s of the whole job (%d x C3: %d routes / %d '
+                     'blocks / %d links)' % (world, n_tot, p_tot, m)) if weak else
+                    ('BB iterations/s of the whole job (%s: %d routes / %d blocks / %d links)'
+                     % (wl, n_tot, p_tot, m)),
+            'iterations_per_s': it_s, 'steps': steps,
+            'ms_per_step': el / steps * 1e3,
+            'scaling': 'weak' if weak else 'strong',
+            'config': {'workload': ('C3 (BASELINE configs[2]): BB (z-space, PAVA projection) on '
+                                    '%d x (1M routes / 50k blocks / 16M nnz), %d links, one '
+                                    'C3 column shard per GPU' % (world, m)) if weak else
+                                   ('%s: BB (z-space, PAVA projection) on %d routes / %d blocks '
+                                    '/ %d links / %d nnz, column-sharded over %d GPU(s)'
+                                    % (wl, n_tot, p_tot, m, nnz_tot, world)),
+                       'routes': n_tot, 'blocks': p_tot, 'links': m, 'nnz': nnz_tot,
+                       'routes_rank0': n_g, 'nnz_rank0': nnz_g,
+                       'parallelism': 'column-shard x%d' % world,
+                       'residual_allreduce_parts': args.parts if world > 1 else None},
+            'roofline': roofline_of(kern, tfile, key) if kern else None,
+            'iteration_roofline': {'survey_bytes_per_iter': ib,
+                                   'achieved_GB_s': ib * it_s / 1e9,
+                                   'frac': ib * it_s / HBM_PEAK,
+                                   'note': 'whole job over all GPUs; peak is one GPU'},
+            'kernels': kern, 'finite': finite,
+            'profiles': 'profiles/%s_%s_kernel_stats.csv' % (ROUND, key),
+        }
+        if shard_of:
+            res['config']['rehearsal'] = ('rank 0 of a %d-way C5 partition on one GPU through '
+                                          'the sharded driver (RCCL with one rank: no fabric)'
+                                          % shard_of)
+    if getattr(eng, '_comm', None) is not None:
+        torch.cuda.synchronize()
+        eng._comm.close()
+    del eng, run
+    torch.cuda.empty_cache()
+    return res
+
+
 def extras(args, legs, out, tfile):
     import torch
     steps3 = max(args.steps, 50)
     sh3 = b3 = None
-    if legs & {'c3', 'c3sv', 'xspace', 'md', 'dore', 'lbfgs', 'gdlbfgs', 'cpu'}:
+    if legs & {'c3sv', 'xspace', 'md', 'dore', 'lbfgs', 'gdlbfgs', 'cpu'}:
         sh3, b3 = build_problem('C3', 1, 0, None)
-    if 'c3' in legs:
-        eng3, run3 = build_engine(sh3, b3, 1, None, 1)
-        el3 = time_run(run3, steps3, args.warmup, None)
-        its3 = steps3 / el3
-        c = sh3['A']
-        kern3 = kernel_table(eng3, 1 + args.warmup + steps3, 50, 1,
-                             eng3.m, eng3.n, eng3.nz, eng3.layout.p, c.nnz)
-        ib3 = survey_iter_bytes(eng3.m, eng3.n, eng3.nz, c.nnz)
-        log('C3: %.1f it/s' % its3)
-        out['c3'] = {'value': its3, 'unit': 'BB iterations/s (C3: 1M routes / 50k blocks / '
-                                            '100k links / 16M nnz, 1 GPU)',
-                     'ms_per_step': el3 / steps3 * 1e3, 'kernels': kern3,
-                     'roofline': roofline_of(kern3, tfile, 'C3'),
-                     'iteration_roofline': {'survey_bytes_per_iter': ib3,
-                                            'achieved_GB_s': ib3 * its3 / 1e9,
-                                            'frac': ib3 * its3 / HBM_PEAK},
-                     'profiles': 'profiles/r03_C3_kernel_stats.csv'}
-        del eng3, run3
-        torch.cuda.empty_cache()
     if 'c3sv' in legs:
         out['c3_stored_values'] = bench_stored_values(sh3, b3, steps3, args.warmup)
         torch.cuda.empty_cache()
@@ -911,6 +940,7 @@ def extras(args, legs, out, tfile):
         torch.cuda.empty_cache()
     if 'proj' in legs:
         out['proj_simplex'] = bench_proj()
+        out['proj_simplex_exact'] = bench_proj(fast=False)
         log('C2 projection done')
     if 'iso' in legs:
         out['isotonic'] = bench_iso()

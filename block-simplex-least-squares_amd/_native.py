@@ -18,6 +18,7 @@ HEADER = os.path.join(os.path.dirname(HERE), 'include', 'bsls_hip.h')
 BSLS_OK = 0
 BSLS_E_ARG = -1
 BSLS_E_WORKSPACE = -2
+BSLS_E_COMM = -100
 
 # scal[] slots and stop reasons (include/bsls_hip.h)
 S_STOP, S_ITER, S_ZBUF, S_T, S_FX, S_SUMDG, S_DZDG, S_DGDG, S_GG, S_RR, S_WARN = range(11)
@@ -169,6 +170,12 @@ _SIGS = {
     'bsls_dore_iterate': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(DoreState), _i64,
                                  _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
+    'bsls_comm_id_bytes': (_sz, []),
+    'bsls_comm_unique_id': (_int, [_vp]),
+    'bsls_comm_create': (_int, [_vp, _int, _int, ctypes.POINTER(_vp)]),
+    'bsls_comm_destroy': (_int, [_vp]),
+    'bsls_comm_all_reduce': (_int, [_vp, _vp, _i64, _vp]),
+    'bsls_bb_shard_iterate': (_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp]),
     'bsls_bb_row_blocks': (_i64, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_residual_rows': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _i64, _vp]),
     'bsls_md_update_gated': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _dbl, _i64, _vp, _vp, _sz,

@@ -20,7 +20,14 @@ HIP library or a HIP device every function raises RuntimeError.  The host path
 (include/bsls_cpu.h, c_extensions/_cpu.py: the reference's own CPU path,
 BASELINE configs[0]) runs NumPy inputs only when selected explicitly
 (BSLS_DEVICE=cpu or _native.set_device('cpu')).
+
+Projections (proj_simplex_c, proj_multi_simplex_c, proj_multi_ball_c) take the
+sort-free kernels (bsls_proj_multi_*_fast: within 1e-12 * max(1, |ref|) of the
+reference, the north star's projection contract) unless BSLS_PROJ=exact
+selects the sorting kernels, which reproduce the reference bit for bit.
 """
+import os
+
 import numpy as np
 
 import _native
@@ -138,7 +145,17 @@ def _work(nbytes):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device='cuda')
 
 
+def _proj_entry(fn_name):
+    """The C entry for a projection: the sort-free _fast kernels unless
+    BSLS_PROJ=exact (read per call, so a test or caller can switch)."""
+    mode = os.environ.get('BSLS_PROJ', 'fast')
+    if mode not in ('fast', 'exact'):
+        raise ValueError('BSLS_PROJ must be fast or exact, not %r' % mode)
+    return fn_name + ('_fast' if mode == 'fast' else '')
+
+
 def _run_proj(fn_name, y, blocks_h, n, first_offset=0):
+    fn_name = _proj_entry(fn_name)
     L = _native.lib()
     st = _Staged(y)
     dev = st.dev if first_offset == 0 else st.dev
@@ -169,8 +186,9 @@ def proj_simplex_c(y, start, end):
     sub = st.dev[:end]
     b = _dev_i64(np.array([start], dtype=np.int64))
     ws = _work(L.bsls_proj_workspace_size(end, 1, end - start))
-    check(L.bsls_proj_multi_simplex(ptr(sub), ptr(b), 1, end, end - start, ptr(ws), ws.numel(),
-                                    stream_handle()), 'proj_simplex_c')
+    fn = getattr(L, _proj_entry('bsls_proj_multi_simplex'))
+    check(fn(ptr(sub), ptr(b), 1, end, end - start, ptr(ws), ws.numel(), stream_handle()),
+          'proj_simplex_c')
     _torch().cuda.synchronize()
     st.commit()
 

@@ -1,0 +1,132 @@
+// shard.hip -- the column-sharded BB iteration of one rank, enqueued from C++
+// with its RCCL collectives in the same loop (include/bsls_hip.h
+// bsls_bb_shard_iterate).  The schedule is distributed.ShardedBB's (python),
+// the orchestration the gloo tests pin against the oracle:
+//     stage 8   K2 (g_g, the four local BB sums) with f / stop test of i - 1
+//     RCCL      all-reduce(sum) of scal[SUMDG..GG]        32 B
+//     stage 4   K3: t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = colv N_g z_g
+//     stage 1   K1: r_g = A_g x_g (+ target on the shard_role 1 rank)
+//     RCCL      all-reduce(sum) of r                      8 m B
+// and stage 9 (f / stop test) after the last iteration of a call.  A Python
+// loop enqueued the same thing at ~4 ctypes calls + 2 torch.distributed calls
+// per iteration (tens of us of host time against a ~100-us device iteration
+// on 8 ranks); here an iteration costs 4 kernel launches + 2 RCCL calls of host
+// time and nothing waits on the host.
+//
+// RCCL is resolved at run time (dlopen of librccl.so.1: in a torch process the
+// copy torch already loaded, so torch.distributed and this driver share one
+// RCCL), so the library has no link-time RCCL dependency and loads without it.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include "bsls_common.hpp"
+
+extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
+
+namespace bsls {
+
+struct RcclApi {
+    bool ok = false;
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+};
+
+static const RcclApi &rccl() {
+    static RcclApi api = [] {
+        RcclApi a;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return a;
+        a.get_id = (decltype(a.get_id))dlsym(h, "ncclGetUniqueId");
+        a.init = (decltype(a.init))dlsym(h, "ncclCommInitRank");
+        a.destroy = (decltype(a.destroy))dlsym(h, "ncclCommDestroy");
+        a.all_reduce = (decltype(a.all_reduce))dlsym(h, "ncclAllReduce");
+        a.err = (decltype(a.err))dlsym(h, "ncclGetErrorString");
+        a.ok = a.get_id && a.init && a.destroy && a.all_reduce;
+        return a;
+    }();
+    return api;
+}
+
+}  // namespace bsls
+
+using namespace bsls;
+
+struct bsls_comm {
+    ncclComm_t comm;
+    int world, rank;
+};
+
+// RCCL failures map to BSLS_E_COMM - ncclResult (distinct from hip errors)
+static int comm_rc(ncclResult_t r) { return r == ncclSuccess ? BSLS_OK : BSLS_E_COMM - (int)r; }
+
+extern "C" size_t bsls_comm_id_bytes(void) { return sizeof(ncclUniqueId); }
+
+extern "C" int bsls_comm_unique_id(void *id_out) {
+    if (!id_out) return BSLS_E_ARG;
+    const RcclApi &R = rccl();
+    if (!R.ok) return BSLS_E_COMM;
+    ncclUniqueId id;
+    const int rc = comm_rc(R.get_id(&id));
+    if (rc == BSLS_OK) memcpy(id_out, &id, sizeof(id));
+    return rc;
+}
+
+extern "C" int bsls_comm_create(const void *id, int world, int rank, bsls_comm **out) {
+    if (!id || !out || world < 1 || rank < 0 || rank >= world) return BSLS_E_ARG;
+    const RcclApi &R = rccl();
+    if (!R.ok) return BSLS_E_COMM;
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    bsls_comm *c = new bsls_comm{nullptr, world, rank};
+    const int rc = comm_rc(R.init(&c->comm, world, uid, rank));
+    if (rc != BSLS_OK) {
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return BSLS_OK;
+}
+
+extern "C" int bsls_comm_destroy(bsls_comm *c) {
+    if (!c) return BSLS_OK;
+    const int rc = comm_rc(rccl().destroy(c->comm));
+    delete c;
+    return rc;
+}
+
+extern "C" int bsls_comm_all_reduce(bsls_comm *c, double *buf, int64_t count, void *stream) {
+    if (!c || !buf || count < 0) return BSLS_E_ARG;
+    return comm_rc(rccl().all_reduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->comm,
+                                     (hipStream_t)stream));
+}
+
+extern "C" int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *c, int64_t first_iter,
+                                     int64_t count, int fuse, void *stream) {
+    if (!p || !c || first_iter < 1 || count < 0) return BSLS_E_ARG;
+    if (p->shard_role != (c->rank == 0 ? 1 : 2)) return BSLS_E_ARG;   // target added once
+    const RcclApi &R = rccl();
+    hipStream_t st = (hipStream_t)stream;
+    int rc;
+    for (int64_t i = first_iter; i < first_iter + count; ++i) {
+        // K2 (+ the fused f / stop test of i - 1), then the BB sums summed over ranks
+        if ((rc = bsls_bb_stage(p, fuse ? 8 : 3, i, stream)) != BSLS_OK) return rc;
+        if ((rc = comm_rc(R.all_reduce(p->scal + BSLS_S_SUMDG, p->scal + BSLS_S_SUMDG, 4,
+                                       ncclFloat64, ncclSum, c->comm, st))) != BSLS_OK)
+            return rc;
+        if ((rc = bsls_bb_stage(p, 4, i, stream)) != BSLS_OK) return rc;
+        // the partial residual, then r = the sum over ranks (the one real exchange)
+        if ((rc = bsls_bb_stage(p, 1, i, stream)) != BSLS_OK) return rc;
+        if ((rc = comm_rc(R.all_reduce(p->r, p->r, (size_t)p->m, ncclFloat64, ncclSum, c->comm,
+                                       st))) != BSLS_OK)
+            return rc;
+        if (!fuse && (rc = bsls_bb_stage(p, 9, i, stream)) != BSLS_OK) return rc;
+    }
+    if (count > 0 && fuse) return bsls_bb_stage(p, 9, first_iter + count - 1, stream);
+    return BSLS_OK;
+}

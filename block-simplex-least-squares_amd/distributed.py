@@ -92,9 +92,13 @@ class ShardedBB:
     SUMS = slice(5, 9)   # scal[SUMDG..GG]
 
     def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None, rank=None,
-                 fuse=None):
+                 fuse=None, native=None):
         self.e = engine
         rank = _shard_rank(rank)
+        # native: an RcclComm -- iterate() then enqueues the whole schedule from
+        # C++ (bsls_bb_shard_iterate: the stages and the two RCCL all-reduces of
+        # an iteration, no Python per iteration); parts > 1 stays Python-driven
+        self.native = native if (native is not None and int(parts) <= 1) else None
         # fuse: K2 folds in the previous iteration's ||r||^2 / f / stopping test
         # (stage 8, one stage-9 launch per call); else stage 3 and a stage-9
         # launch after every residual exchange.  BSLS_SHARD_FUSE=0|1 (A/B).
@@ -141,6 +145,15 @@ class ShardedBB:
 
     def iterate(self, first, count):
         e = self.e
+        if self.native is not None:
+            import _native
+            from _native import check, stream_handle
+            if count > 0:
+                check(_native.lib().bsls_bb_shard_iterate(e.P, self.native.handle, int(first),
+                                                          int(count), int(self.fuse),
+                                                          stream_handle()),
+                      'bsls_bb_shard_iterate')
+            return
         for i in range(first, first + count):
             if self.fuse:
                 e.stage(8, i)    # K2 + f / stopping test of iteration i - 1
@@ -169,3 +182,45 @@ def torch_all_reduce_async(group=None):
     def f(t):
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
     return f
+
+
+class RcclComm:
+    """A C-ABI communicator (bsls_comm_*, csrc/shard.hip) over the ranks of the
+    initialized torch.distributed group: rank 0 makes the RCCL id, a broadcast
+    over the group hands it to the others, every rank joins on its current
+    device.  In a torch process csrc/shard.hip resolves the RCCL torch loaded,
+    so both drive the same library."""
+
+    def __init__(self, group=None):
+        import ctypes
+        import torch
+        import torch.distributed as dist
+        import _native
+        from _native import check
+        L = _native.lib()
+        nb = int(L.bsls_comm_id_bytes())
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        buf = ctypes.create_string_buffer(nb)
+        if self.rank == 0:
+            check(L.bsls_comm_unique_id(buf), 'bsls_comm_unique_id')
+        t = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+        if dist.get_backend(group) == 'nccl':
+            t = t.cuda()
+        dist.broadcast(t, src=0, group=group)
+        raw = bytes(t.cpu().numpy().tobytes())
+        h = ctypes.c_void_p()
+        check(L.bsls_comm_create(raw, self.world, self.rank, ctypes.byref(h)), 'bsls_comm_create')
+        self.handle = h
+
+    def all_reduce(self, t):
+        """In-place sum of a float64 device tensor over the ranks (current stream)."""
+        import _native
+        from _native import check, ptr, stream_handle
+        check(_native.lib().bsls_comm_all_reduce(self.handle, ptr(t), t.numel(),
+                                                 stream_handle()), 'bsls_comm_all_reduce')
+
+    def close(self):
+        import _native
+        if self.handle is not None:
+            _native.lib().bsls_comm_destroy(self.handle)
+            self.handle = None

@@ -30,6 +30,7 @@ extern "C" {
 #define BSLS_OK 0
 #define BSLS_E_ARG (-1)        /* bad size / null pointer / layout */
 #define BSLS_E_WORKSPACE (-2)  /* workspace smaller than *_workspace_size() */
+#define BSLS_E_COMM (-100)     /* RCCL missing (exactly this) or failed (minus its ncclResult_t) */
 
 /* Block layout shared by every projection entry: block b covers
  * [d_starts[b], d_starts[b+1]) (the last block ends at n); d_starts strictly
@@ -399,6 +400,28 @@ int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *strea
 int64_t bsls_bb_row_blocks(const bsls_bb_problem *p, int64_t *rows_per_block);
 int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
                           void *stream);
+
+/* ---- multi-GPU: one rank's column-sharded iterations, RCCL in the loop ----
+ * The reference has no parallel code; this is the driver of
+ * distributed.ShardedBB (python) moved to C++ so no Python runs per
+ * iteration.  A communicator of `world` ranks (one per GPU, created on the
+ * current device; RCCL is resolved at run time from librccl.so.1, so in a
+ * torch process it is the RCCL torch.distributed uses): rank 0 makes the id,
+ * every rank passes the same bytes to bsls_comm_create. */
+typedef struct bsls_comm bsls_comm;
+size_t bsls_comm_id_bytes(void);
+int bsls_comm_unique_id(void *id_out);
+int bsls_comm_create(const void *id, int world, int rank, bsls_comm **out);
+int bsls_comm_destroy(bsls_comm *comm);
+/* in-place sum of `count` doubles over the ranks, on `stream` */
+int bsls_comm_all_reduce(bsls_comm *comm, double *d_buf, int64_t count, void *stream);
+/* Iterations first_iter .. first_iter+count-1 of the sharded schedule (fuse 1:
+ * per iteration stage 8, all-reduce scal[SUMDG..GG], stage 4, stage 1,
+ * all-reduce r; stage 9 after the last.  fuse 0: stage 3 instead of 8 and a
+ * stage 9 after every r exchange).  p->shard_role must be 1 on rank 0 and 2
+ * elsewhere (target added once).  All on `stream`; nothing waits on the host. */
+int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *comm, int64_t first_iter,
+                          int64_t count, int fuse, void *stream);
 
 /* ---- DORE on the fused images (python/DORE.py:6-90, gradient_descent.py:55-67)
  * The reference loop with linop = scale * A N, linop_T = scale * N'A',

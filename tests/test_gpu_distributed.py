@@ -39,7 +39,7 @@ def _partitioned(rank, world):
     return sh, add_noise(full['Ax'], 0.02, seed=33), full
 
 
-def _run(rank, world, backend, port, out_q, fmt=None, parts=1, max_iter=10 ** 9):
+def _run(rank, world, backend, port, out_q, fmt=None, parts=1, max_iter=10 ** 9, native=False):
     for p in (ROOT, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -76,8 +76,12 @@ def _run(rank, world, backend, port, out_q, fmt=None, parts=1, max_iter=10 ** 9)
     eng = BBEngine(A_g, None, sz_g, options={'max_iter': max_iter, 'opt_tol': 1e-30},
                    early_exit=max_iter < 10 ** 9, target=target, fmt=fmt)
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    comm = None
+    if native:
+        from distributed import RcclComm
+        comm = RcclComm()
     drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
-                    all_reduce_async=torch_all_reduce_async(), rank=rank)
+                    all_reduce_async=torch_all_reduce_async(), rank=rank, native=comm)
     drv.prologue()
     traj = {}
     for i in range(1, ITERS + 1):
@@ -89,16 +93,20 @@ def _run(rank, world, backend, port, out_q, fmt=None, parts=1, max_iter=10 ** 9)
         traj['r'] = eng.r.cpu().numpy().copy()
         traj['scal'] = eng.scalars().copy()
     out_q.put((rank, traj))
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _spawn(world, backend, fmt=None, parts=1, max_iter=10 ** 9, raw=False):
+def _spawn(world, backend, fmt=None, parts=1, max_iter=10 ** 9, raw=False, native=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29700 + (os.getpid() % 500) + world + 3 * parts + (max_iter % 7)
-    procs = [ctx.Process(target=_run, args=(r, world, backend, port, q, fmt, parts, max_iter))
+    port = 29700 + (os.getpid() % 500) + world + 3 * parts + (max_iter % 7) + 11 * int(native)
+    procs = [ctx.Process(target=_run, args=(r, world, backend, port, q, fmt, parts, max_iter,
+                                            native))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -171,3 +179,26 @@ def test_sharded_stop_keeps_final_residual(cuda, orc):
     r7 = sh['A'].dot(particular_x0(sizes) + block_sizes_to_N(sizes).dot(ref[7])) - b
     for r in range(2):
         assert np.max(np.abs(res[r]['r'] - r7)) <= 1e-9 * max(1.0, np.max(np.abs(r7)))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize('fmt', [None, 'tiles'])
+def test_native_shard_driver_rccl(cuda, orc, fmt):
+    """The C++ driver (bsls_bb_shard_iterate: the stages and both RCCL
+    all-reduces of an iteration enqueued from C++, its own communicator made
+    through RcclComm) follows the oracle, on the panels and on the tiles."""
+    _check(_spawn(1, 'nccl', fmt=fmt, native=True), orc, partitioned=fmt == 'tiles')
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_native_shard_driver_equals_python_loop(cuda):
+    """Same kernels, same order, the same one-rank collectives: the C++ loop
+    gives the Python loop's iterates bit for bit, and the same stop."""
+    a = _spawn(1, 'nccl', fmt='tiles', native=True, raw=True)[0]
+    b = _spawn(1, 'nccl', fmt='tiles', native=False, raw=True)[0]
+    for i in CHECK:
+        assert np.array_equal(a[i], b[i]), i
+    a = _spawn(1, 'nccl', max_iter=7, native=True, raw=True)[0]
+    assert a['scal'][0] == 2 and a['scal'][1] == 7

@@ -24,9 +24,27 @@ def cx(cuda):
     return c_extensions
 
 
+@pytest.fixture
+def exact_proj(monkeypatch):
+    """c_extensions' projections on the bit-identical sorting kernels
+    (BSLS_PROJ=exact); the default is the sort-free _fast path."""
+    monkeypatch.setenv('BSLS_PROJ', 'exact')
+
+
+@pytest.fixture
+def fast_proj(monkeypatch):
+    monkeypatch.setenv('BSLS_PROJ', 'fast')
+
+
+def close12(a, ref):
+    """The north star's projection contract: |a - ref| <= 1e-12 max(1, |ref|)."""
+    a, ref = np.asarray(a, dtype=np.float64), np.asarray(ref, dtype=np.float64)
+    return a.shape == ref.shape and bool(np.all(np.abs(a - ref) <= 1e-12 * np.maximum(1.0, np.abs(ref))))
+
+
 # ------------------------------------------------------------------ projections
 
-def test_proj_golden_numpy(cx, golden):
+def test_proj_golden_numpy(cx, golden, exact_proj):
     G = golden('proj_simplex.npz')
     for ci in range(int(G['ncases'])):
         y, b = G['c%d_y' % ci], G['c%d_blocks' % ci]
@@ -38,7 +56,7 @@ def test_proj_golden_numpy(cx, golden):
     assert exact(y, G['single_out'])
 
 
-def test_proj_kats(cx):
+def test_proj_kats(cx, exact_proj):
     z = np.array([5.352, 3.23, 32.78, -1.234, 1.7, 104., 53.])
     for truth, s, e in [([5.352, 3.23, 1., 0., 1.7, 104., 53.], 2, 4),
                         ([0., 0., 0., 0., 0, 1., 0.], 0, 7), (list(z), 4, 4)]:
@@ -54,7 +72,7 @@ def test_proj_kats(cx):
 
 
 @pytest.mark.parametrize('kind', ['unif', 'gauss'])
-def test_proj_c2_full_size_bit_exact(cx, orc, kind):
+def test_proj_c2_full_size_bit_exact(cx, orc, kind, exact_proj):
     """Config C2 (3.2M fp64, 100k blocks) on device tensors vs the oracle."""
     import torch
     from synthetic import proj_input
@@ -66,7 +84,7 @@ def test_proj_c2_full_size_bit_exact(cx, orc, kind):
     assert exact(yd.cpu().numpy(), ref)
 
 
-def test_proj_size_classes(cx, orc):
+def test_proj_size_classes(cx, orc, exact_proj):
     """Blocks straddling every path: lane (<=64), LDS (<=8192), global (>8192)."""
     rs = np.random.RandomState(SEED)
     sizes = np.array([1, 2, 3, 7, 8, 9, 16, 17, 31, 33, 63, 64, 65, 100, 1000, 4096, 8192, 8193,
@@ -83,7 +101,7 @@ def test_proj_size_classes(cx, orc):
                 assert exact(a, r), (trial, scale, name)
 
 
-def test_proj_ties_and_zeros(cx, orc):
+def test_proj_ties_and_zeros(cx, orc, exact_proj):
     rs = np.random.RandomState(SEED + 3)
     n = 5000
     starts = np.sort(rs.choice(np.arange(1, n), 150, replace=False))
@@ -95,7 +113,7 @@ def test_proj_ties_and_zeros(cx, orc):
         assert exact(a, r)
 
 
-def test_proj_borderline_decisions(cx, orc):
+def test_proj_borderline_decisions(cx, orc, exact_proj):
     """Values on coarse dyadic grids make u_i + (1 - S_i)/(i + 1) land exactly
     on, or within a few ulps of, zero for many i: the cases the kernel decides
     with the reference's own division instead of the fma sign test."""
@@ -115,6 +133,140 @@ def test_proj_borderline_decisions(cx, orc):
             a = y.copy(); getattr(cx, name)(a, starts)
             r = y.copy(); getattr(orc, name)(r, starts)
             assert exact(a, r), (gi, name)
+
+
+# ------------------------------------------------- sort-free projection (_fast)
+# bsls_proj_multi_*_fast (the c_extensions default): Newton on the threshold,
+# no sort -- held to the north star's contract |d| <= 1e-12 max(1, |ref|)
+# against the oracle (which is pinned to the reference), on the same inputs
+# the bit-exact tests above use.
+
+def test_fast_proj_golden_and_kats(cx, golden, fast_proj):
+    G = golden('proj_simplex.npz')
+    for ci in range(int(G['ncases'])):
+        y, b = G['c%d_y' % ci], G['c%d_blocks' % ci]
+        ys = y.copy(); cx.proj_multi_simplex_c(ys, b)
+        assert close12(ys, G['c%d_simplex' % ci]), ('simplex', ci)
+        yb = y.copy(); cx.proj_multi_ball_c(yb, b)
+        assert close12(yb, G['c%d_ball' % ci]), ('ball', ci)
+    y = G['single_y'].copy(); cx.proj_simplex_c(y, 10, 40)
+    assert close12(y, G['single_out'])
+    # tests/fast/test_proj_simplex.py:24-82: the reference's exact-equality KATs
+    z = np.array([5.352, 3.23, 32.78, -1.234, 1.7, 104., 53.])
+    for truth, s_, e_ in [([5.352, 3.23, 1., 0., 1.7, 104., 53.], 2, 4),
+                          ([0., 0., 0., 0., 0, 1., 0.], 0, 7), (list(z), 4, 4)]:
+        y = z.copy(); cx.proj_simplex_c(y, s_, e_)
+        assert list(y) == truth
+    for b, truth in [([0, 2, 4], [1., 0., 1., 0., 0., 1., 0.]),
+                     ([0], [0., 0., 0., 0., 0., 1., 0.]), ([0, 3], [0., 0., 1., 0., 0., 1., 0.])]:
+        y = z.copy(); cx.proj_multi_simplex_c(y, np.array(b))
+        assert list(y) == truth
+    y = np.array([0.234, 0.5, 1.3, -1.234, 1.7, -1.0, 53.])
+    cx.proj_multi_ball_c(y, np.array([0, 2, 4]))
+    assert list(y) == [0.234, 0.5, 1., 0., 0., 0., 1.]
+    np.random.seed(SEED)
+    y = np.random.rand(7)
+    cx.proj_simplex_c(y, 0, 7)
+    assert np.linalg.norm(y - np.array([0., .05006376, .54108944, 0., .38841272, 0.,
+                                        .02043408])) < 1e-6
+
+
+@pytest.mark.parametrize('kind', ['unif', 'gauss'])
+def test_fast_proj_c2_full_size(cx, orc, kind, fast_proj):
+    """Config C2 (3.2M fp64, 100k blocks), U[0,1) and 5 N(0,1), simplex and
+    ball, device tensors, vs the oracle at 1e-12; and deterministic."""
+    import torch
+    from synthetic import proj_input
+    y, starts = proj_input(kind=kind)
+    st = torch.from_numpy(starts).cuda()
+    for gpu, cpu in ((cx.proj_multi_simplex_c, orc.proj_multi_simplex_c),
+                     (cx.proj_multi_ball_c, orc.proj_multi_ball_c)):
+        ref = y.copy()
+        cpu(ref, starts)
+        yd = torch.from_numpy(y).cuda()
+        gpu(yd, st)
+        out = yd.cpu().numpy()
+        assert close12(out, ref), (kind, gpu.__name__)
+        yd2 = torch.from_numpy(y).cuda()
+        gpu(yd2, st)
+        assert exact(yd2.cpu().numpy(), out)            # fixed reduction order
+        # the sums of the projected blocks (simplex: exactly the unit simplex)
+        if gpu is cx.proj_multi_simplex_c:
+            sums = np.add.reduceat(out, starts)
+            assert np.max(np.abs(sums - 1.0)) < 1e-12
+
+
+def test_fast_proj_size_classes_ties_borderline(cx, orc, fast_proj):
+    """Every size class (lane groups <= 64, the exact workgroup / whole-chip
+    paths beyond), scales 1e-3..1e2, ties, zeros, signed zeros, the dyadic
+    borderline grids where u_i + (1 - S_i)/(i + 1) lands on or near zero."""
+    rs = np.random.RandomState(SEED)
+    sizes = np.array([1, 2, 3, 4, 5, 7, 8, 9, 16, 17, 31, 33, 63, 64, 65, 100, 1000, 4096,
+                      8193, 5, 64, 1])
+    for trial in range(3):
+        perm = rs.permutation(sizes)
+        starts = np.concatenate(([3], 3 + np.cumsum(perm)[:-1])).astype(np.int64)
+        n = 3 + int(perm.sum())
+        for scale in (1.0, 0.001, 100.0):
+            y = rs.randn(n) * scale
+            for name in ('proj_multi_simplex_c', 'proj_multi_ball_c'):
+                a = y.copy(); getattr(cx, name)(a, starts)
+                r = y.copy(); getattr(orc, name)(r, starts)
+                assert close12(a, r), (trial, scale, name)
+    n = 5000
+    starts = np.sort(rs.choice(np.arange(1, n), 150, replace=False))
+    starts = np.concatenate(([0], starts)).astype(np.int64)
+    for y in (np.zeros(n), np.full(n, 0.25), np.round(rs.rand(n) * 3) / 3, -np.abs(rs.randn(n)),
+              np.where(rs.rand(n) < 0.5, -0.0, 0.0), np.full(n, 1e6), np.full(n, -3.0)):
+        for name in ('proj_multi_simplex_c', 'proj_multi_ball_c'):
+            a = y.copy(); getattr(cx, name)(a, starts)
+            r = y.copy(); getattr(orc, name)(r, starts)
+            assert close12(a, r), name
+    n = 60_000
+    sizes = rs.randint(1, 65, size=3000)
+    sizes = sizes[np.cumsum(sizes) <= n]
+    n = int(sizes.sum())
+    starts = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+    grids = [rs.randint(-16, 17, size=n) / 8.0,
+             rs.randint(-64, 65, size=n) / 64.0,
+             1.0 / rs.randint(1, 9, size=n) - rs.randint(0, 2, size=n) / 3.0,
+             np.repeat(rs.randint(-4, 5, size=sizes.size) / 4.0, sizes)
+             + rs.randint(-2, 3, size=n) * 2.0 ** -50]
+    for gi, y in enumerate(grids):
+        for name in ('proj_multi_simplex_c', 'proj_multi_ball_c'):
+            a = y.copy(); getattr(cx, name)(a, starts)
+            r = y.copy(); getattr(orc, name)(r, starts)
+            assert close12(a, r), (gi, name)
+
+
+def test_fast_proj_c_abi_entry(cuda, orc):
+    """bsls_proj_multi_simplex_fast through the C ABI directly (what bench.py
+    times), on a wave-boundary layout: 16-block waves with the last wave
+    partial, a first block starting past 0, blocks of 64 and 65."""
+    import torch
+    import _native
+    from _native import ptr, stream_handle, check
+    L = _native.lib()
+    rs = np.random.RandomState(SEED + 11)
+    sizes = np.concatenate((rs.randint(1, 65, size=16 * 37 + 5), [64, 65, 1]))
+    starts = np.concatenate(([2], 2 + np.cumsum(sizes)[:-1])).astype(np.int64)
+    n = 2 + int(sizes.sum())
+    y = rs.rand(n) * 2 - 0.5
+    mb = int(sizes.max())
+    for fn, cpu in ((L.bsls_proj_multi_simplex_fast, orc.proj_multi_simplex_c),
+                    (L.bsls_proj_multi_ball_fast, orc.proj_multi_ball_c)):
+        yd = torch.from_numpy(y).cuda()
+        sd = torch.from_numpy(starts).cuda()
+        ws = torch.zeros(L.bsls_proj_workspace_size(n, sizes.size, mb), dtype=torch.uint8,
+                         device='cuda')
+        check(fn(ptr(yd), ptr(sd), sizes.size, n, mb, ptr(ws), ws.numel(), stream_handle()),
+              'fast')
+        r = y.copy()
+        cpu(r, starts)
+        out = yd.cpu().numpy()
+        assert close12(out, r)
+        assert out[0] == y[0] and out[1] == y[1]      # before the first block: untouched
+    assert L.bsls_proj_multi_simplex_fast(None, None, 0, 0, 1, None, 0, None) == _native.BSLS_E_ARG
 
 
 # ------------------------------------------------------------------ PAVA
@@ -268,7 +420,7 @@ def test_spmv_vs_scipy(cuda, shape, per_row):
 
 # ------------------------------------------------------------------ stress shapes
 
-def test_proj_stress_shapes_bit_exact(cx, orc):
+def test_proj_stress_shapes_bit_exact(cx, orc, exact_proj):
     """python/experiments/test_stress_proj_simplex.py:24-44: single U[0,1) blocks
     up to 1e6 and 1e6 elements in 10 / 100 / 1e4 random blocks (the whole-chip
     sort path for blocks > 8192), simplex and l1-ball, vs the oracle."""
