@@ -1,0 +1,146 @@
+"""Deep full-size parity (noise-free data, iterates at fixed
+iteration counts).  Needs an MI355X.
+
+* C3 (BASELINE configs[2], 1M routes / 50k blocks / 100k links / 16M nnz),
+  b = A x* exactly: BB iterates at 1, 10, 50 and 200 against the oracle's
+  restatement of python/BB.py over SciPy, within the north star's 1e-6, on the
+  default engine (dealt tiles) and the fixed-order one (panels);
+* C5 (configs[4], 10M routes / 500k blocks / 1M links / 160M nnz), noise-free,
+  iterates 1 and 10;
+* rank 0's and rank 1's shards of make_partitioned's C5-density 2-way split
+  (1.2M routes, 120k links, 16 entries per route -- the density an 8-way C5
+  shard sees per link block) on the device, two gloo ranks sharing the GPU,
+  against the oracle at 1, 5 and 20.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def _run_engine(eng, iters):
+    rec = {}
+
+    def log(i, s, dt):
+        rec[i] = np.array(s)
+        return 0.0
+    eng.solve(log=log, record_every=1, poll=1)
+    return rec
+
+
+@pytest.fixture(scope='module')
+def c3_clean(cuda, orc):
+    from synthetic import make_shard, CONFIGS, SEED
+    c = CONFIGS['C3']
+    sh = make_shard(c['n'], c['p'], c['m'], c['per_col'], seed=SEED)
+    b = sh['Ax'].copy()                                     # noise-free: b = A x*
+    ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], 200, record_every=1)
+    return sh, b, {i: ref[i] for i in (1, 10, 50, 200)}
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('deterministic', [False, True])
+def test_c3_noise_free_iterates_1_10_50_200(c3_clean, deterministic):
+    from device import BBEngine
+    sh, b, ref = c3_clean
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 200, 'opt_tol': 1e-30},
+                   AT=sh['AT'], deterministic=deterministic)
+    rec = _run_engine(eng, 200)
+    for i in (1, 10, 50, 200):
+        assert rel_err(rec[i], ref[i]) < 1e-6, (deterministic, i, rel_err(rec[i], ref[i]))
+
+
+@pytest.mark.timeout(1200)
+def test_c5_noise_free_iterates_1_10(cuda, orc):
+    from synthetic import make_partitioned
+    from device import BBEngine
+    sh = make_partitioned(10_000_000, 500_000, 1_000_000)
+    b = sh['Ax'].copy()
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 10, 'opt_tol': 1e-30},
+                   AT=sh['AT'], colv=sh['colv'])
+    rec = _run_engine(eng, 10)
+    del eng
+    ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], 10, record_every=1)
+    for i in (1, 10):
+        assert rel_err(rec[i], ref[i]) < 1e-6, (i, rel_err(rec[i], ref[i]))
+
+
+# ---- two ranks on the device over C5-density shards (make_partitioned) -------
+
+N5, P5, M5 = 1_200_000, 60_000, 120_000      # C5's routes:links ratio and density
+CHECK5 = (1, 5, 20)
+
+
+def _run5(rank, world, port, out_q):
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    from device import BBEngine
+    from distributed import ShardedBB, torch_all_reduce
+    from synthetic import make_partitioned
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    full = make_partitioned(N5, P5, M5)
+    sh = make_partitioned(N5, P5, M5, rank=rank, world=world)
+    b = full['Ax']
+    x0 = np.zeros(sh['n'])
+    x0[np.cumsum(sh['block_sizes']) - 1] = 1.0
+    part = torch.from_numpy(sh['A'].dot(x0))
+    dist.all_reduce(part)
+    target = torch.from_numpy(part.numpy() - b).cuda()
+    eng = BBEngine(sh['A'], None, sh['block_sizes'], options={'max_iter': 10 ** 9,
+                                                              'opt_tol': 1e-30},
+                   early_exit=False, target=target, AT=sh['AT'], colv=sh['colv'])
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    drv = ShardedBB(eng, torch_all_reduce(), rank=rank)
+    drv.prologue()
+    traj = {}
+    for i in range(1, max(CHECK5) + 1):
+        drv.iterate(i, 1)
+        if i in CHECK5:
+            traj[i] = eng.current_z(i & 1).cpu().numpy().copy()
+    out_q.put((rank, traj, eng.fmt_A, eng.fmt_AT))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_two_rank_c5_density_shards_vs_oracle(cuda, orc):
+    import torch.multiprocessing as mp
+    from synthetic import make_partitioned
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 31200 + (os.getpid() % 500)
+    procs = [ctx.Process(target=_run5, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, traj, fa, fat = q.get(timeout=600)
+        res[r] = traj
+        assert fa == 'tiles' and fat == 'tiles'           # C5's kernels
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = make_partitioned(N5, P5, M5)
+    ref = orc.bb_trace(full['A'], full['Ax'], full['block_sizes'], max(CHECK5),
+                       record_every=1)
+    for i in CHECK5:
+        got = np.concatenate([res[0][i], res[1][i]])
+        assert rel_err(got, ref[i]) < 1e-6, (i, rel_err(got, ref[i]))
