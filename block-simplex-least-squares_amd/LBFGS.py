@@ -7,14 +7,20 @@ On the device the search direction (LBFGS.py:59-71) and the history rotation
 (:75-77) run on csrc/lbfgs.hip (_DeviceHistory): the m pairs live in a ring of
 device slots with their Gram matrices, and one direction is one multi-dot pass,
 one one-wave recursion on the dots and one combine pass -- instead of 2m
-dependent dot products (each a device -> host read) and 2m AXPYs.  The line
-search's decisions (f(pt) >= ..., LBFGS.py:26-53) stay on the host as in the
-reference."""
+dependent dot products (each a device -> host read) and 2m AXPYs.  When the
+closures are a device.BBEngine's, the weak Wolfe line search (LBFGS.py:9-53)
+runs on the device too (device.LineSearch: every trial's projection, f, and
+when Armijo holds the gradient and the curvature test, decided by gated
+kernels; the host reads the state once per chunk of trials), and the rest of
+an iteration -- s, y, y.s, the stopping rule's norms -- costs one more read.
+BSLS_LBFGS_LS=host keeps the line search's decisions on the host (the
+reference's structure) for A/B."""
 import ctypes
 import math
+import os
 import time
 
-from _arr import copy, dot, is_torch, norm
+from _arr import Normed, copy, dot, is_torch, norm
 
 MAX_DEVICE_CORRECTIONS = 127     # bsls_lbfgs_coef
 
@@ -98,6 +104,21 @@ def weak_wolfe_ls(x, d, f, nabla_f, proj=lambda v: v, c1=1e-3, c2=0.9):
             return t
 
 
+def _device_engine(f, nabla_f, proj, x):
+    """The BBEngine whose closures f / nabla_f / proj these are (x on its
+    device), or None -- then the line search runs over the closures."""
+    eng = getattr(f, '__self__', None)
+    if (eng is None or not hasattr(eng, 'line_search') or proj is None
+            or getattr(nabla_f, '__self__', None) is not eng
+            or getattr(proj, '__self__', None) is not eng):
+        return None
+    if not (is_torch(x) and x.is_cuda and x.dim() == 1 and x.numel() == eng.nz):
+        return None
+    if os.environ.get('BSLS_LBFGS_LS', 'device') == 'host':
+        return None
+    return eng
+
+
 def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None, options=None):
     def direction(g_new, y_new, s_new, rho, Y, S):
         q = g_new
@@ -123,6 +144,9 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
     g_new = nabla_f(x)
     y_new, s_new = g_new, zero + 1
     rho_new = 1 / dot(y_new, s_new)
+    eng = _device_engine(f, nabla_f, proj, x)
+    ls = eng.line_search() if eng is not None else None
+    fx_dev = None          # f(x) on the device once x is a projected point
     while not stop:
         i += 1
         if hist is not None:
@@ -133,6 +157,38 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
             Y = Y[1:] + [y_new]
             S = S[1:] + [s_new]
             rho = rho[1:] + [rho_new]
+        if ls is not None and fx_dev is not None:
+            # x = proj(x) (the last x_next) and g_new = nabla_f(x): the line
+            # search's proj(x) / nabla_f(proj(x)) (LBFGS.py:18-19) are these
+            t, why, _, dnorm = ls.search(x, d, g_new, fx_dev)
+            s_new = t * d
+            g = g_new
+            if why == 1:       # accepted: the last trial is x_next
+                x_next, g_new, fx_dev = ls.take()
+            else:              # t was never evaluated (the two other exits)
+                x_next = proj(x + s_new)
+                g_new = nabla_f(x_next)
+                fx_dev = None
+            y_new = g_new - g
+            import torch
+            vals = torch.stack([y_new.dot(s_new), g_new.dot(g_new),
+                                fx_dev[0] if fx_dev is not None else g_new.new_zeros(())]).cpu()
+            ys, gg = float(vals[0]), float(vals[1])
+            fx = float(vals[2]) if fx_dev is not None else f(x_next)
+            if ys == 0:
+                print('iter=%d, f=%8.5e' % (i, fx))
+                print('Exiting... no change in gradient')
+                break
+            rho_new = 1 / ys
+            x = x_next
+            fx_dev = g_new.new_tensor([fx]) if fx_dev is None else fx_dev
+            if math.isnan(fx):
+                raise ArithmeticError('objective function evaluates to NaN')
+            stop = stopping(Normed(g_new, math.sqrt(gg)), fx, i, t, d=Normed(d, dnorm),
+                            options=options)
+            if i % record_every == 0:
+                start = log(i, copy(x), time.time() - start)
+            continue
         t = weak_wolfe_ls(x, d, f, nabla_f, proj=proj or (lambda v: v))
         s_new = t * d
         x_next = x + s_new
@@ -151,6 +207,8 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
         fx = f(x)
         if math.isnan(fx):
             raise ArithmeticError('objective function evaluates to NaN')
+        if ls is not None:
+            fx_dev = x.new_tensor([fx])      # x is proj(x + s): the device search can take over
         stop = stopping(g_new, fx, i, t, d=d, options=options)
         if i % record_every == 0:
             start = log(i, copy(x), time.time() - start)

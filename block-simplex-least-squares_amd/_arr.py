@@ -11,7 +11,22 @@ def is_torch(a):
     return isinstance(a, torch.Tensor)
 
 
+class Normed:
+    """A vector whose norm is already known on the host (the device L-BFGS
+    loop reads it with its other scalars): norm(v) is that value, and t * v
+    (solvers.stopping's step test) keeps |t| times it, without a device read."""
+    __slots__ = ('v', 'bsls_norm')
+
+    def __init__(self, v, n):
+        self.v, self.bsls_norm = v, float(n)
+
+    def __rmul__(self, t):
+        return Normed(None, abs(float(t)) * self.bsls_norm)
+
+
 def norm(a):
+    if isinstance(a, Normed):
+        return a.bsls_norm
     if is_torch(a):
         return float(a.norm())
     return float(np.linalg.norm(a))

@@ -92,6 +92,19 @@ DORE_NC, DORE_EE, DORE_A1, DORE_A2, DORE_SEL, DORE_STOPIT = range(6)
 DORE_COUNT = 16
 
 
+class LsState(ctypes.Structure):
+    """Mirror of bsls_ls_state (include/bsls_hip.h): LBFGS.solve's line search."""
+    _fields_ = [('x', _vp), ('d', _vp), ('gx', _vp), ('pt', _vp), ('gpt', _vp), ('zero', _vp),
+                ('fx', _vp), ('st', _vp), ('S1', _vp), ('S2', _vp), ('part', _vp),
+                ('tickets', _vp), ('c1', _dbl), ('c2', _dbl)]
+
+
+LS_T, LS_LO, LS_HI, LS_STOP, LS_SLOPE, LS_FX, LS_DNORM, LS_NTRIAL, LS_TLAST, LS_FT, LS_DGT = \
+    range(11)
+LS_COUNT = 16
+LS_ACCEPTED, LS_BRACKET, LS_SMALL = 1, 2, 3
+
+
 class CSR(ctypes.Structure):
     """Mirror of struct bsls_csr (include/bsls_hip.h)."""
     _fields_ = [('rows', _i64), ('indptr', _vp), ('indices', _vp), ('data', _vp),
@@ -170,6 +183,10 @@ _SIGS = {
     'bsls_dore_iterate': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(DoreState), _i64,
                                  _i64, _vp]),
     'bsls_bb_stage': (_int, [ctypes.POINTER(BBProblem), _int, _i64, _vp]),
+    'bsls_lbfgs_ls_work_size': (_sz, [_i64]),
+    'bsls_lbfgs_ls_begin': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(LsState), _vp]),
+    'bsls_lbfgs_ls_trials': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(LsState), _i64,
+                                    _vp]),
     'bsls_comm_id_bytes': (_sz, []),
     'bsls_comm_unique_id': (_int, [_vp]),
     'bsls_comm_create': (_int, [_vp, _int, _int, ctypes.POINTER(_vp)]),

@@ -973,44 +973,49 @@ static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, h
     }
 }
 
+// (dz: the vector the ITER sums dot with delta_g -- the workspace's z - z_prev
+// unless given: the line search passes its direction d, with g_prev = 0)
 template <int MODE, bool ITER, bool FUSE>
 static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *gout,
-                           const BBWork &w, hipStream_t st, int64_t iter) {
+                           const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
     allow_lds(bb_k2<MODE, ITER, FUSE>);
     bb_k2<MODE, ITER, FUSE><<<grid_for(P.AT.npanels, PANEL_WAVES), 1024, panel_lds_bytes(P.AT),
-                              st>>>(P, w.dz, gp, gout, w.p2, w.tk2, iter);
+                              st>>>(P, dz, gp, gout, w.p2, w.tk2, iter);
 }
 
 template <int MODE, bool ITER, bool FUSE, int CV>
 static void launch_k2t_cv(const bsls_bb_problem &P, const double *gp, double *gout,
-                          const BBWork &w, hipStream_t st, int64_t iter) {
+                          const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
     allow_lds(bb_k2t<MODE, ITER, FUSE, CV>);
     bb_k2t<MODE, ITER, FUSE, CV><<<(int)(P.ATt.nrb * P.ATt.ngroups), BSLS_TILE_THREADS,
                                    tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(
-        P, w.dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter);
+        P, dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter);
 }
 
 template <int MODE, bool ITER, bool FUSE>
 static void launch_k2t_mode(const bsls_bb_problem &P, const double *gp, double *gout,
-                            const BBWork &w, hipStream_t st, int64_t iter) {
-    if (MODE != 1 && P.colv_codec == 2) launch_k2t_cv<MODE, ITER, FUSE, 2>(P, gp, gout, w, st, iter);
+                            const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
+    if (MODE != 1 && P.colv_codec == 2)
+        launch_k2t_cv<MODE, ITER, FUSE, 2>(P, gp, gout, w, st, iter, dz);
     else if (MODE != 1 && P.colv_codec == 1)
-        launch_k2t_cv<MODE, ITER, FUSE, 1>(P, gp, gout, w, st, iter);
-    else launch_k2t_cv<MODE, ITER, FUSE, 0>(P, gp, gout, w, st, iter);
+        launch_k2t_cv<MODE, ITER, FUSE, 1>(P, gp, gout, w, st, iter, dz);
+    else launch_k2t_cv<MODE, ITER, FUSE, 0>(P, gp, gout, w, st, iter, dz);
 }
 
 template <bool ITER, bool FUSE = false>
 static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
-                      const BBWork &w, hipStream_t st, int64_t iter = 0) {
+                      const BBWork &w, hipStream_t st, int64_t iter = 0,
+                      const double *dz = nullptr) {
+    if (!dz) dz = w.dz;
     if (P.ATt.ent) {
-        if (!P.colv) launch_k2t_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter);
+        if (!P.colv) launch_k2t_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
         else if (P.ATt.ngroups == 1 && P.ATt.layout == 0)
-            launch_k2t_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter);
-        else launch_k2t_mode<3, ITER, FUSE>(P, gp, gout, w, st, iter);
+            launch_k2t_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
+        else launch_k2t_mode<3, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
     } else if (P.colv) {
-        launch_k2_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter);
+        launch_k2_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
     } else {
-        launch_k2_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter);
+        launch_k2_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
     }
 }
 
@@ -1085,6 +1090,94 @@ static int check_problem(const bsls_bb_problem *p) {
     if (p->long_packs && (p->nlong < 0 || (p->nlong > 0 && (!p->long_off || !p->long_scratch))))
         return BSLS_E_ARG;
     return BSLS_OK;
+}
+
+// ---- LBFGS.solve's weak Wolfe line search on the device -------------------------
+// (python/LBFGS.py:9-53; include/bsls_hip.h bsls_lbfgs_ls_*).  One trial =
+//   K3 on S1:  pt = clip01(PAVA(x - (-t) d)) = proj(x + t d) (the reference's
+//              roundings: (-t) d = -(t d)), x_engine = colv N pt
+//   K1 on S1:  r = A x + target, S1[FX] = f(pt)
+//   armijo:    f(pt) >= fx + c1 t slope -> beta = t, t = (alpha + beta) / 2;
+//              else open S2 for the curvature test
+//   K2 on S2:  g(pt) = N'A'r -> gpt; the sums with g_prev = 0 and dz = d give
+//              S2[DZDG] = d . g(pt)
+//   curvature: d . g(pt) < c2 slope -> alpha = t, t = 2 alpha or (alpha +
+//              beta) / 2; else accepted
+// then the reference's two exits (|alpha - beta| <= 1e-14, ||t d|| <= 1e-8,
+// the norm as |t| ||d||).  Every kernel of a trial is gated by the state, so
+// the host enqueues trials in chunks and reads the state once per chunk.
+// st[]: BSLS_LS_* slots.
+__device__ __forceinline__ void ls_stop(double *st, double *S1, double *S2, double why) {
+    st[BSLS_LS_STOP] = why;
+    S1[BSLS_S_STOP] = 1.0;
+    S2[BSLS_S_STOP] = 1.0;
+}
+
+// the exits after a new t (LBFGS.py:45-49), else the next trial's K3 step
+__device__ __forceinline__ void ls_next(double *st, double *S1, double *S2, double tn) {
+    st[BSLS_LS_T] = tn;
+    if (fabs(st[BSLS_LS_LO] - st[BSLS_LS_HI]) <= 1e-14) ls_stop(st, S1, S2, BSLS_LS_BRACKET);
+    else if (fabs(tn) * st[BSLS_LS_DNORM] <= 1e-8) ls_stop(st, S1, S2, BSLS_LS_SMALL);
+    else S1[BSLS_S_DZDG] = -tn;
+}
+
+__global__ __launch_bounds__(256) void ls_begin_kernel(const double *__restrict__ d,
+                                                       const double *__restrict__ gx, int64_t nz,
+                                                       const double *__restrict__ fx, double *st,
+                                                       double *S1, double *S2, double *part,
+                                                       unsigned *tickets) {
+    __shared__ double red[2 * 4];
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    double v[2] = {0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nz; i += gs) {
+        const double di = d[i];
+        v[0] += di * gx[i];
+        v[1] += di * di;
+    }
+    block_sum<2>(v, red);
+    double tot[2];
+    if (last_block_sum<2>(v, part, tickets, tot, red) && threadIdx.x == 0) {
+        for (int k = 0; k < BSLS_LS_COUNT; ++k) st[k] = 0.0;
+        for (int k = 0; k < BSLS_S_COUNT; ++k) S1[k] = S2[k] = 0.0;
+        st[BSLS_LS_T] = 1.0;
+        st[BSLS_LS_HI] = INFINITY;
+        st[BSLS_LS_SLOPE] = tot[0];
+        st[BSLS_LS_DNORM] = sqrt(tot[1]);
+        st[BSLS_LS_FX] = *fx;
+        S1[BSLS_S_SUMDG] = 1.0;      // K3's t = S1[DZDG] / S1[DGDG] = -t
+        S1[BSLS_S_DZDG] = -1.0;
+        S1[BSLS_S_DGDG] = 1.0;
+        S2[BSLS_S_STOP] = 1.0;
+    }
+}
+
+__global__ void ls_armijo_kernel(double *st, double *S1, double *S2, double c1) {
+    if (threadIdx.x != 0 || st[BSLS_LS_STOP] != 0.0) return;
+    const double t = st[BSLS_LS_T], ft = S1[BSLS_S_FX];
+    st[BSLS_LS_NTRIAL] += 1.0;
+    st[BSLS_LS_TLAST] = t;
+    st[BSLS_LS_FT] = ft;
+    if (ft >= st[BSLS_LS_FX] + c1 * t * st[BSLS_LS_SLOPE]) {   // Armijo violated (LBFGS.py:26)
+        st[BSLS_LS_HI] = t;
+        S2[BSLS_S_STOP] = 1.0;
+        ls_next(st, S1, S2, 0.5 * (st[BSLS_LS_LO] + t));
+    } else {
+        S2[BSLS_S_STOP] = 0.0;     // the curvature test needs g(pt)
+    }
+}
+
+__global__ void ls_curv_kernel(double *st, double *S1, double *S2, double c2) {
+    if (threadIdx.x != 0 || st[BSLS_LS_STOP] != 0.0 || S2[BSLS_S_STOP] != 0.0) return;
+    const double t = st[BSLS_LS_T];
+    S2[BSLS_S_STOP] = 1.0;
+    st[BSLS_LS_DGT] = S2[BSLS_S_DZDG];
+    if (S2[BSLS_S_DZDG] < c2 * st[BSLS_LS_SLOPE]) {            // curvature violated (:33)
+        st[BSLS_LS_LO] = t;
+        const double hi = st[BSLS_LS_HI];
+        ls_next(st, S1, S2, (hi == INFINITY) ? 2 * t : 0.5 * (t + hi));
+    } else {
+        ls_stop(st, S1, S2, BSLS_LS_ACCEPTED);                  // both conditions pass (:39)
+    }
 }
 
 // ---- DORE on the fused images (include/bsls_hip.h bsls_dore_iterate) --------
@@ -1297,6 +1390,56 @@ extern "C" int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state
         launch_k1<false, false, true>(P2, i, w, st);
         dore_sel<<<gm, 256, 0, st>>>(P2, D);
         dore_copy<<<gb, 256, 0, st>>>(P2, D, xn, axo);
+        BSLS_LAUNCH_CHECK();
+    }
+    return BSLS_OK;
+}
+
+extern "C" size_t bsls_lbfgs_ls_work_size(int64_t nz) {
+    return (size_t)(((nz > 0 ? nz : 1) + 255) / 256 + 1) * 2 * sizeof(double);
+}
+
+static int check_ls(const bsls_ls_state *s) {
+    if (!s || !s->x || !s->d || !s->gx || !s->pt || !s->gpt || !s->zero || !s->fx || !s->st ||
+        !s->S1 || !s->S2 || !s->part || !s->tickets)
+        return BSLS_E_ARG;
+    return BSLS_OK;
+}
+
+extern "C" int bsls_lbfgs_ls_begin(const bsls_bb_problem *p, const bsls_ls_state *s, void *stream) {
+    int rc = check_problem(p);
+    if (rc != BSLS_OK || (rc = check_ls(s)) != BSLS_OK) return rc;
+    constexpr int LS_GRID = 512;
+    const int g = grid_for(p->nz, 256);
+    ls_begin_kernel<<<g < LS_GRID ? g : LS_GRID, 256, 0, (hipStream_t)stream>>>(
+        s->d, s->gx, p->nz, s->fx, s->st, s->S1, s->S2, s->part, s->tickets);
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" int bsls_lbfgs_ls_trials(const bsls_bb_problem *p, const bsls_ls_state *s,
+                                    int64_t count, void *stream) {
+    int rc = check_problem(p);
+    if (rc != BSLS_OK || (rc = check_ls(s)) != BSLS_OK) return rc;
+    if (count < 0) return BSLS_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const BBWork w = bb_layout(*p);
+    // the trial's problems: S1 gates K3 / K1 (and takes f), S2 gates K2; no
+    // stopping rule of their own (max_iter unreachable, no early exits)
+    bsls_bb_problem P1 = *p, P2 = *p;
+    P1.scal = s->S1;
+    P2.scal = s->S2;
+    P1.max_iter = P2.max_iter = INT64_MAX;
+    P1.early_exit = P2.early_exit = 0;
+    for (int64_t k = 0; k < count; ++k) {
+        launch_k3(P1, 1, s->x, s->d, s->pt, w, st);
+        BSLS_LAUNCH_CHECK();
+        launch_k1<true, true, true>(P1, 1, w, st);
+        BSLS_LAUNCH_CHECK();
+        ls_armijo_kernel<<<1, 64, 0, st>>>(s->st, s->S1, s->S2, s->c1);
+        launch_k2<true>(P2, s->zero, s->gpt, w, st, 1, s->d);
+        BSLS_LAUNCH_CHECK();
+        ls_curv_kernel<<<1, 64, 0, st>>>(s->st, s->S1, s->S2, s->c2);
         BSLS_LAUNCH_CHECK();
     }
     return BSLS_OK;

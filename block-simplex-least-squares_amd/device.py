@@ -727,6 +727,60 @@ def iso_plan(starts_h, n):
     return plan
 
 
+class LineSearch:
+    """LBFGS.solve's weak Wolfe line search (python/LBFGS.py:9-53) on a BBEngine,
+    decided on the device (bsls_lbfgs_ls_begin / _trials): trials enqueued in
+    chunks, the state read once per chunk.  search() returns (t, exit, trials,
+    ||d||); after the accepted exit take() gives x_next, nabla_f(x_next) and
+    f(x_next)."""
+
+    CHUNK = 4
+
+    def __init__(self, eng, c1=1e-3, c2=0.9):
+        torch = _torch()
+        L = _native.lib()
+        nz = eng.nz
+        f64 = dict(dtype=torch.float64, device='cuda')
+        self.eng = eng
+        self.pt = torch.empty(nz, **f64)
+        self.gpt = torch.empty(nz, **f64)
+        self.zero = torch.zeros(nz, **f64)
+        self.fx = torch.zeros(1, **f64)
+        self.st = torch.zeros(_native.LS_COUNT, **f64)
+        self.S = torch.zeros(2, _native.S_COUNT, **f64)
+        self.part = torch.zeros(max(1, L.bsls_lbfgs_ls_work_size(nz) // 8), **f64)
+        self.tickets = torch.zeros(max(1, L.bsls_ticket_bytes() // 4), dtype=torch.int32,
+                                   device='cuda')
+        self.c1, self.c2 = float(c1), float(c2)
+
+    def _state(self, x, d, gx, fx):
+        return _native.LsState(x.data_ptr(), d.data_ptr(), gx.data_ptr(), self.pt.data_ptr(),
+                               self.gpt.data_ptr(), self.zero.data_ptr(), fx.data_ptr(),
+                               self.st.data_ptr(), self.S[0].data_ptr(), self.S[1].data_ptr(),
+                               self.part.data_ptr(), self.tickets.data_ptr(), self.c1, self.c2)
+
+    def search(self, x, d, gx, fx):
+        """x (projected), d, gx = nabla_f(x): contiguous device vectors of nz;
+        fx: f(x) as a one-element device tensor.  Returns (t, exit, trials,
+        ||d||) after one host read per chunk of trials."""
+        L = _native.lib()
+        S = self._state(x, d, gx, fx)
+        P = self.eng.P
+        check(L.bsls_lbfgs_ls_begin(P, S, stream_handle()), 'bsls_lbfgs_ls_begin')
+        while True:
+            check(L.bsls_lbfgs_ls_trials(P, S, self.CHUNK, stream_handle()), 'bsls_lbfgs_ls_trials')
+            st = self.st.cpu().numpy()
+            if st[_native.LS_STOP] != 0:
+                return (float(st[_native.LS_T]), int(st[_native.LS_STOP]),
+                        int(st[_native.LS_NTRIAL]), float(st[_native.LS_DNORM]))
+
+    def take(self):
+        """(x_next, nabla_f(x_next), f(x_next) as a one-element device tensor)
+        of the accepted trial, as new tensors."""
+        return (self.pt.clone(), self.gpt.clone(),
+                self.S[0][_native.S_FX:_native.S_FX + 1].clone())
+
+
 class BlockLayout:
     """Block structure of x (sizes k_b) and of z (sizes k_b - 1), on device."""
 
@@ -1064,6 +1118,13 @@ class BBEngine:
         self.stage(7, 0)
         self.stage(3, 0)
         return self.g[0][:self.nz].clone()
+
+    def line_search(self):
+        """This engine's device weak Wolfe line search (LBFGS.solve)."""
+        ls = getattr(self, '_ls', None)
+        if ls is None:
+            ls = self._ls = LineSearch(self)
+        return ls
 
     def apply_A_x(self, x):
         """A x for an x-space vector (LS_postprocess's A x_true)."""

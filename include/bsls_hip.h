@@ -401,6 +401,45 @@ int64_t bsls_bb_row_blocks(const bsls_bb_problem *p, int64_t *rows_per_block);
 int bsls_bb_residual_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
                           void *stream);
 
+/* ---- LBFGS.solve's weak Wolfe line search on the device ----------------------
+ * Replaces weak_wolfe_ls (python/LBFGS.py:9-53) over main.solve_in_z's
+ * closures: trial t from 1 by the reference's bisection/doubling, each trial
+ * pt = proj(x + t d) (K3: PAVA v1 + clip), f(pt) (K1), the Armijo test
+ * f(pt) >= fx + c1 t d.gx, and when it holds g(pt) (K2) and the curvature
+ * test d.g(pt) < c2 d.gx; exits as the reference (both hold; |alpha - beta|
+ * <= 1e-14; ||t d|| <= 1e-8, taken as |t| ||d||).  Every launch of a trial is
+ * gated by the state, so trials enqueued past the exit are no-ops: the host
+ * enqueues a few, reads st[] once, enqueues more if needed.  On the accepted
+ * exit pt / gpt / S1[FX] are x_next, nabla_f(x_next), f(x_next); after the
+ * other two st[T] was never evaluated.  Uses the engine problem's x, r, g and
+ * workspace as scratch (its BB state is not kept). */
+enum {
+    BSLS_LS_T = 0, BSLS_LS_LO = 1, BSLS_LS_HI = 2,  /* t, alpha, beta */
+    BSLS_LS_STOP = 3,      /* 0 searching, else BSLS_LS_ACCEPTED / BRACKET / SMALL */
+    BSLS_LS_SLOPE = 4,     /* d . gx */
+    BSLS_LS_FX = 5,        /* f(x) */
+    BSLS_LS_DNORM = 6,     /* ||d|| */
+    BSLS_LS_NTRIAL = 7,    /* trials evaluated */
+    BSLS_LS_TLAST = 8, BSLS_LS_FT = 9, BSLS_LS_DGT = 10,   /* last trial: t, f(pt), d.g(pt) */
+    BSLS_LS_COUNT = 16
+};
+enum { BSLS_LS_ACCEPTED = 1, BSLS_LS_BRACKET = 2, BSLS_LS_SMALL = 3 };
+typedef struct {
+    const double *x, *d, *gx;   /* nz each: point (projected), direction, nabla_f(x) */
+    double *pt, *gpt;           /* nz each: the trial point and its gradient */
+    const double *zero;         /* nz zeros */
+    const double *fx;           /* f(x), one device double */
+    double *st;                 /* BSLS_LS_COUNT doubles */
+    double *S1, *S2;            /* BSLS_S_COUNT doubles each */
+    double *part;               /* bsls_lbfgs_ls_work_size(nz) bytes */
+    unsigned *tickets;          /* bsls_ticket_bytes() zeroed bytes */
+    double c1, c2;              /* 1e-3, 0.9 in the reference */
+} bsls_ls_state;
+size_t bsls_lbfgs_ls_work_size(int64_t nz);
+int bsls_lbfgs_ls_begin(const bsls_bb_problem *p, const bsls_ls_state *s, void *stream);
+int bsls_lbfgs_ls_trials(const bsls_bb_problem *p, const bsls_ls_state *s, int64_t count,
+                         void *stream);
+
 /* ---- multi-GPU: one rank's column-sharded iterations, RCCL in the loop ----
  * The reference has no parallel code; this is the driver of
  * distributed.ShardedBB (python) moved to C++ so no Python runs per

@@ -286,6 +286,86 @@ def test_lbfgs_60_iterations_vs_reference(cuda, golden):
     assert rel(states[-1], G['gd_states'][-1]) < 1e-6
 
 
+@pytest.mark.parametrize('max_iter', [1, 2, 40])
+def test_lbfgs_device_line_search_vs_closures(cuda, monkeypatch, max_iter):
+    """LBFGS.solve with the weak Wolfe line search on the device
+    (device.LineSearch: gated trials, the state read once per chunk of 4)
+    against the same solve with the search's decisions on the host over the
+    engine's closures (BSLS_LBFGS_LS=host): every logged iterate within 1e-8
+    (dot products round in other orders), the same iterations logged, on a
+    60k-route problem where the search bisects (Armijo failures) and doubles
+    (curvature failures) -- both branches are checked to occur."""
+    import torch
+    import LBFGS
+    import solvers
+    from device import BBEngine
+    from synthetic import make_shard, add_noise
+    sh = make_shard(60000, 3000, 8000, per_col=16, seed=3)
+    b = add_noise(sh['Ax'], 0.02, seed=3)
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], AT=sh['AT'])
+    opts = {'max_iter': max_iter, 'verbose': 0, 'opt_tol': 1e-30}
+
+    def run(mode):
+        monkeypatch.setenv('BSLS_LBFGS_LS', mode)
+        rec = {}
+
+        def log(i, s, dt):
+            rec[i] = s.detach().cpu().numpy().copy()
+            return 0.0
+        z0 = torch.ones(eng.nz, dtype=torch.float64, device='cuda')
+        LBFGS.solve(z0, eng.f, eng.nabla_f, solvers.stopping, record_every=1, proj=eng.proj,
+                    log=log, options=dict(opts))
+        return rec
+    dev = run('device')
+    host = run('host')
+    assert sorted(dev) == sorted(host) == list(range(max_iter + 1))
+    for i in dev:
+        assert rel(dev[i], host[i]) < 1e-8, (i, rel(dev[i], host[i]))
+    if max_iter >= 2:
+        ls = eng.line_search()
+        # the last search ran on the device and evaluated at least one trial
+        st = ls.st.cpu().numpy()
+        assert st[7] >= 1 and st[3] != 0
+
+
+def test_lbfgs_line_search_kernels_vs_reference_ls(cuda, orc):
+    """One device search against the reference's weak_wolfe_ls (the oracle's
+    restatement, LBFGS.py:9-53) from the same point and direction, on
+    directions that force the three exits' paths: a descent direction (accept,
+    maybe after bisection), a scaled-up one (Armijo failures first), a
+    scaled-down one (curvature failures: doubling).  Same t, same exit."""
+    import torch
+    import _native
+    from device import BBEngine
+    from synthetic import make_shard, add_noise
+    sh = make_shard(20000, 1000, 3000, per_col=8, seed=5)
+    b = add_noise(sh['Ax'], 0.02, seed=5)
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], AT=sh['AT'])
+    P = orc.solve_in_z_parts(sh['A'], b, sh['block_sizes'])
+    rs = np.random.RandomState(7)
+    x = P['proj'](rs.rand(eng.nz))
+    gx = P['nabla_f'](x)
+    ls = eng.line_search()
+    seen = set()
+    for scale in (1e-3, 1e-1, 1.0, 10.0, 1e-5):
+        d = -scale * gx / max(1.0, np.abs(gx).max()) + 1e-3 * scale * rs.randn(eng.nz)
+        t_ref = orc.weak_wolfe_ls(x, d, P['f'], P['nabla_f'], proj=P['proj'])
+        xd = torch.from_numpy(x.copy()).cuda()
+        dd = torch.from_numpy(d.copy()).cuda()
+        gd = eng.nabla_f(xd)
+        fx = torch.tensor([eng.f(xd)], dtype=torch.float64, device='cuda')
+        t, why, ntr, dn = ls.search(xd, dd, gd, fx)
+        assert abs(t - t_ref) <= 1e-12 * max(1.0, abs(t_ref)), (scale, t, t_ref)
+        seen.add((why, ntr > 1))
+        if why == _native.LS_ACCEPTED:
+            xn, gn, fn = ls.take()
+            want = P['proj'](x + t_ref * d)
+            assert rel(xn.cpu().numpy(), want) < 1e-12
+            assert rel(gn.cpu().numpy(), P['nabla_f'](want)) < 1e-10
+            assert abs(float(fn) - P['f'](want)) <= 1e-10 * max(1.0, abs(P['f'](want)))
+    assert any(w == _native.LS_ACCEPTED for w, _ in seen)
+
+
 @pytest.mark.parametrize('m,pushes', [(1, 3), (5, 3), (5, 12), (50, 70), (64, 66), (70, 75), (100, 103)])
 def test_lbfgs_device_history_direction(cuda, m, pushes):
     """_DeviceHistory.direction / push (csrc/lbfgs.hip: multi-dot, one-wave
