@@ -21,8 +21,12 @@ struct LsqWork {
     unsigned *tk;       // ||r||^2 hand-off
     unsigned *tkrb;     // one ticket per row block
     double *part;       // one partial per row block
+    unsigned *tkm;      // fixed-point residual: max|x| hand-off
+    double *mpart;      //   its partials (LSQ_MAX_GRID)
+    double *xmax;       //   max |x| (of colv * x with a scaled incidence)
     size_t bytes;
 };
+constexpr int LSQ_MAX_GRID = 512;
 
 static size_t lal(size_t v) { return (v + 255) & ~(size_t)255; }
 
@@ -37,8 +41,36 @@ static LsqWork lsq_layout(void *base, int64_t A_npanels) {
     off += lal((size_t)rbs * 4);
     w.part = (double *)(p + off);
     off += lal((size_t)rbs * 8);
+    w.tkm = (unsigned *)(p + off);
+    off += lal(TICKET_BYTES);
+    w.mpart = (double *)(p + off);
+    off += lal((size_t)LSQ_MAX_GRID * 8);
+    w.xmax = (double *)(p + off);
+    off += lal(8);
     w.bytes = off;
     return w;
+}
+
+// max |x| over n entries (with colv: of xs = colv * x, written on the way), by
+// the last arriving workgroup in a fixed order (deterministic, like the sums)
+__global__ __launch_bounds__(256) void lsq_xmax_kernel(double *__restrict__ xs,
+                                                       const double *__restrict__ colv,
+                                                       const double *__restrict__ x, int64_t n,
+                                                       double *mpart, unsigned *ticket,
+                                                       double *xmax) {
+    __shared__ double red[4];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    double mx[1] = {0.0};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double v = x[i];
+        if (colv) {
+            v = colv[i] * v;
+            xs[i] = v;
+        }
+        mx[0] = nan_max(mx[0], fabs(v));
+    }
+    double tot[1];
+    if (last_block_reduce<1, 1u>(mx, mpart, ticket, tot, red) && threadIdx.x == 0) *xmax = tot[0];
 }
 
 __global__ __launch_bounds__(256) void lsq_scale_kernel(double *__restrict__ xs,
@@ -165,6 +197,38 @@ __global__ __launch_bounds__(1024) void lsq_k1t(bsls_tiles T, int64_t m,
         rpart[g * m + row] = lds[row - r0];
 }
 
+// The same in 64-bit fixed point (bsls_lsq_op.fixed): the scale 2^k puts
+// every term within +-2^50 (|term| <= fx_amax * max|x|, max|x| from
+// lsq_xmax_kernel), the integer row sums are order-free, so r -- and f --
+// repeat bit for bit at the same x (the exits of the x-space solvers need
+// that), at the dealt walk's speed.  Two words (tiles.hpp fx_add): each term
+// rounds by at most 2^-101 (fx_amax max|x|), the sum converts back once.
+template <int MODE>
+__global__ __launch_bounds__(1024) void lsq_k1t_fx(bsls_tiles T, int64_t m,
+                                                   const double *__restrict__ x,
+                                                   double *__restrict__ rpart,
+                                                   const double *__restrict__ xmax, double amax) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    int64_t rb, g;
+    tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, g);
+    const double B = amax * *xmax;
+    int ex = 0;
+    if (B > 0.0 && B <= 1.7976931348623157e308) (void)frexp(B, &ex);
+    const double fxs = ldexp(1.0, 50 - ex), inv = ldexp(1.0, ex - 50);
+    const int HR = (int)tile_lds_doubles(T, true);   // two words per row
+    for (int i = threadIdx.x; i < HR; i += blockDim.x) lds[i] = 0.0;   // integer 0 too
+    __syncthreads();
+    tile_walk_any<MODE, true>(T, rb, g, x, lds, nullptr, fxs);
+    __syncthreads();
+    const int lo_off = (int)(T.H + T.halo + 1);
+    const int64_t r0 = rb * T.H, r1 = (r0 + T.H < m) ? r0 + T.H : m;
+    // a NaN / inf in x (no finite scale): the rows are NaN, as a float sum
+    // would make them (the solvers' NaN checks must still see it)
+    const bool bad = !(B <= 1.7976931348623157e308);
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+        rpart[g * m + row] = bad ? __builtin_nan("") : fx_value(lds, (int)(row - r0), lo_off, inv);
+}
+
 __global__ __launch_bounds__(256) void lsq_t_sum(int64_t m, int64_t G, const double *rpart,
                                                  const double *__restrict__ add,
                                                  double *__restrict__ r, double *sq_out,
@@ -236,7 +300,9 @@ static bool lsq_ok(const bsls_lsq_op *op) {
     }
     if (op->At.ent) {
         const bsls_tiles &K = op->At;
-        if (!tiles_valid(K, op->m, op->n, 0, op->colv == nullptr, false, LSQ_LDS_MAX)) return false;
+        // (the fixed-point walk keeps two words per row: twice the LDS)
+        if (!tiles_valid(K, op->m, op->n, 0, op->colv == nullptr, op->fixed != 0, LSQ_LDS_MAX))
+            return false;
         if ((K.layout & 3) == 0) return false;
         if ((op->colv == nullptr) != (K.val != nullptr)) return false;
     } else {
@@ -244,6 +310,9 @@ static bool lsq_ok(const bsls_lsq_op *op) {
         if (A.prow < 1 || A.prow > BSLS_PANEL_ROWS) return false;
     }
     if (!op->rpart || !op->work) return false;
+    if (op->fixed && (!op->At.ent || (op->At.layout & 3) == 0 || !(op->fx_amax > 0.0) ||
+                      op->fx_amax > 1e300 || (op->colv && !op->xs)))
+        return false;
     if (op->colv && !op->xs) return false;
     if (!op->ATt.ent && (op->colv ? T.val != nullptr : !T.val)) return false;
     if (!op->At.ent && (op->colv ? A.val != nullptr : !A.val)) return false;
@@ -267,6 +336,31 @@ extern "C" int bsls_lsq_residual(const bsls_lsq_op *op, const double *d_x, const
     LsqWork w = lsq_layout(op->work, op->At.ent ? LSQ_SUM_GRID * PANEL_WAVES : op->A.npanels);
     if (op->work_bytes < w.bytes) return BSLS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
+    if (op->At.ent && op->fixed) {
+        const bsls_tiles &K = op->At;
+        const int gm0 = grid_for(op->n, 256);
+        lsq_xmax_kernel<<<gm0 < LSQ_MAX_GRID ? gm0 : LSQ_MAX_GRID, 256, 0, st>>>(
+            op->xs, op->colv, d_x, op->n, w.mpart, w.tkm, w.xmax);
+        BSLS_LAUNCH_CHECK();
+        const double *xin = op->colv ? op->xs : d_x;
+        const int grid = (int)(K.nrb * K.ngroups);
+        const size_t lds = tile_lds_doubles(K, true) * 8;
+        if (op->colv) {
+            lsq_allow_lds(lsq_k1t_fx<0>);
+            lsq_k1t_fx<0><<<grid, BSLS_TILE_THREADS, lds, st>>>(K, op->m, xin, op->rpart, w.xmax,
+                                                               op->fx_amax);
+        } else {
+            lsq_allow_lds(lsq_k1t_fx<1>);
+            lsq_k1t_fx<1><<<grid, BSLS_TILE_THREADS, lds, st>>>(K, op->m, xin, op->rpart, w.xmax,
+                                                               op->fx_amax);
+        }
+        BSLS_LAUNCH_CHECK();
+        const int gk = grid_for(op->m, 256);
+        lsq_t_sum<<<gk < LSQ_SUM_GRID ? gk : LSQ_SUM_GRID, 256, 0, st>>>(
+            op->m, K.ngroups, op->rpart, d_add, d_r, d_sq_out, w.part, w.tk);
+        BSLS_LAUNCH_CHECK();
+        return BSLS_OK;
+    }
     if (op->At.ent) {
         const bsls_tiles &K = op->At;
         const double *xin = d_x;

@@ -210,10 +210,38 @@ __device__ __forceinline__ void tile_vals4(const double *__restrict__ val, int64
     }
 }
 
-template <int MODE, bool NT, bool PK3 = false, int VT = 0, int P = BSLS_TILE_P, int D = BSLS_TILE_D>
+// FX: the row sums in two-word fixed point instead (order-free: integer
+// adds commute, so a row's sum is the same bits whatever order the atomics
+// land in).  fxs = 2^k puts every term * fxs within [-2^50, 2^50]; the high
+// word takes it rounded to an integer (the 1.5 * 2^52 trick: one add, one
+// 64-bit subtract), the low word the exact remainder scaled by 2^50 and
+// rounded: 100 bits below the bound, two ds_add_u64 per entry.  The low
+// words sit H + halo + 1 slots after the high ones (twice the LDS).
+constexpr double FX_MAGIC = 6755399441055744.0;   // 1.5 * 2^52: ulp 1 over +-2^51
+
+__device__ __forceinline__ void fx_add(double *rows, int lr, int lo_off, double v) {
+    const double t = v + FX_MAGIC;
+    const double h = t - FX_MAGIC;                  // v rounded to an integer, exactly
+    const double l = (v - h) * 0x1p50;              // |v - h| <= 1/2: exact, then scaled
+    const double tl = l + FX_MAGIC;
+    atomicAdd(reinterpret_cast<unsigned long long *>(&rows[lr]),
+              (unsigned long long)(__double_as_longlong(t) - __double_as_longlong(FX_MAGIC)));
+    atomicAdd(reinterpret_cast<unsigned long long *>(&rows[lr + lo_off]),
+              (unsigned long long)(__double_as_longlong(tl) - __double_as_longlong(FX_MAGIC)));
+}
+
+// a row's two words back to a double: hi 2^-k + lo 2^-(k+50)
+__device__ __forceinline__ double fx_value(const double *rows, int lr, int lo_off, double inv) {
+    const long long hi = reinterpret_cast<const long long *>(rows)[lr];
+    const long long lo = reinterpret_cast<const long long *>(rows)[lr + lo_off];
+    return (double)hi * inv + (double)lo * (inv * 0x1p-50);
+}
+
+template <int MODE, bool NT, bool PK3 = false, int VT = 0, int P = BSLS_TILE_P,
+          int D = BSLS_TILE_D, bool FX = false>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
-                                                const double *rcol) {
+                                                const double *rcol, double fxs = 1.0) {
     static_assert(D >= 1 && D < P, "gathers run ahead of the entry loads");
     if (BSLS_TILE_KO == 3) return;
     typedef typename TileEnt<PK3>::type ent_t;
@@ -239,6 +267,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
     const int4 *Bq = reinterpret_cast<const int4 *>(T.base) + q0 * 16 + wv;
     const int64_t v0 = 4 * l0;   // first value of this lane (MODE 1)
     const double *xb = src + T.group_col[g];
+    const int lo_off = (int)(T.H + T.halo + 1);     // FX: the low words
     ent_t ring[P];
     int4 bring[P];
 #pragma unroll
@@ -281,7 +310,8 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
 #elif BSLS_TILE_KO == 2
                     ko += term;                       // (knock-out: no LDS)
 #else
-                    atomicAdd(&rows[lr], term);
+                    if constexpr (FX) fx_add(rows, lr, lo_off, term * fxs);
+                    else atomicAdd(&rows[lr], term);
 #endif
                 }
             }
@@ -298,32 +328,35 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
 }
 
 // the dealt walk with its value type (MODE 1 only: the other modes store none)
-template <int MODE, bool NT, bool PK3>
+template <int MODE, bool NT, bool PK3, bool FX = false>
 __device__ __forceinline__ void tile_walk_dealt_vt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                    const double *__restrict__ src, double *rows,
-                                                   const double *rcol) {
+                                                   const double *rcol, double fxs = 1.0) {
+    constexpr int P = BSLS_TILE_P, D = BSLS_TILE_D;
     if constexpr (MODE == 1) {
-        if (T.layout & BSLS_TILE_VAL16) tile_walk_dealt<MODE, NT, PK3, 2>(T, rb, g, src, rows, rcol);
+        if (T.layout & BSLS_TILE_VAL16)
+            tile_walk_dealt<MODE, NT, PK3, 2, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
         else if (T.layout & BSLS_TILE_VAL32)
-            tile_walk_dealt<MODE, NT, PK3, 1>(T, rb, g, src, rows, rcol);
-        else tile_walk_dealt<MODE, NT, PK3, 0>(T, rb, g, src, rows, rcol);
+            tile_walk_dealt<MODE, NT, PK3, 1, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
+        else tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
     } else {
-        tile_walk_dealt<MODE, NT, PK3, 0>(T, rb, g, src, rows, rcol);
+        tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
     }
 }
 
-// the walk of either layout
-template <int MODE>
+// the walk of either layout (FX: dealt layouts only)
+template <int MODE, bool FX = false>
 __device__ __forceinline__ void tile_walk_any(const bsls_tiles &T, int64_t rb, int64_t g,
                                               const double *__restrict__ src, double *rows,
-                                              const double *rcol) {
+                                              const double *rcol, double fxs = 1.0) {
     const int64_t lay = T.layout & ~(int64_t)(BSLS_TILE_VAL32 | BSLS_TILE_VAL16);
-    if (lay == 1) tile_walk_dealt_vt<MODE, false, false>(T, rb, g, src, rows, rcol);
-    else if (lay == (1 | BSLS_TILE_NT)) tile_walk_dealt_vt<MODE, true, false>(T, rb, g, src, rows, rcol);
-    else if (lay == 2) tile_walk_dealt_vt<MODE, false, true>(T, rb, g, src, rows, rcol);
+    if (lay == 1) tile_walk_dealt_vt<MODE, false, false, FX>(T, rb, g, src, rows, rcol, fxs);
+    else if (lay == (1 | BSLS_TILE_NT))
+        tile_walk_dealt_vt<MODE, true, false, FX>(T, rb, g, src, rows, rcol, fxs);
+    else if (lay == 2) tile_walk_dealt_vt<MODE, false, true, FX>(T, rb, g, src, rows, rcol, fxs);
     else if (lay == (2 | BSLS_TILE_NT))
-        tile_walk_dealt_vt<MODE, true, true>(T, rb, g, src, rows, rcol);
-    else tile_walk<MODE>(T, rb, g, src, rows, rcol);
+        tile_walk_dealt_vt<MODE, true, true, FX>(T, rb, g, src, rows, rcol, fxs);
+    else if constexpr (!FX) tile_walk<MODE>(T, rb, g, src, rows, rcol);
 }
 
 // Host-side validation of a tile image against the matrix it claims to hold

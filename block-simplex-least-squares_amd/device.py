@@ -579,7 +579,9 @@ class DeviceLSQ:
     the reference's exits rely on -- BATCH.solve_LBFGS's revert stops on
     |f_old - f| < prog_tol with delta_x = 0); k1='tiles' (or
     BSLS_LSQ_K1=tiles) walks a dealt tile image of A instead (the z-space
-    K1's walk: LDS atomic row sums, faster, the same sums to rounding only).
+    K1's walk: LDS atomic row sums, faster, the same sums to rounding only);
+    k1='tiles_fixed' walks it with 64-bit fixed-point row sums (order-free:
+    bit-repeatable like the panels, at the dealt walk's speed).
     A' is one group of panels (every row in CSR order: g bit-identical to
     SciPy's csr_matvec); k2='tiles' (or BSLS_LSQ_K2=tiles) walks a dealt tile
     image of A' instead (one group, LDS atomic row sums scaled by colv once per
@@ -596,8 +598,11 @@ class DeviceLSQ:
         self.scaled = colv is not None
         k1 = k1 or os.environ.get('BSLS_LSQ_K1', 'panels')
         self.A_pan = self.A_til = None
-        if k1 == 'tiles':
-            self.A_til = DeviceTiles(A, 0, values=not self.scaled, layout=2)
+        if k1 in ('tiles', 'tiles_fixed'):
+            # (the fixed-point walk keeps two words per row: plan for twice the LDS)
+            plan = (tile_plan(self.m, self.n, 0, colv_lds=True, layout=2, nnz=A.nnz)
+                    if k1 == 'tiles_fixed' else None)
+            self.A_til = DeviceTiles(A, 0, values=not self.scaled, layout=2, plan=plan)
             groups, npanels = self.A_til.img['ngroups'], 0
         else:
             prow, groups = k1_plan(self.m)
@@ -638,6 +643,17 @@ class DeviceLSQ:
         op.rpart = self.rpart.data_ptr()
         op.xs = ptr(self.xs)
         op.work, op.work_bytes = self.work.data_ptr(), self.work.numel()
+        if k1 == 'tiles_fixed':
+            # fixed-point row sums: the bound of a row's |terms| per unit of
+            # max|x| -- its entry count for a scaled incidence (the walk
+            # gathers colv * x), else sum_j |A_ij|
+            op.fixed = 1
+            if self.scaled:
+                op.fx_amax = float(max(1, int(np.max(np.diff(A.indptr))) if A.nnz else 1))
+            else:
+                rows = np.repeat(np.arange(self.m), np.diff(A.indptr))
+                ra = np.bincount(rows, weights=np.abs(A.data), minlength=self.m)
+                op.fx_amax = float(max(np.max(ra) if ra.size else 0.0, 1e-300))
         self.op = op
 
     def residual(self, x, out, add=None, sq=None):

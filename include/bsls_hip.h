@@ -529,6 +529,14 @@ typedef struct bsls_lsq_op {
      * atomic row sums scaled by colv once per row: g to rounding, not SciPy's
      * order; mirror descent) and op->AT is unused. */
     bsls_tiles ATt;
+    /* 1 (with At, dealt): the residual's row sums in 64-bit fixed point,
+     * order-free -- r and ||r||^2 repeat bit for bit at the same x, at the
+     * dealt walk's speed (the x-space solvers' exits compare f across rounds).
+     * fx_amax >= max_i sum_j |A_ij| (a scaled incidence: the most entries in a
+     * row); the scale is set per call from fx_amax * max|x|, each term rounds
+     * to 2^-50 of that bound. */
+    int64_t fixed;
+    double fx_amax;
 } bsls_lsq_op;
 
 size_t bsls_lsq_workspace_size(int64_t m, int64_t A_npanels);

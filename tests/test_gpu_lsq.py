@@ -7,7 +7,8 @@ order); r within 1e-12 relative of SciPy on both residual walks, and on the
 panels (the default) bit-identical to the host restatement of the panel walk
 (device.panels_matvec: 8 column-group partials summed in group order) and
 run-to-run; the dealt tile residual (k1='tiles', LDS atomic sums) within
-1e-12 run-to-run; ||r||^2 within 1e-12 relative.
+1e-12 run-to-run, and with fixed-point row sums (k1='tiles_fixed')
+bit-identical run-to-run; ||r||^2 within 1e-12 relative.
 """
 import numpy as np
 import pytest
@@ -34,7 +35,8 @@ def _scaled(m, n, per_col, rs):
 @pytest.mark.parametrize('m,n,per_col', [(1000, 9001, 5), (37, 300, 3), (20000, 150000, 12),
                                          (4096, 64, 40)])
 @pytest.mark.parametrize('scaled', [True, False])
-@pytest.mark.parametrize('k1,k2', [('tiles', 'panels'), ('panels', 'panels'), ('tiles', 'tiles')])
+@pytest.mark.parametrize('k1,k2', [('tiles', 'panels'), ('panels', 'panels'), ('tiles', 'tiles'),
+                                   ('tiles_fixed', 'panels')])
 def test_lsq_operator(cuda, m, n, per_col, scaled, k1, k2):
     import torch
     from device import DeviceLSQ, panels_matvec
@@ -86,7 +88,8 @@ def test_lsq_operator(cuda, m, n, per_col, scaled, k1, k2):
     sq3 = torch.zeros(1, dtype=torch.float64, device='cuda')
     for _ in range(3):
         op.residual(xd, r3, add=ad, sq=sq3)
-    if k1 == 'panels':
+    if k1 in ('panels', 'tiles_fixed'):
+        # (tiles_fixed: two-word fixed-point row sums, order-free)
         assert exact(r3.cpu().numpy(), rh) and float(sq3.item()) == float(sq.item())
     else:
         np.testing.assert_allclose(r3.cpu().numpy(), rh, rtol=1e-12,
@@ -162,3 +165,42 @@ def test_mirror_descent_ragged_blocks_vs_oracle(cuda, orc):
         x = mirror_descent.least_squares(A, b, list(sizes), iters=it, tolerance=0.0, poll=5)
         xr = orc.md_least_squares(A, b, list(sizes), iters=it, tolerance=0.0)
         np.testing.assert_allclose(x, xr, rtol=1e-10, atol=1e-14)
+
+
+def test_lsq_fixed_point_residual_edges(cuda):
+    """k1='tiles_fixed': x = 0 (scale from a zero bound), huge and tiny
+    magnitudes (1e150, 1e-150: the scale follows max|x|), a NaN in x (NaN
+    residual rows, not a finite garbage sum), heavy cancellation (r ~ 1e-9 of
+    the terms: the two-word sums keep it to 1e-12 of the terms), and the
+    order-free sums: the same r after the input entries' dealing changes
+    nothing but run order (three calls, bit-identical)."""
+    import torch
+    from device import DeviceLSQ
+    rs = np.random.RandomState(SEED + 9)
+    m, n = 3000, 40000
+    A = _scaled(m, n, 6, rs)
+    op = DeviceLSQ(A, A.T.tocsr(), k1='tiles_fixed', k2='panels')
+    r = torch.empty(m, dtype=torch.float64, device='cuda')
+    for scale in (0.0, 1e150, 1e-150, 1.0):
+        x = rs.rand(n) * scale
+        op.residual(torch.from_numpy(x).cuda(), r)
+        ref = A.dot(x)
+        np.testing.assert_allclose(r.cpu().numpy(), ref, rtol=1e-12,
+                                   atol=1e-12 * max(np.abs(ref).max(), 1e-300))
+    x = rs.rand(n)
+    x[123] = np.nan
+    op.residual(torch.from_numpy(x).cuda(), r)
+    assert np.isnan(r.cpu().numpy()).any()
+    # cancellation: add = -A x + tiny
+    x = rs.rand(n)
+    ax = A.dot(x)
+    tiny = 1e-9 * np.abs(ax).max() * rs.randn(m)
+    add = torch.from_numpy(tiny - ax).cuda()
+    op.residual(torch.from_numpy(x).cuda(), r, add=add)
+    got = r.cpu().numpy()
+    assert np.max(np.abs(got - tiny)) <= 1e-12 * np.abs(ax).max()
+    outs = []
+    for _ in range(3):
+        op.residual(torch.from_numpy(x).cuda(), r, add=add)
+        outs.append(r.cpu().numpy().copy())
+    assert all(exact(o, outs[0]) for o in outs)
