@@ -772,19 +772,24 @@ __device__ __forceinline__ double next_down(double x) {
     return __longlong_as_double(x > 0.0 ? b - 1 : b + 1);
 }
 
+__device__ __forceinline__ double buf_ld(const __amdgpu_buffer_rsrc_t &rs, int off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+}
+
 template <int LPB, int EB, bool BALL>
-__device__ __forceinline__ void thr_solve(double *__restrict__ y, int64_t s, int64_t s0, int k,
-                                          int j, const __amdgpu_buffer_rsrc_t &rs) {
+__device__ __forceinline__ void thr_solve(int64_t s, int64_t s0, int k, int j,
+                                          const __amdgpu_buffer_rsrc_t &rs) {
     constexpr double PAD = -1.7976931348623157e308;   // below every entry, finite
-    const double *blk = y + (k > 0 ? s : 0);
-    const int off0 = (int)(s - s0) * 8;                 // byte offset of the block in rs
+    // every access through the wave's buffer resource: one offset register
+    // (the block's start + j), slot e at + 8 LPB e (folded into the
+    // instruction); ne = this lane's live slots
+    const int base = (int)(s - s0 + j) * 8;
+    const int ne = (k > j) ? (k - j + LPB - 1) / LPB : 0;
     double v[EB];
-    // unconditional loads at clamped offsets: all EB in flight at once
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
-        const int i = j + LPB * e;
-        const double t = blk[i < k ? i : 0];
-        v[e] = (i < k) ? t : PAD;
+        const double t = buf_ld(rs, base + 8 * LPB * e);   // past the range: 0
+        v[e] = (e < ne) ? t : PAD;
     }
     bool need = true;
     if constexpr (BALL) {
@@ -792,7 +797,7 @@ __device__ __forceinline__ void thr_solve(double *__restrict__ y, int64_t s, int
         double acc = 0.0;
 #pragma unroll
         for (int e = 0; e < EB; ++e) {
-            const bool ok = j + LPB * e < k;
+            const bool ok = e < ne;
             v[e] = (ok & (v[e] < 0.0)) ? 0.0 : v[e];
             acc += ok ? v[e] : 0.0;
         }
@@ -808,21 +813,18 @@ __device__ __forceinline__ void thr_solve(double *__restrict__ y, int64_t s, int
         // |y| ~ 1e12+ rounding could reach it), so the max never leaves the set
         const double Mdn = next_down(M);
         double tau = fmin(M - 1.0, Mdn);
-        // active flags: padding never passes (PAD < tau of a live block)
-        bool a[EB];
-#pragma unroll
-        for (int e = 0; e < EB; ++e) a[e] = true;
         double cprev = 1.0;   // tau_0 is the tau of the set {max}
         double S = M, c = 1.0;
         for (int pass = 0; pass <= LPB * EB; ++pass) {
             double sl = 0.0, cl = 0.0;
 #pragma unroll
             for (int e = 0; e < EB; ++e) {
-                // branch-free: the set only shrinks (& with the old flag); sum
-                // and count by a 0 / 1 factor (fma: one rounding, = the add;
-                // the count is exact in a double)
-                a[e] = a[e] & (v[e] > tau);
-                const double f = a[e] ? 1.0 : 0.0;
+                // branch-free and mask-free: an entry leaving the set becomes
+                // PAD in v (the sets only shrink, and PAD never passes again);
+                // sum and count by a 0 / 1 factor (fma: one rounding, = the add)
+                const bool keep = v[e] > tau;
+                v[e] = keep ? v[e] : PAD;
+                const double f = keep ? 1.0 : 0.0;
                 sl = __builtin_fma(f, v[e], sl);
                 cl += f;
             }
@@ -835,22 +837,31 @@ __device__ __forceinline__ void thr_solve(double *__restrict__ y, int64_t s, int
         }
         lam = (1. - S) / c;
     }
-    // out through the wave's buffer resource: offsets of padding slots are
-    // past its end, so the hardware drops them (no per-slot branch)
+    // out: the entries read again (the passes overwrote the dropped ones; the
+    // lines are still in the caches), padding slots' offsets past the end so
+    // the hardware drops their stores (no per-slot branch)
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
-        const int i = j + LPB * e;
-        const double r = need ? relu_ref(lam + v[e]) : v[e];
+        double o = buf_ld(rs, base + 8 * LPB * e);
+        if (BALL) o = (o < 0.0) ? 0.0 : o;
+        const double r = need ? relu_ref(lam + o) : o;
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, r), rs,
-            (i < k) ? off0 + 8 * i : 0x7FFFFFF0, 0, 0);
+            (e < ne) ? base + 8 * LPB * e : 0x7FFFFFF0, 0, 0);
     }
 }
 
 // One wave: blocks b0 .. b0 + 64/LPB - 1 (block ends from the same coalesced
 // read of starts); blocks > SMALL_MAX go to the big list as in lds_group.
+// at least BSLS_PROJ_MINW waves per SIMD (<= 512 / MINW VGPRs): the C2 grid
+// (6250 waves at LPB 4) must be resident in one round -- at 73 VGPRs (six
+// waves per SIMD, 6144 slots) 106 waves ran as a second round
+#ifndef BSLS_PROJ_MINW
+#define BSLS_PROJ_MINW 8
+#endif
 template <bool BALL, int LPB>
-__global__ __launch_bounds__(256) void proj_thr_kernel(double *__restrict__ y,
+__global__ __launch_bounds__(256, BSLS_PROJ_MINW) void proj_thr_kernel(double *__restrict__ y,
                                                       const int64_t *__restrict__ starts,
                                                       int64_t nb, int64_t n,
                                                       int64_t *__restrict__ big_list,
@@ -893,14 +904,14 @@ __global__ __launch_bounds__(256) void proj_thr_kernel(double *__restrict__ y,
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(y + s0, 0, (int)((e1 - s0) * 8), 0x00020000);
     const int E = (kmax + LPB - 1) / LPB;
-    if (E <= 4) thr_solve<LPB, 4, BALL>(y, s, s0, k, j, rs);
-    else if (E <= 8) thr_solve<LPB, 8, BALL>(y, s, s0, k, j, rs);
+    if (E <= 4) thr_solve<LPB, 4, BALL>(s, s0, k, j, rs);
+    else if (E <= 8) thr_solve<LPB, 8, BALL>(s, s0, k, j, rs);
     else if constexpr (LPB <= 4) {
-        if (E <= 12) thr_solve<LPB, 12, BALL>(y, s, s0, k, j, rs);
-        else if (E <= 16) thr_solve<LPB, 16, BALL>(y, s, s0, k, j, rs);
+        if (E <= 12) thr_solve<LPB, 12, BALL>(s, s0, k, j, rs);
+        else if (E <= 16) thr_solve<LPB, 16, BALL>(s, s0, k, j, rs);
         else if constexpr (LPB == 2) {
-            if (E <= 24) thr_solve<LPB, 24, BALL>(y, s, s0, k, j, rs);
-            else thr_solve<LPB, 32, BALL>(y, s, s0, k, j, rs);
+            if (E <= 24) thr_solve<LPB, 24, BALL>(s, s0, k, j, rs);
+            else thr_solve<LPB, 32, BALL>(s, s0, k, j, rs);
         }
     }
 }
