@@ -22,9 +22,10 @@ BASELINE configs[0]) runs NumPy inputs only when selected explicitly
 (BSLS_DEVICE=cpu or _native.set_device('cpu')).
 
 Projections (proj_simplex_c, proj_multi_simplex_c, proj_multi_ball_c) take the
-sort-free kernels (bsls_proj_multi_*_fast: within 1e-12 * max(1, |ref|) of the
-reference, the north star's projection contract) unless BSLS_PROJ=exact
-selects the sorting kernels, which reproduce the reference bit for bit.
+sorting kernels, which reproduce the reference bit for bit; BSLS_PROJ=fast
+selects the sort-free ones (bsls_proj_multi_*_fast: within 1e-12 * max(1,
+|ref|), the north star's projection contract -- measured no faster on C2,
+DESIGN.md §4).
 """
 import os
 
@@ -146,9 +147,10 @@ def _work(nbytes):
 
 
 def _proj_entry(fn_name):
-    """The C entry for a projection: the sort-free _fast kernels unless
-    BSLS_PROJ=exact (read per call, so a test or caller can switch)."""
-    mode = os.environ.get('BSLS_PROJ', 'fast')
+    """The C entry for a projection: the bit-identical sorting kernels, or
+    the sort-free _fast ones with BSLS_PROJ=fast (read per call, so a test or
+    caller can switch)."""
+    mode = os.environ.get('BSLS_PROJ', 'exact')
     if mode not in ('fast', 'exact'):
         raise ValueError('BSLS_PROJ must be fast or exact, not %r' % mode)
     return fn_name + ('_fast' if mode == 'fast' else '')

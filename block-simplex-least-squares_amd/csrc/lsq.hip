@@ -69,6 +69,7 @@ __global__ __launch_bounds__(256) void lsq_xmax_kernel(double *__restrict__ xs,
         }
         mx[0] = nan_max(mx[0], fabs(v));
     }
+    block_reduce<1, 1u>(mx, red);
     double tot[1];
     if (last_block_reduce<1, 1u>(mx, mpart, ticket, tot, red) && threadIdx.x == 0) *xmax = tot[0];
 }

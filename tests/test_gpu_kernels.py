@@ -27,7 +27,8 @@ def cx(cuda):
 @pytest.fixture
 def exact_proj(monkeypatch):
     """c_extensions' projections on the bit-identical sorting kernels
-    (BSLS_PROJ=exact); the default is the sort-free _fast path."""
+    (BSLS_PROJ=exact, the default, set explicitly); fast_proj: the sort-free
+    _fast path."""
     monkeypatch.setenv('BSLS_PROJ', 'exact')
 
 
@@ -136,7 +137,7 @@ def test_proj_borderline_decisions(cx, orc, exact_proj):
 
 
 # ------------------------------------------------- sort-free projection (_fast)
-# bsls_proj_multi_*_fast (the c_extensions default): Newton on the threshold,
+# bsls_proj_multi_*_fast (c_extensions with BSLS_PROJ=fast): Newton on the threshold,
 # no sort -- held to the north star's contract |d| <= 1e-12 max(1, |ref|)
 # against the oracle (which is pinned to the reference), on the same inputs
 # the bit-exact tests above use.

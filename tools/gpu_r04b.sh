@@ -2,9 +2,8 @@
 # fast projection A/B (lanes per block x min waves), then the r04a remainder
 set -o pipefail
 mkdir -p gpurun_out
-for l in 4 8; do
+for l in 4; do
   echo "LPB=$l MINW=8"; BSLS_PROJ_LPB=$l timeout -k 10 120 python -u tools/proj_fast_time.py || exit 1
-  echo "LPB=$l MINW=6"; BSLS_LIB=$PWD/block-simplex-least-squares_amd/lib/libbsls_hip_pw6.so BSLS_PROJ_LPB=$l timeout -k 10 120 python -u tools/proj_fast_time.py || exit 1
 done
 timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_distributed.py tests/test_gpu_lsq.py -x -q \
   -k "proj or native or rccl or lsq" --timeout 300 --timeout-method thread > gpurun_out/t_b.log 2>&1
