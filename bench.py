@@ -776,6 +776,23 @@ def traffic_file():
     return fs[-1] if fs else None
 
 
+class _StdoutToStderr:
+    """fd 1 -> fd 2 for a block: RCCL prints its version banner on stdout
+    when it initialises, and bench.py's stdout must be the one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -823,10 +840,11 @@ def main():
                          ('WORLD_SIZE', '1')):
                 os.environ.setdefault(k, v)
         backend = os.environ.get('BSLS_DIST_BACKEND', 'nccl')
-        if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-        else:
-            dist.init_process_group(backend)
+        with _StdoutToStderr():
+            if backend == 'nccl':
+                dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+            else:
+                dist.init_process_group(backend)
 
     tfile = traffic_file()
     out = {} if rank == 0 else None
@@ -860,11 +878,14 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
     (whole-job rate in the workload's unit), kernels (HIP-event table of the
     rank-0 stages) and their roofline."""
     import torch
-    sh, b = build_problem(wl, world, rank, dist, shard_of=shard_of)
-    log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
-        % (wl, rank, world, sh['n'], sh['p'], sh['m'],
-           sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
-    eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(shard_of))
+    # (the first collectives and the driver's communicator initialise RCCL:
+    # its banner goes to stderr)
+    with _StdoutToStderr():
+        sh, b = build_problem(wl, world, rank, dist, shard_of=shard_of)
+        log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
+            % (wl, rank, world, sh['n'], sh['p'], sh['m'],
+               sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
+        eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(shard_of))
     log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
     el = time_run(run, steps, args.warmup, dist)
     it_s = steps / el

@@ -13,7 +13,8 @@ run() {   # label, then env assignments
       > gpurun_out/sweep_$label.json 2> gpurun_out/sweep_$label.err || { echo "$label FAILED"; return 1; }
   python - "$label" <<'PY'
 import json, sys
-d = json.load(open('gpurun_out/sweep_%s.json' % sys.argv[1]))
+t = open('gpurun_out/sweep_%s.json' % sys.argv[1]).read()
+d = json.loads(t[t.index('{'):])
 k = {n: round(v['avg_us'], 1) for n, v in d['kernels'].items() if n != 'formats'}
 print('%-14s %8.1f it/s  %6.1f us/it  %s' % (sys.argv[1], d['value'], d['ms_per_step'] * 1e3, k), flush=True)
 PY
