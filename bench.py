@@ -614,7 +614,7 @@ def build_problem(name, world, rank, dist, shard_of=None):
     return sh, b
 
 
-def build_engine(sh, b, world, dist, parts, sharded=False):
+def build_engine(sh, b, world, dist, parts, sharded=False, slices=None):
     """(engine, run(first, count)) for one rank: the fused single-GPU loop, or
     the column-sharded stages with the RCCL all-reduces (distributed.ShardedBB;
     `sharded` forces them at world 1 -- the per-rank host and launch path of
@@ -646,7 +646,7 @@ def build_engine(sh, b, world, dist, parts, sharded=False):
         comm = RcclComm()
     drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
                     all_reduce_async=torch_all_reduce_async(),
-                    rank=dist.get_rank(), native=comm)
+                    rank=dist.get_rank(), native=comm, slices=slices)
     drv.prologue()
     eng._comm = comm            # kept alive with the engine
     return eng, drv.iterate
@@ -885,7 +885,8 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
         log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
             % (wl, rank, world, sh['n'], sh['p'], sh['m'],
                sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
-        eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(shard_of))
+        eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(shard_of),
+                                slices=shard_of)
     log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
     el = time_run(run, steps, args.warmup, dist)
     it_s = steps / el
@@ -938,8 +939,10 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
         }
         if shard_of:
             res['config']['rehearsal'] = ('rank 0 of a %d-way C5 partition on one GPU through '
-                                          'the sharded driver (RCCL with one rank: no fabric)'
-                                          % shard_of)
+                                          'the sharded driver: every kernel of its iteration '
+                                          '(||r||^2 over its 1/%d slice), the collectives of a '
+                                          'one-rank communicator skipped -- per-rank compute, '
+                                          'no fabric' % (shard_of, shard_of))
     if getattr(eng, '_comm', None) is not None:
         torch.cuda.synchronize()
         eng._comm.close()

@@ -102,16 +102,21 @@ __device__ __forceinline__ double colv_t(const bsls_bb_problem &P, int64_t i) {
     else return P.colv[i];
 }
 
+// solvers.py:40-63 on iteration iter's g.g and dg.dg (the all-reduced sums)
+__device__ __forceinline__ int bb_stop_reason(const bsls_bb_problem &P, int64_t iter, double fx,
+                                              double gg, double dgdg) {
+    if (iter >= P.max_iter) return BSLS_STOP_MAXITER;
+    if (P.early_exit) {
+        const double gn = sqrt(gg);
+        if (gn * gn <= P.opt_tol * (1 + fabs(fx))) return BSLS_STOP_GRAD;
+        if (sqrt(dgdg) == 0) return BSLS_STOP_DG;
+    }
+    return 0;
+}
+
 __device__ __forceinline__ void bb_stop_check(const bsls_bb_problem &P, int64_t iter, double fx) {
     double *s = P.scal;
-    int reason = 0;
-    if (iter >= P.max_iter) {
-        reason = BSLS_STOP_MAXITER;
-    } else if (P.early_exit) {
-        const double gn = sqrt(s[BSLS_S_GG]);
-        if (gn * gn <= P.opt_tol * (1 + fabs(fx))) reason = BSLS_STOP_GRAD;
-        else if (sqrt(s[BSLS_S_DGDG]) == 0) reason = BSLS_STOP_DG;
-    }
+    const int reason = bb_stop_reason(P, iter, fx, s[BSLS_S_GG], s[BSLS_S_DGDG]);
     if (reason) s[BSLS_S_STOP] = (double)reason;
 }
 
@@ -369,7 +374,12 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
 // f and runs the stopping test of iteration iter - 1 before it stores this
 // iteration's sums.  (At the end of the finishing workgroups only, the slice
 // sums cost 13 us of tail in the 8-way rehearsal.)
-template <int MODE, bool ITER, bool FUSE = false, int CV = 0>
+// FUSE 2 (stage 10, the sliced schedule): the same r^2, but over this rank's
+// rows [P.rr_lo, P.rr_hi) of r only (1/world of m: the other ranks sum the
+// rest), stored with the sums as scal[RR] for the all-reduce; the last
+// workgroup keeps iteration iter - 1's sums in scal[PSUMDG..PGG] for the
+// stop test that follows the all-reduce (stage 12), instead of testing.
+template <int MODE, bool ITER, int FUSE = 0, int CV = 0>
 __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
                                                const double *__restrict__ gp,
                                                double *__restrict__ gout, double *part,
@@ -395,7 +405,9 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
             // every workgroup); same left-to-right order, padding adds +0
             constexpr int RR = 4;
             const int64_t ns = T.nrb * G, sl = rb * G + g;
-            const int64_t q0 = sl * P.m / ns, q1 = (sl + 1) * P.m / ns;
+            const bool cut = FUSE == 2 && P.rr_hi > P.rr_lo;
+            const int64_t lo = cut ? P.rr_lo : 0, span = (cut ? P.rr_hi : P.m) - lo;
+            const int64_t q0 = lo + sl * span / ns, q1 = lo + (sl + 1) * span / ns;
             for (int64_t i0 = q0 + threadIdx.x; i0 < q1; i0 += RR * (int64_t)blockDim.x) {
                 double v[RR];
 #pragma unroll
@@ -529,17 +541,45 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
                                : last_of_sum<NS>(sums, part, (unsigned)rb, (unsigned)T.nrb, ticket,
                                                  tot, red);
     if (last && threadIdx.x == 0) {
-        if constexpr (FUSE) {
+        if constexpr (FUSE == 1) {
             bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
             // stopped at iter - 1: keep that iteration's sums (what the
             // unfused schedule leaves in scal); g[iter & 1], written above,
             // is the other buffer -- the stopping iterate's g is untouched
             if (P.scal[BSLS_S_STOP] != 0.0) return;
         }
+        if constexpr (FUSE == 2) {
+            double *sc = P.scal;
+            for (int q = 0; q < 4; ++q) sc[BSLS_S_PSUMDG + q] = sc[BSLS_S_SUMDG + q];
+            sc[BSLS_S_RR] = tot[4];
+        }
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
         P.scal[BSLS_S_GG] = tot[3];
+    }
+}
+
+// Stage 12 (the sliced schedule, after the all-reduce of scal[SUMDG..RR]):
+// f(iter - 1) from the summed ||r||^2 and the stopping test of iter - 1 on
+// its own g.g and dg.dg (kept by stage 10 in scal[PSUMDG..PGG]); on a stop the
+// scal sums go back to that iteration's, as the unfused schedule leaves them.
+__global__ void bb_shard_record(bsls_bb_problem P, int64_t iter) {
+    if (threadIdx.x != 0) return;
+    double *s = P.scal;
+    const int64_t it = iter - 1;
+    if (it > 0 && s[BSLS_S_STOP] != 0.0) return;
+    const double rr = s[BSLS_S_RR];
+    const double nr = sqrt(rr);
+    const double fx = 0.5 * (nr * nr);      // 0.5 * la.norm(r)**2, main.py:53
+    s[BSLS_S_FX] = fx;
+    if (it <= 0) return;
+    s[BSLS_S_ITER] = (double)it;
+    s[BSLS_S_ZBUF] = (double)(it & 1);
+    const int reason = bb_stop_reason(P, it, fx, s[BSLS_S_PGG], s[BSLS_S_PDGDG]);
+    if (reason) {
+        s[BSLS_S_STOP] = (double)reason;
+        for (int q = 0; q < 4; ++q) s[BSLS_S_SUMDG + q] = s[BSLS_S_PSUMDG + q];
     }
 }
 
@@ -577,7 +617,7 @@ constexpr int R_FINISH_GRID = 512;
 // no faster).  The ITER epilogue reads g_prev and dz = z - z_prev (K3 wrote
 // dz from the z's it holds, bit-identical to the subtraction here): 15.2 MB
 // that no walk overlaps, where z and z_prev were 22.8 MB.
-template <int MODE, bool ITER, bool FUSE = false>
+template <int MODE, bool ITER, int FUSE = 0>
 __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *__restrict__ dzv,
                                               const double *__restrict__ gp,
                                               double *__restrict__ gout, double *part,
@@ -651,9 +691,11 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
         }
     }
     if (!ITER) return;
-    if constexpr (FUSE) {   // stage 8: this workgroup's slice of ||r||^2 (see bb_k2t)
-        const int64_t q0 = (int64_t)blockIdx.x * P.m / gridDim.x;
-        const int64_t q1 = ((int64_t)blockIdx.x + 1) * P.m / gridDim.x;
+    if constexpr (FUSE) {   // stage 8 / 10: this workgroup's slice of ||r||^2 (see bb_k2t)
+        const bool cut = FUSE == 2 && P.rr_hi > P.rr_lo;
+        const int64_t lo = cut ? P.rr_lo : 0, span = (cut ? P.rr_hi : P.m) - lo;
+        const int64_t q0 = lo + (int64_t)blockIdx.x * span / gridDim.x;
+        const int64_t q1 = lo + ((int64_t)blockIdx.x + 1) * span / gridDim.x;
         for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
             const double v = P.r[i];
             sums[4] += v * v;
@@ -662,9 +704,14 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
     block_sum<NS>(sums, lds);
     double tot[NS];
     if (last_block_sum<NS>(sums, part, ticket, tot, lds) && threadIdx.x == 0) {
-        if constexpr (FUSE) {
+        if constexpr (FUSE == 1) {
             bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
             if (P.scal[BSLS_S_STOP] != 0.0) return;   // as bb_k2t
+        }
+        if constexpr (FUSE == 2) {
+            double *sc = P.scal;
+            for (int q = 0; q < 4; ++q) sc[BSLS_S_PSUMDG + q] = sc[BSLS_S_SUMDG + q];
+            sc[BSLS_S_RR] = tot[4];
         }
         P.scal[BSLS_S_SUMDG] = tot[0];
         P.scal[BSLS_S_DZDG] = tot[1];
@@ -975,7 +1022,7 @@ static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, h
 
 // (dz: the vector the ITER sums dot with delta_g -- the workspace's z - z_prev
 // unless given: the line search passes its direction d, with g_prev = 0)
-template <int MODE, bool ITER, bool FUSE>
+template <int MODE, bool ITER, int FUSE>
 static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *gout,
                            const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
     allow_lds(bb_k2<MODE, ITER, FUSE>);
@@ -983,7 +1030,7 @@ static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *g
                               st>>>(P, dz, gp, gout, w.p2, w.tk2, iter);
 }
 
-template <int MODE, bool ITER, bool FUSE, int CV>
+template <int MODE, bool ITER, int FUSE, int CV>
 static void launch_k2t_cv(const bsls_bb_problem &P, const double *gp, double *gout,
                           const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
     allow_lds(bb_k2t<MODE, ITER, FUSE, CV>);
@@ -992,7 +1039,7 @@ static void launch_k2t_cv(const bsls_bb_problem &P, const double *gp, double *go
         P, dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter);
 }
 
-template <int MODE, bool ITER, bool FUSE>
+template <int MODE, bool ITER, int FUSE>
 static void launch_k2t_mode(const bsls_bb_problem &P, const double *gp, double *gout,
                             const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
     if (MODE != 1 && P.colv_codec == 2)
@@ -1002,7 +1049,7 @@ static void launch_k2t_mode(const bsls_bb_problem &P, const double *gp, double *
     else launch_k2t_cv<MODE, ITER, FUSE, 0>(P, gp, gout, w, st, iter, dz);
 }
 
-template <bool ITER, bool FUSE = false>
+template <bool ITER, int FUSE = 0>
 static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
                       const BBWork &w, hipStream_t st, int64_t iter = 0,
                       const double *dz = nullptr) {
@@ -1488,7 +1535,16 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
             break;
         case 8:  // stage 3 with stage 9 of iteration iter - 1 folded in
             if (iter <= 0) return BSLS_E_ARG;
-            launch_k2<true, true>(P, P.g[zc], P.g[zn], w, st, iter);
+            launch_k2<true, 1>(P, P.g[zc], P.g[zn], w, st, iter);
+            break;
+        case 10:  // stage 3 with this rank's slice of ||r||^2 (sliced schedule)
+            if (iter <= 0) return BSLS_E_ARG;
+            if (P.rr_lo < 0 || P.rr_hi > P.m || P.rr_lo > P.rr_hi) return BSLS_E_ARG;
+            launch_k2<true, 2>(P, P.g[zc], P.g[zn], w, st, iter);
+            break;
+        case 12:  // f / stopping test of iteration iter - 1 (after the sums' all-reduce)
+            if (iter <= 0) return BSLS_E_ARG;
+            bb_shard_record<<<1, 64, 0, st>>>(P, iter);
             break;
         case 3:  // g = N'A'r (+ sums)
             if (iter > 0) launch_k2<true>(P, P.g[zc], P.g[zn], w, st);

@@ -1,13 +1,18 @@
 // shard.hip -- the column-sharded BB iteration of one rank, enqueued from C++
 // with its RCCL collectives in the same loop (include/bsls_hip.h
 // bsls_bb_shard_iterate).  The schedule is distributed.ShardedBB's (python),
-// the orchestration the gloo tests pin against the oracle:
-//     stage 8   K2 (g_g, the four local BB sums) with f / stop test of i - 1
-//     RCCL      all-reduce(sum) of scal[SUMDG..GG]        32 B
+// the orchestration the gloo tests pin against the oracle (fuse 2, default):
+//     stage 10  K2 (g_g, the four local BB sums) + this rank's 1/world slice
+//               of ||r||^2 (r is the same all-reduced vector on every rank)
+//     RCCL      all-reduce(sum) of scal[SUMDG..RR]        40 B
+//     stage 12  f and the stopping test of i - 1 (one thread)
 //     stage 4   K3: t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = colv N_g z_g
 //     stage 1   K1: r_g = A_g x_g (+ target on the shard_role 1 rank)
 //     RCCL      all-reduce(sum) of r                      8 m B
-// and stage 9 (f / stop test) after the last iteration of a call.  A Python
+// and stage 9 (f / stop test) after the last iteration of a call; fuse 1
+// reads all of r for ||r||^2 in K2 (stage 8: the f of i - 1 in its last
+// workgroup, 14 us of an 8-way C5 rank's iteration for the 8 MB), fuse 0 runs
+// stage 3 and a stage 9 per iteration.  A Python
 // loop enqueued the same thing at ~4 ctypes calls + 2 torch.distributed calls
 // per iteration (tens of us of host time against a ~100-us device iteration
 // on 8 ranks); here an iteration costs 4 kernel launches + 2 RCCL calls of host
@@ -108,23 +113,35 @@ extern "C" int bsls_comm_all_reduce(bsls_comm *c, double *buf, int64_t count, vo
 
 extern "C" int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *c, int64_t first_iter,
                                      int64_t count, int fuse, void *stream) {
-    if (!p || !c || first_iter < 1 || count < 0) return BSLS_E_ARG;
+    if (!p || !c || first_iter < 1 || count < 0 || fuse < 0 || fuse > 2) return BSLS_E_ARG;
     if (p->shard_role != (c->rank == 0 ? 1 : 2)) return BSLS_E_ARG;   // target added once
     const RcclApi &R = rccl();
     hipStream_t st = (hipStream_t)stream;
+    // a sum over one rank is the identity: a one-rank communicator (the
+    // rehearsal of one rank's share on one GPU) skips the collectives, whose
+    // one-rank form is RCCL's own copies and flag fills (~17 us an iteration)
+    const bool comm = c->world > 1;
+    auto all_reduce = [&](double *buf, size_t cnt) -> int {
+        if (!comm) return BSLS_OK;
+        return comm_rc(R.all_reduce(buf, buf, cnt, ncclFloat64, ncclSum, c->comm, st));
+    };
     int rc;
     for (int64_t i = first_iter; i < first_iter + count; ++i) {
-        // K2 (+ the fused f / stop test of i - 1), then the BB sums summed over ranks
-        if ((rc = bsls_bb_stage(p, fuse ? 8 : 3, i, stream)) != BSLS_OK) return rc;
-        if ((rc = comm_rc(R.all_reduce(p->scal + BSLS_S_SUMDG, p->scal + BSLS_S_SUMDG, 4,
-                                       ncclFloat64, ncclSum, c->comm, st))) != BSLS_OK)
-            return rc;
+        if (fuse == 2) {
+            // K2 with this rank's slice of ||r||^2, the five sums over ranks,
+            // then f and the stop test of i - 1
+            if ((rc = bsls_bb_stage(p, 10, i, stream)) != BSLS_OK) return rc;
+            if ((rc = all_reduce(p->scal + BSLS_S_SUMDG, 5)) != BSLS_OK) return rc;
+            if ((rc = bsls_bb_stage(p, 12, i, stream)) != BSLS_OK) return rc;
+        } else {
+            // K2 (+ the fused f / stop test of i - 1), then the BB sums over ranks
+            if ((rc = bsls_bb_stage(p, fuse ? 8 : 3, i, stream)) != BSLS_OK) return rc;
+            if ((rc = all_reduce(p->scal + BSLS_S_SUMDG, 4)) != BSLS_OK) return rc;
+        }
         if ((rc = bsls_bb_stage(p, 4, i, stream)) != BSLS_OK) return rc;
         // the partial residual, then r = the sum over ranks (the one real exchange)
         if ((rc = bsls_bb_stage(p, 1, i, stream)) != BSLS_OK) return rc;
-        if ((rc = comm_rc(R.all_reduce(p->r, p->r, (size_t)p->m, ncclFloat64, ncclSum, c->comm,
-                                       st))) != BSLS_OK)
-            return rc;
+        if ((rc = all_reduce(p->r, (size_t)p->m)) != BSLS_OK) return rc;
         if (!fuse && (rc = bsls_bb_stage(p, 9, i, stream)) != BSLS_OK) return rc;
     }
     if (count > 0 && fuse) return bsls_bb_stage(p, 9, first_iter + count - 1, stream);

@@ -1047,6 +1047,13 @@ class BBEngine:
         check(_native.lib().bsls_bb_stage(self.P, int(k), int(it), stream_handle()),
               'bsls_bb_stage %d' % k)
 
+    def set_rr_slice(self, lo, hi):
+        """Rows [lo, hi) of r whose ||r||^2 stage 10 sums (the sliced sharded
+        schedule: each rank its 1/world share)."""
+        if not (0 <= lo <= hi <= self.m):
+            raise ValueError('slice out of range')
+        self.P.rr_lo, self.P.rr_hi = int(lo), int(hi)
+
     def set_shard_role(self, role):
         """bsls_bb_problem.shard_role: 0 the whole problem here, 1 a column
         shard that adds target to its partial residual, 2 another column shard

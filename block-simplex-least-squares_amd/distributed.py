@@ -7,10 +7,12 @@ blockify() already makes each block's columns contiguous
 blocks = a column slice A_g (m x n_g), its transpose, and its slices of
 z, g, x.  Per BB iteration:
 
-    stage 8   g_g = N_g' A_g' r  and the four local BB sums; folded into it, the
-              previous iteration's ||r||^2, f and stopping test (r is the same
-              all-reduced vector on every rank, so every rank decides alike)
-    all-reduce(sum) of the 4 BB sums  (32 bytes)
+    stage 10  g_g = N_g' A_g' r  and the four local BB sums, and this rank's
+              1/world slice of ||r||^2 (r is the same all-reduced vector on
+              every rank)
+    all-reduce(sum) of the 4 BB sums and ||r||^2  (40 bytes)
+    stage 12  f and the stopping test of the previous iteration (every rank
+              tests the same summed values, so every rank decides alike)
     stage 4   t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = x0_g + N_g z_g   (local)
     stage 1   r_g = A_g x_g, + target on rank 0 (partial residual, length m)
     all-reduce(sum) of r_g  (8 m bytes: the one real exchange of the algorithm)
@@ -57,6 +59,16 @@ def row_parts(nblocks, parts):
     return [int(v) for v in np.round(np.linspace(0, nblocks, parts + 1)).astype(np.int64)]
 
 
+def _world_size():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size()
+    except ImportError:
+        pass
+    return 1
+
+
 def _shard_rank(rank):
     """The rank that decides the shard role: the caller's, else the initialized
     default process group's.  Without either there is no safe default -- every
@@ -89,22 +101,36 @@ class ShardedBB:
     part p overlaps the computation of part p + 1; the compute stream waits
     for every part before stage 2."""
 
-    SUMS = slice(5, 9)   # scal[SUMDG..GG]
+    SUMS = slice(5, 9)      # scal[SUMDG..GG]
+    SUMS_RR = slice(5, 10)  # scal[SUMDG..RR]
 
     def __init__(self, engine, all_reduce, parts=1, all_reduce_async=None, rank=None,
-                 fuse=None, native=None):
+                 fuse=None, native=None, slices=None):
         self.e = engine
         rank = _shard_rank(rank)
         # native: an RcclComm -- iterate() then enqueues the whole schedule from
         # C++ (bsls_bb_shard_iterate: the stages and the two RCCL all-reduces of
         # an iteration, no Python per iteration); parts > 1 stays Python-driven
         self.native = native if (native is not None and int(parts) <= 1) else None
-        # fuse: K2 folds in the previous iteration's ||r||^2 / f / stopping test
-        # (stage 8, one stage-9 launch per call); else stage 3 and a stage-9
-        # launch after every residual exchange.  BSLS_SHARD_FUSE=0|1 (A/B).
+        # fuse 2 (default): K2 sums this rank's slice of ||r||^2 beside the BB
+        # sums (stage 10), all-reduced with them, then f / stopping test
+        # (stage 12); 1: K2 reads all of r for it and tests in its last
+        # workgroup (stage 8); 0: stage 3 and a stage-9 launch after every
+        # residual exchange.  BSLS_SHARD_FUSE=0|1|2 (A/B).
         if fuse is None:
-            fuse = os.environ.get('BSLS_SHARD_FUSE', '1') != '0'
-        self.fuse = bool(fuse)
+            fuse = int(os.environ.get('BSLS_SHARD_FUSE', '2'))
+        self.fuse = int(fuse)
+        if self.fuse not in (0, 1, 2):
+            raise ValueError('fuse must be 0, 1 or 2')
+        if self.fuse == 2:
+            # rows [lo, hi) of r: this rank's share of ||r||^2.  slices: the
+            # rank count (the process group's); a one-GPU rehearsal of rank 0
+            # of N passes N (its ||r||^2 is then 1/N of the true one: timing
+            # only)
+            if slices is None:
+                slices = _world_size()
+            m = engine.r.shape[0]
+            engine.set_rr_slice(rank * m // slices, (rank + 1) * m // slices)
         # rank 0 adds target to its partial residual; the others zero theirs
         # once the run has stopped (bsls_bb_problem.shard_role)
         engine.set_shard_role(1 if rank == 0 else 2)
@@ -155,11 +181,13 @@ class ShardedBB:
                       'bsls_bb_shard_iterate')
             return
         for i in range(first, first + count):
-            if self.fuse:
-                e.stage(8, i)    # K2 + f / stopping test of iteration i - 1
+            if self.fuse == 2:
+                e.stage(10, i)   # K2 + this rank's slice of ||r||^2
+                self.all_reduce(e.scal[self.SUMS_RR])
+                e.stage(12, i)   # f / stopping test of iteration i - 1
             else:
-                e.stage(3, i)
-            self.all_reduce(e.scal[self.SUMS])
+                e.stage(8 if self.fuse else 3, i)   # (8: + f / stop test of i - 1)
+                self.all_reduce(e.scal[self.SUMS])
             e.stage(4, i)
             self.residual(i)
             if not self.fuse:

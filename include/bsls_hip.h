@@ -161,6 +161,8 @@ enum {
     BSLS_S_GG = 8,         /* g . g */
     BSLS_S_RR = 9,         /* r . r */
     BSLS_S_WARN = 10,      /* count of |t| outside [1e-10, 1e10] (BB.py:27-28) */
+    BSLS_S_PSUMDG = 11,    /* stage 10: iteration i - 1's SUMDG, DZDG, DGDG, GG (11..14) */
+    BSLS_S_PDZDG = 12, BSLS_S_PDGDG = 13, BSLS_S_PGG = 14,
     BSLS_S_COUNT = 16
 };
 enum {
@@ -358,6 +360,9 @@ typedef struct bsls_bb_problem {
      * read the scales of every route per iteration (C5: 80 MB as doubles). */
     const void *colv_n;
     int64_t colv_codec;
+    /* Column-sharded sliced schedule (stage 10): the rows [rr_lo, rr_hi) of r
+     * whose ||r||^2 this rank sums (1/world of m each; 0, 0: all of them). */
+    int64_t rr_lo, rr_hi;
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
@@ -389,10 +394,16 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  *      and runs the stopping test of iter - 1 (with the all-reduced g.g of
  *      iter - 1) before it stores iteration iter's four sums
  *   9  ||r||^2, f, stopping test of iteration `iter` (r already the residual)
+ *  10  stage 3 (iter >= 1) with this rank's share of ||r||^2 (rows [rr_lo,
+ *      rr_hi)) into scal[RR] beside the four sums, iteration iter - 1's sums
+ *      kept in scal[PSUMDG..PGG]; all-reduce scal[SUMDG..RR] (5) afterwards
+ *  12  f and the stopping test of iteration iter - 1 from those (after the
+ *      all-reduce, before stage 4)
  * One iteration i >= 1 = 3, [allreduce sums], 4, 1, [allreduce r], 2; on one GCD
  * bsls_bb_iterate runs 3, 4, 7.  The column-sharded driver (distributed.py,
  * shard_role 1 / 2) runs 8, [allreduce sums], 4, 1, [allreduce r] per
- * iteration and 9 after the last one. */
+ * iteration and 9 after the last one (fuse 1), or the sliced form 10,
+ * [allreduce 5 sums], 12, 4, 1, [allreduce r] (fuse 2, the default). */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 /* Stage 1 restricted to K1's row blocks [rb0, rb1) (rows rb0 * R .. rb1 * R - 1,
  * R = *rows_per_block from bsls_bb_row_blocks, which returns the block count):
@@ -454,11 +465,14 @@ int bsls_comm_create(const void *id, int world, int rank, bsls_comm **out);
 int bsls_comm_destroy(bsls_comm *comm);
 /* in-place sum of `count` doubles over the ranks, on `stream` */
 int bsls_comm_all_reduce(bsls_comm *comm, double *d_buf, int64_t count, void *stream);
-/* Iterations first_iter .. first_iter+count-1 of the sharded schedule (fuse 1:
- * per iteration stage 8, all-reduce scal[SUMDG..GG], stage 4, stage 1,
- * all-reduce r; stage 9 after the last.  fuse 0: stage 3 instead of 8 and a
- * stage 9 after every r exchange).  p->shard_role must be 1 on rank 0 and 2
- * elsewhere (target added once).  All on `stream`; nothing waits on the host. */
+/* Iterations first_iter .. first_iter+count-1 of the sharded schedule (fuse 2:
+ * per iteration stage 10, all-reduce scal[SUMDG..RR], stage 12, stage 4,
+ * stage 1, all-reduce r; fuse 1: stage 8, all-reduce scal[SUMDG..GG], 4, 1,
+ * all-reduce r; fuse 0: stage 3 instead of 8 and a stage 9 after every r
+ * exchange; stage 9 after the last iteration in all three).  p->shard_role
+ * must be 1 on rank 0 and 2 elsewhere (target added once).  A one-rank
+ * communicator skips the collectives (a sum over one rank).  All on
+ * `stream`; nothing waits on the host. */
 int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *comm, int64_t first_iter,
                           int64_t count, int fuse, void *stream);
 

@@ -40,6 +40,11 @@ class FakeStages:
     def set_shard_role(self, role):
         self.role = role
 
+    rr_lo = rr_hi = 0
+
+    def set_rr_slice(self, lo, hi):
+        self.rr_lo, self.rr_hi = lo, hi
+
     def Nz(self, z):
         out = np.empty(self.n)
         for b, (xs, k) in enumerate(zip(self.xst, self.sizes)):
@@ -95,7 +100,7 @@ class FakeStages:
             self._partial(it, 0, self.A.shape[0])
         elif k == 9:
             self._record(it)
-        elif k in (3, 8):
+        elif k in (3, 8, 10):
             if it > 0 and float(s[0]) != 0:
                 return
             g = self.Ntw(self.AT.dot(self.r.numpy()))
@@ -107,7 +112,23 @@ class FakeStages:
             dz = self.z[zc] - self.z[zn]
             if k == 8:
                 self._record(it - 1)     # before this iteration's sums land
+            if k == 10:
+                s[11:15] = s[5:9].clone()            # iteration it - 1's sums, for stage 12
+                rs = self.r[self.rr_lo:self.rr_hi] if self.rr_hi > self.rr_lo else self.r
+                s[9] = float(rs.dot(rs))             # this rank's slice of ||r||^2
             s[5], s[6], s[7], s[8] = dg.sum(), dz.dot(dg), dg.dot(dg), g.dot(g)
+        elif k == 12:
+            # f / stopping test of it - 1 from the all-reduced ||r||^2 (s[9])
+            p = it - 1
+            if p > 0 and float(s[0]) != 0:
+                return
+            rr = float(s[9])
+            s[4] = 0.5 * np.sqrt(rr) ** 2
+            if p > 0:
+                s[1], s[2] = p, p & 1
+                if p >= self.max_iter:
+                    s[0] = 2
+                    s[5:9] = s[11:15].clone()
         elif k == 4:
             if float(s[0]) != 0:
                 return
@@ -237,19 +258,26 @@ def test_two_rank_stop_keeps_final_residual(orc):
 
 @pytest.mark.timeout(600)
 def test_two_rank_unfused_schedule(orc, monkeypatch):
-    """ShardedBB(fuse=False) (BSLS_SHARD_FUSE=0: stage 3, then a stage-9 stop
-    test after every residual exchange, instead of stage 8's one-iteration
-    delay): the same trajectory as the fused schedule, and the same stop."""
+    """The three schedules (BSLS_SHARD_FUSE=2, the default: stage 10's sliced
+    ||r||^2 all-reduced with the sums and stage 12's stop test; 1: stage 8's
+    fused test; 0: stage 3 and a stage-9 test after every exchange): the same
+    trajectory, and the same stop."""
     iters = 10
-    fused = _spawn(2, iters)
-    monkeypatch.setenv('BSLS_SHARD_FUSE', '0')
-    plain = _spawn(2, iters)
-    for i in fused:
-        d = np.max(np.abs(fused[i] - plain[i])) / max(1.0, np.max(np.abs(fused[i])))
-        assert d < 1e-12, (i, d)
-    two = _spawn(2, 9, stop_at=5)
+    fused = _spawn(2, iters)                    # the sliced schedule (fuse 2, default)
+    for mode in ('0', '1'):
+        monkeypatch.setenv('BSLS_SHARD_FUSE', mode)
+        plain = _spawn(2, iters)
+        for i in fused:
+            d = np.max(np.abs(fused[i] - plain[i])) / max(1.0, np.max(np.abs(fused[i])))
+            assert d < 1e-12, (mode, i, d)
+        two = _spawn(2, 9, stop_at=5)
+        for rank in (0, 1):
+            assert two[rank]['scal'][0] == 2 and two[rank]['scal'][1] == 5, mode
+            # the stopping iteration's sums stay in scal whatever the schedule
+        monkeypatch.delenv('BSLS_SHARD_FUSE')
+    base = _spawn(2, 9, stop_at=5)
     for rank in (0, 1):
-        assert two[rank]['scal'][0] == 2 and two[rank]['scal'][1] == 5
+        assert base[rank]['scal'][0] == 2 and base[rank]['scal'][1] == 5
 
 
 def test_row_parts():
