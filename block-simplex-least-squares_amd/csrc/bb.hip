@@ -788,9 +788,32 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
                                              const double *__restrict__ g,
                                              double *__restrict__ zn,
                                              double *__restrict__ dzo,
-                                             int32_t *__restrict__ wsc) {
+                                             int32_t *__restrict__ wsc, int rec) {
     const double sc[4] = {P.scal[BSLS_S_STOP], P.scal[BSLS_S_SUMDG], P.scal[BSLS_S_DZDG],
                           P.scal[BSLS_S_DGDG]};
+    // rec (stage 13, the sliced sharded schedule): stage 12 folded in -- f and
+    // the stopping test of iter - 1 from the all-reduced scal[RR] and the kept
+    // scal[PGG] / scal[PDGDG], decided alike by every workgroup (the same
+    // inputs), recorded by workgroup 0; on a stop every workgroup returns
+    if (rec && !(iter - 1 > 0 && sc[0] != 0.0)) {
+        double *s = P.scal;
+        const int64_t it = iter - 1;
+        const double nr = sqrt(s[BSLS_S_RR]);
+        const double fx = 0.5 * (nr * nr);
+        const int reason = it > 0 ? bb_stop_reason(P, it, fx, s[BSLS_S_PGG], s[BSLS_S_PDGDG]) : 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            s[BSLS_S_FX] = fx;
+            if (it > 0) {
+                s[BSLS_S_ITER] = (double)it;
+                s[BSLS_S_ZBUF] = (double)(it & 1);
+            }
+            if (reason) {
+                s[BSLS_S_STOP] = (double)reason;
+                for (int q = 0; q < 4; ++q) s[BSLS_S_SUMDG + q] = s[BSLS_S_PSUMDG + q];
+            }
+        }
+        if (reason) return;
+    }
     const int l = lane_id();
     const int wv = threadIdx.x / WAVE;
     const int64_t nw = (int64_t)gridDim.x * 4;
@@ -1079,18 +1102,20 @@ static bool k3_merge(const bsls_bb_problem &P) {
 
 template <int CV>
 static void launch_k3_cv(const bsls_bb_problem &P, int64_t iter, const double *zc,
-                         const double *g, double *zn, const BBWork &w, hipStream_t st) {
+                         const double *g, double *zn, const BBWork &w, hipStream_t st, int rec) {
     if (k3_merge(P))
-        bb_k3<2, true, CV><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+        bb_k3<2, true, CV><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc,
+                                                                   rec);
     else
-        bb_k3<1, false, CV><<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc);
+        bb_k3<1, false, CV><<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.dz,
+                                                                    w.wsc, rec);
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
-                      double *zn, const BBWork &w, hipStream_t st) {
-    if (P.colv && P.colv_codec == 2) launch_k3_cv<2>(P, iter, zc, g, zn, w, st);
-    else if (P.colv && P.colv_codec == 1) launch_k3_cv<1>(P, iter, zc, g, zn, w, st);
-    else launch_k3_cv<0>(P, iter, zc, g, zn, w, st);
+                      double *zn, const BBWork &w, hipStream_t st, int rec = 0) {
+    if (P.colv && P.colv_codec == 2) launch_k3_cv<2>(P, iter, zc, g, zn, w, st, rec);
+    else if (P.colv && P.colv_codec == 1) launch_k3_cv<1>(P, iter, zc, g, zn, w, st, rec);
+    else launch_k3_cv<0>(P, iter, zc, g, zn, w, st, rec);
     if (P.long_packs && P.nlong > 0)
         bb_k3_long<<<(int)P.nlong, LONG_T, 0, st>>>(P, iter, zc, g, zn, w.dz);
 }
@@ -1541,6 +1566,10 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
             if (iter <= 0) return BSLS_E_ARG;
             if (P.rr_lo < 0 || P.rr_hi > P.m || P.rr_lo > P.rr_hi) return BSLS_E_ARG;
             launch_k2<true, 2>(P, P.g[zc], P.g[zn], w, st, iter);
+            break;
+        case 13:  // stage 12 folded into stage 4's K3 (one launch fewer)
+            if (iter <= 0) return BSLS_E_ARG;
+            launch_k3(P, iter, P.z[zc], P.g[zn], P.z[zn], w, st, 1);
             break;
         case 12:  // f / stopping test of iteration iter - 1 (after the sums' all-reduce)
             if (iter <= 0) return BSLS_E_ARG;

@@ -11,9 +11,9 @@ z, g, x.  Per BB iteration:
               1/world slice of ||r||^2 (r is the same all-reduced vector on
               every rank)
     all-reduce(sum) of the 4 BB sums and ||r||^2  (40 bytes)
-    stage 12  f and the stopping test of the previous iteration (every rank
-              tests the same summed values, so every rank decides alike)
-    stage 4   t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = x0_g + N_g z_g   (local)
+    stage 13  f and the stopping test of the previous iteration (every rank
+              tests the same summed values, so every rank decides alike), then
+              t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = x0_g + N_g z_g  (K3)
     stage 1   r_g = A_g x_g, + target on rank 0 (partial residual, length m)
     all-reduce(sum) of r_g  (8 m bytes: the one real exchange of the algorithm)
 and after the last iteration of a call stage 9 (||r||^2, f, stopping test of
@@ -184,11 +184,11 @@ class ShardedBB:
             if self.fuse == 2:
                 e.stage(10, i)   # K2 + this rank's slice of ||r||^2
                 self.all_reduce(e.scal[self.SUMS_RR])
-                e.stage(12, i)   # f / stopping test of iteration i - 1
+                e.stage(13, i)   # K3 after f / the stopping test of iteration i - 1
             else:
                 e.stage(8 if self.fuse else 3, i)   # (8: + f / stop test of i - 1)
                 self.all_reduce(e.scal[self.SUMS])
-            e.stage(4, i)
+                e.stage(4, i)
             self.residual(i)
             if not self.fuse:
                 e.stage(9, i)    # f / stopping test of iteration i

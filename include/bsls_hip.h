@@ -399,11 +399,13 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  *      kept in scal[PSUMDG..PGG]; all-reduce scal[SUMDG..RR] (5) afterwards
  *  12  f and the stopping test of iteration iter - 1 from those (after the
  *      all-reduce, before stage 4)
+ *  13  stage 12 folded into stage 4 (K3's workgroups all decide the stop of
+ *      iter - 1 from the same scal values, workgroup 0 records it)
  * One iteration i >= 1 = 3, [allreduce sums], 4, 1, [allreduce r], 2; on one GCD
  * bsls_bb_iterate runs 3, 4, 7.  The column-sharded driver (distributed.py,
  * shard_role 1 / 2) runs 8, [allreduce sums], 4, 1, [allreduce r] per
  * iteration and 9 after the last one (fuse 1), or the sliced form 10,
- * [allreduce 5 sums], 12, 4, 1, [allreduce r] (fuse 2, the default). */
+ * [allreduce 5 sums], 13, 1, [allreduce r] (fuse 2, the default). */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 /* Stage 1 restricted to K1's row blocks [rb0, rb1) (rows rb0 * R .. rb1 * R - 1,
  * R = *rows_per_block from bsls_bb_row_blocks, which returns the block count):
@@ -466,8 +468,8 @@ int bsls_comm_destroy(bsls_comm *comm);
 /* in-place sum of `count` doubles over the ranks, on `stream` */
 int bsls_comm_all_reduce(bsls_comm *comm, double *d_buf, int64_t count, void *stream);
 /* Iterations first_iter .. first_iter+count-1 of the sharded schedule (fuse 2:
- * per iteration stage 10, all-reduce scal[SUMDG..RR], stage 12, stage 4,
- * stage 1, all-reduce r; fuse 1: stage 8, all-reduce scal[SUMDG..GG], 4, 1,
+ * per iteration stage 10, all-reduce scal[SUMDG..RR], stage 13, stage 1,
+ * all-reduce r; fuse 1: stage 8, all-reduce scal[SUMDG..GG], 4, 1,
  * all-reduce r; fuse 0: stage 3 instead of 8 and a stage 9 after every r
  * exchange; stage 9 after the last iteration in all three).  p->shard_role
  * must be 1 on rank 0 and 2 elsewhere (target added once).  A one-rank

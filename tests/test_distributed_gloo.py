@@ -117,6 +117,9 @@ class FakeStages:
                 rs = self.r[self.rr_lo:self.rr_hi] if self.rr_hi > self.rr_lo else self.r
                 s[9] = float(rs.dot(rs))             # this rank's slice of ||r||^2
             s[5], s[6], s[7], s[8] = dg.sum(), dz.dot(dg), dg.dot(dg), g.dot(g)
+        elif k == 13:             # stage 12 then stage 4 (K3 with the record folded in)
+            self.stage(12, it)
+            self.stage(4, it)
         elif k == 12:
             # f / stopping test of it - 1 from the all-reduced ||r||^2 (s[9])
             p = it - 1
