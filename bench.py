@@ -291,8 +291,9 @@ def bench_xspace(sh, b, rounds=40, reps=5, k1=None):
     nr = rounds * reps
     common = 24 * nnz + 4 * (m + n + 2) + 24 * m + 16 * n + 32 * n
     byt = nr * common + (nr - bts) * (40 * n + 16 * n + 4 * (p + 1)) + bts * 24 * n
-    opname = 'csr' if obj.lsq is None else ('tiles residual + panels gradient'
-                                           if obj.lsq.k1 == 'tiles' else 'panels')
+    opname = 'csr' if obj.lsq is None else {
+        'tiles': 'tiles residual + panels gradient',
+        'tiles_fixed': 'fixed-point tiles residual + panels gradient'}.get(obj.lsq.k1, 'panels')
     return {'operator': opname,
             'rounds': nr, 'us_per_round': ms * 1e3 / nr,
             'rounds_per_s': nr / (ms * 1e-3), 'iterations_per_s': its / (ms * 1e-3),
@@ -975,6 +976,9 @@ def extras(args, legs, out, tfile):
         # the opt-in dealt-tile residual (not bit-reproducible: the
         # reference's exact-revert exit needs the panels)
         out['xspace_bb_tiles'] = bench_xspace(sh3, b3, k1='tiles')
+        # the dealt walk with two-word fixed-point row sums: bit-repeatable
+        # like the panels (the revert exit), at the tiles' speed
+        out['xspace_bb_fixed'] = bench_xspace(sh3, b3, k1='tiles_fixed')
         torch.cuda.empty_cache()
     if 'md' in legs:
         out['mirror_descent'] = bench_md(sh3, b3)
