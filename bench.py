@@ -972,13 +972,13 @@ def extras(args, legs, out, tfile):
     if 'iso' in legs:
         out['isotonic'] = bench_iso()
     if 'xspace' in legs:
+        # the default operator: the dealt tile residual with two-word
+        # fixed-point row sums (bit-repeatable, as the reference's revert exit
+        # needs); beside it the fixed-order panels (the round-3 default) and
+        # the float-atomic tiles (opt-in, not bit-repeatable)
         out['xspace_bb'] = bench_xspace(sh3, b3)
-        # the opt-in dealt-tile residual (not bit-reproducible: the
-        # reference's exact-revert exit needs the panels)
+        out['xspace_bb_panels'] = bench_xspace(sh3, b3, k1='panels')
         out['xspace_bb_tiles'] = bench_xspace(sh3, b3, k1='tiles')
-        # the dealt walk with two-word fixed-point row sums: bit-repeatable
-        # like the panels (the revert exit), at the tiles' speed
-        out['xspace_bb_fixed'] = bench_xspace(sh3, b3, k1='tiles_fixed')
         torch.cuda.empty_cache()
     if 'md' in legs:
         out['mirror_descent'] = bench_md(sh3, b3)

@@ -20,6 +20,8 @@ obj is a SparseLSQ / DenseQP object, proj a BlockProj and line_search carries
 `.obj`, so BATCH.solve_BB can recognise the sparse x-space case and hand the
 whole loop to the fused device engine (device.XBBEngine, csrc/xbb.hip).
 """
+import os
+
 import numpy as np
 import scipy.sparse as sps
 
@@ -128,10 +130,13 @@ class SparseLSQ:
     """sparse_least_squares_obj (algorithm_utils.py:88-94) over device CSR:
     tmp = A x - b; g = A' tmp; f = .5 tmp.tmp.
 
-    `panels`: also build the panel images (device.DeviceLSQ, csrc/lsq.hip) and
-    run both products on them -- the default from PANEL_MIN_NNZ nonzeros up.
-    g is bit-identical either way; tmp differs from SciPy's row order by
-    <= 1e-12 relative on the panel path (8 column-group partials)."""
+    `panels`: also build the images of device.DeviceLSQ (csrc/lsq.hip) and run
+    both products on them -- the default from PANEL_MIN_NNZ nonzeros up: the
+    residual on a dealt tile image of A with two-word fixed-point row sums
+    (k1='tiles_fixed': order-free, so f repeats bit for bit at the same x, as
+    the solvers' revert exit needs; BSLS_LSQ_K1=panels keeps the fixed-order
+    panel walk), the gradient on the A' panels (bit-identical to SciPy).
+    tmp differs from SciPy's row order by <= 1e-12 relative."""
 
     PANEL_MIN_NNZ = 1 << 20
 
@@ -146,7 +151,8 @@ class SparseLSQ:
         self.AT = DeviceCSR(AT)
         if panels is None:
             panels = A.nnz >= self.PANEL_MIN_NNZ
-        self.lsq = lsq_operator(A, AT) if panels else None
+        self.lsq = (lsq_operator(A, AT, k1=os.environ.get('BSLS_LSQ_K1', 'tiles_fixed'))
+                    if panels else None)
         self.b = _dev(np.asarray(b, dtype=np.float64).ravel())
         self.neg_b = -self.b
         self.tmp = torch.empty(self.m, dtype=torch.float64, device='cuda')
