@@ -221,10 +221,12 @@ def test_k3_wave_pava_bit_exact(cuda, orc, monkeypatch, merge):
         assert np.array_equal(dz.view(np.int64), (got - zc).view(np.int64)), trial
 
 
-def test_dense_row_network_falls_back_to_tiles(cuda, orc):
+def test_dense_row_network_falls_back_to_tiles(cuda, orc, monkeypatch):
     """A 100k-route network with 8 links every route crosses: the panel image
     overflows, the engine takes the streamed tiles for A, and the iterates
-    still follow the oracle; the x-space operator falls back to the CSR kernels."""
+    still follow the oracle; the x-space operator's residual walks its
+    fixed-point tile image (f, g as SciPy's to 1e-12), and on the panels
+    (BSLS_LSQ_K1=panels) it falls back to the CSR kernels."""
     from device import BBEngine
     from algorithm_utils import SparseLSQ
     from test_host import _dense_row_matrix
@@ -245,7 +247,16 @@ def test_dense_row_network_falls_back_to_tiles(cuda, orc):
     for i in (1, 5, 10):
         assert rel_err(rec[i], ref[i]) < 1e-6, i
     op = SparseLSQ(A, b, panels=True)
-    assert op.lsq is None
+    assert op.lsq is not None and op.lsq.k1 == 'tiles_fixed'
+    xt = rs.rand(A.shape[1])
+    gh = np.zeros(A.shape[1])
+    f = op(xt, gh)                           # g written in place, as np.copyto
+    tmp = A.dot(xt) - b
+    assert abs(float(f) - 0.5 * tmp.dot(tmp)) <= 1e-12 * 0.5 * tmp.dot(tmp)
+    gref = A.T.dot(tmp)
+    assert np.max(np.abs(gh - gref)) <= 1e-10 * np.max(np.abs(gref))
+    monkeypatch.setenv('BSLS_LSQ_K1', 'panels')
+    assert SparseLSQ(A, b, panels=True).lsq is None
 
 
 def test_bb_iterates_with_long_blocks_vs_oracle(cuda, orc):
