@@ -891,8 +891,10 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
     log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
     el = time_run(run, steps, args.warmup, dist)
     it_s = steps / el
-    finite = bool(np.isfinite(eng.scalars()[4]))
-    log('%s: %d iterations in %.3f s: %.1f it/s' % (wl, steps, el, it_s))
+    sc = eng.scalars()
+    finite = bool(np.isfinite(sc[4]))
+    log('%s: %d iterations in %.3f s: %.1f it/s (f %.6e, stop flag %g, iteration %g)'
+        % (wl, steps, el, it_s, sc[4], sc[0], sc[1]))
     m, n_g, nz_g, p_g, nnz_g = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
     kern = {}
     if args.profile_iters > 0 and rank == 0:

@@ -58,9 +58,9 @@ class _DeviceHistory:
         """-r of LBFGS.py:59-71 (no host read)."""
         P, ck, L = self.native.ptr, self.native.check, self.L
         st = self.native.stream_handle()
-        self.g.copy_(g_new.reshape(-1))
-        self.yn.copy_(y_new.reshape(-1))
-        self.sn.copy_(s_new.reshape(-1))
+        for buf, v in ((self.g, g_new), (self.yn, y_new), (self.sn, s_new)):
+            if v is not buf:       # (the device line search writes y, s in place)
+                buf.copy_(v.reshape(-1))
         ck(L.bsls_multi_dot(P(self.rows), 3, P(self.cols), self.K, self.n, P(self.dots),
                             P(self.work), self.wbytes, st), 'bsls_multi_dot')
         ck(L.bsls_lbfgs_coef(self.m, self.head, P(self.state), P(self.dots), st), 'bsls_lbfgs_coef')
@@ -102,6 +102,12 @@ def weak_wolfe_ls(x, d, f, nabla_f, proj=lambda v: v, c1=1e-3, c2=0.9):
             return t
         if abs(lo - hi) <= 1e-14 or norm(t * d) <= 1e-8:
             return t
+
+
+def _host_floats(*vals):
+    """Device scalars to host floats in one read."""
+    import torch
+    return [float(v) for v in torch.stack(list(vals)).cpu()]
 
 
 def _device_engine(f, nabla_f, proj, x):
@@ -159,29 +165,36 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
             rho = rho[1:] + [rho_new]
         if ls is not None and fx_dev is not None:
             # x = proj(x) (the last x_next) and g_new = nabla_f(x): the line
-            # search's proj(x) / nabla_f(proj(x)) (LBFGS.py:18-19) are these
-            t, why, _, dnorm = ls.search(x, d, g_new, fx_dev)
-            s_new = t * d
+            # search's proj(x) / nabla_f(proj(x)) (LBFGS.py:18-19) are these.
+            # On the accepted exit the search's one read per chunk also brings
+            # f(x_next), y.s and g.g, and y / s land in the history's buffers.
+            yb = hist.yn if hist is not None else None
+            sb = hist.sn if hist is not None else None
+            t, why, _, dnorm = ls.search(x, d, g_new, fx_dev, y_out=yb, s_out=sb)
             g = g_new
-            if why == 1:       # accepted: the last trial is x_next
+            if why == 1 and ls.last is not None:     # accepted: the last trial is x_next
                 x_next, g_new, fx_dev = ls.take()
+                fx, ys, gg = ls.last
+                if hist is not None:
+                    y_new, s_new = hist.yn, hist.sn
+                else:
+                    s_new = t * d
+                    y_new = g_new - g
             else:              # t was never evaluated (the two other exits)
+                s_new = t * d
                 x_next = proj(x + s_new)
                 g_new = nabla_f(x_next)
-                fx_dev = None
-            y_new = g_new - g
-            import torch
-            vals = torch.stack([y_new.dot(s_new), g_new.dot(g_new),
-                                fx_dev[0] if fx_dev is not None else g_new.new_zeros(())]).cpu()
-            ys, gg = float(vals[0]), float(vals[1])
-            fx = float(vals[2]) if fx_dev is not None else f(x_next)
+                y_new = g_new - g
+                vals = _host_floats(y_new.dot(s_new), g_new.dot(g_new))
+                ys, gg = vals[0], vals[1]
+                fx = f(x_next)
+                fx_dev = g_new.new_tensor([fx])
             if ys == 0:
                 print('iter=%d, f=%8.5e' % (i, fx))
                 print('Exiting... no change in gradient')
                 break
             rho_new = 1 / ys
             x = x_next
-            fx_dev = g_new.new_tensor([fx]) if fx_dev is None else fx_dev
             if math.isnan(fx):
                 raise ArithmeticError('objective function evaluates to NaN')
             stop = stopping(Normed(g_new, math.sqrt(gg)), fx, i, t, d=Normed(d, dnorm),

@@ -79,7 +79,8 @@ class BBProblem(ctypes.Structure):
                 ('early_exit', _i32), ('shard_role', _i32),
                 ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz),
                 ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp),
-                ('colv_n', _vp), ('colv_codec', _i64), ('rr_lo', _i64), ('rr_hi', _i64)]
+                ('colv_n', _vp), ('colv_codec', _i64), ('rr_lo', _i64), ('rr_hi', _i64),
+                ('pava_warm', _i64)]
 
 
 class DoreState(ctypes.Structure):
@@ -100,8 +101,8 @@ class LsState(ctypes.Structure):
                 ('tickets', _vp), ('c1', _dbl), ('c2', _dbl)]
 
 
-LS_T, LS_LO, LS_HI, LS_STOP, LS_SLOPE, LS_FX, LS_DNORM, LS_NTRIAL, LS_TLAST, LS_FT, LS_DGT = \
-    range(11)
+(LS_T, LS_LO, LS_HI, LS_STOP, LS_SLOPE, LS_FX, LS_DNORM, LS_NTRIAL, LS_TLAST, LS_FT, LS_DGT,
+ LS_YS, LS_GG, LS_DONE) = range(14)
 LS_COUNT = 16
 LS_ACCEPTED, LS_BRACKET, LS_SMALL = 1, 2, 3
 
@@ -187,6 +188,8 @@ _SIGS = {
     'bsls_lbfgs_ls_work_size': (_sz, [_i64]),
     'bsls_lbfgs_ls_begin': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(LsState), _vp]),
     'bsls_lbfgs_ls_trials': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(LsState), _i64,
+                                    _vp]),
+    'bsls_lbfgs_ls_finish': (_int, [ctypes.POINTER(BBProblem), ctypes.POINTER(LsState), _vp, _vp,
                                     _vp]),
     'bsls_comm_id_bytes': (_sz, []),
     'bsls_comm_unique_id': (_int, [_vp]),

@@ -50,6 +50,7 @@ struct BBWork {
     double *p1, *p2, *pf;
     int32_t *wsc;
     double *dz;   // z - z_prev, written by K3 (and the prologue) for the next K2
+    uint64_t *hd; // K3's warm start: each pack's last run-head mask (<= n - nz packs)
     size_t bytes;
 };
 
@@ -78,6 +79,8 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     off += al16((size_t)(nz > 0 ? nz : 1) * 4);
     w.dz = (double *)(p + off);
     off += al16((size_t)(nz > 0 ? nz : 1) * 8);
+    w.hd = (uint64_t *)(p + off);
+    off += al16((size_t)(n - nz > 0 ? n - nz : 1) * 8);
     w.bytes = off;
     return w;
 }
@@ -301,11 +304,25 @@ __global__ __launch_bounds__(256) void bb_k1_sum(bsls_bb_problem P, int64_t iter
         bb_record_f(P, iter, tot[0], ITER);
 }
 
+// K1 with global atomics (BSLS_K1_ATOMIC): rows [r0, r1) of r start as
+// target (ADD) or 0 for the groups to add into; once the run has stopped, the
+// shard_role 1 rank keeps its r (the final residual) and the others write 0.
+template <bool ITER, bool ADD>
+__global__ __launch_bounds__(256) void bb_k1_init(bsls_bb_problem P, int64_t r0, int64_t r1) {
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
+        k1_stopped_rows(P, r0, r1, t0, gs);
+        return;
+    }
+    for (int64_t row = r0 + t0; row < r1; row += gs) P.r[row] = ADD ? P.target[row] : 0.0;
+}
+
 // K1 on a tile image (tiles.hpp): workgroup (rb, g) sums its rows over group
 // g's columns of x in LDS; with one group it finishes the block itself,
 // otherwise it publishes its partials (rpart, sc1) and the last of the block's
 // G workgroups finishes (group order) -- as bb_k1.
-template <int MODE, bool ITER, bool ADD, bool REDUCE>
+template <int MODE, bool ITER, bool ADD, bool REDUCE, bool ATOM = false>
 __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, unsigned *tkrb,
                                                double *part, unsigned *ticket, int64_t rb_base) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -316,8 +333,9 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
     tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, g);
     rb += rb_base;
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
-        // (several groups with the split finish: bb_k1_sum zeroes the rows)
-        if (g == 0 && (T.ngroups == 1 || !BSLS_K1_SPLIT))
+        // (several groups with the split finish: bb_k1_sum zeroes the rows;
+        // ATOM: bb_k1_init did)
+        if (!ATOM && g == 0 && (T.ngroups == 1 || !BSLS_K1_SPLIT))
             k1_stopped_rows(P, rb * T.H, (rb * T.H + T.H < P.m) ? rb * T.H + T.H : P.m,
                             threadIdx.x, blockDim.x);
         return;
@@ -332,6 +350,14 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
     if (G == 1) {
         k1_finish<ADD, REDUCE>(P, iter, ITER, rb, (unsigned)T.nrb, r0, r1, 1, lds, part, ticket,
                                red);
+        return;
+    }
+    if (ATOM) {
+        // r was set to target / 0 by bb_k1_init: every group adds its sums
+        // (global f64 atomics; the order over groups varies run to run, as the
+        // dealt walk's LDS sums do)
+        for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+            unsafeAtomicAdd(&P.r[row], lds[row - r0]);
         return;
     }
     if (BSLS_K1_SPLIT) {
@@ -788,7 +814,8 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
                                              const double *__restrict__ g,
                                              double *__restrict__ zn,
                                              double *__restrict__ dzo,
-                                             int32_t *__restrict__ wsc, int rec) {
+                                             int32_t *__restrict__ wsc, int rec,
+                                             uint64_t *__restrict__ hd) {
     const double sc[4] = {P.scal[BSLS_S_STOP], P.scal[BSLS_S_SUMDG], P.scal[BSLS_S_DZDG],
                           P.scal[BSLS_S_DGDG]};
     // rec (stage 13, the sliced sharded schedule): stage 12 folded in -- f and
@@ -823,7 +850,7 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
     __shared__ int pv_c[4][65];
     int64_t z0[K3_PPW], b0[K3_PPW];
     int L[K3_PPW];
-    uint64_t B[K3_PPW];
+    uint64_t B[K3_PPW], H[K3_PPW];
 #pragma unroll
     for (int q = 0; q < K3_PPW; ++q) {
         // unconditional loads at a clamped index (straight-line, one round trip)
@@ -833,6 +860,7 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
         b0[q] = P.pk_b0[pc];
         L[q] = pk < P.npacks ? P.pk_len[pc] : 0;
         B[q] = (uint64_t)P.pk_mask[pc];
+        H[q] = hd ? hd[pc] : 0ull;
     }
     double zv[K3_PPW], gv[K3_PPW], cv[K3_PPW], cv2[K3_PPW];
 #pragma unroll
@@ -857,15 +885,29 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
     for (int q = 0; q < K3_PPW; ++q)   // x_next = x - t g (BB.py:29)
         yv[q] = (l < L[q] && L[q] <= WAVE) ? zv[q] - t * gv[q] : 0.0;
     if (BSLS_K3_KO != 1) {
-        if (MERGE && K3_PPW == 2 && L[0] > 0 && L[0] <= WAVE && L[K3_PPW - 1] > 0 &&
-            L[K3_PPW - 1] <= WAVE) {
+        // warm start: the last run partition of each pack, tested first
+        // (pava_warm); a pack that passes needs no reference pass
+        bool need[K3_PPW];
+#pragma unroll
+        for (int q = 0; q < K3_PPW; ++q) {
+            need[q] = L[q] > 0 && L[q] <= WAVE;
+            if (hd && need[q] && (H[q] & B[q]) == B[q] && (H[q] & ~mask_lt(L[q])) == 0ull)
+                need[q] = !pava_warm(yv[q], L[q], B[q], H[q]);
+        }
+        uint64_t Hn[K3_PPW];
+        if (MERGE && K3_PPW == 2 && need[0] && need[K3_PPW - 1]) {
             pava_v1_wave_pair(yv[0], L[0], B[0], yv[K3_PPW - 1], L[K3_PPW - 1], B[K3_PPW - 1],
-                              pv_y[wv], pv_p[wv], pv_c[wv]);
+                              pv_y[wv], pv_p[wv], pv_c[wv], &Hn[0], &Hn[K3_PPW - 1]);
         } else {
 #pragma unroll
             for (int q = 0; q < K3_PPW; ++q)
-                if (L[q] > 0 && L[q] <= WAVE)
-                    pava_v1_wave_c(yv[q], L[q], B[q], pv_y[wv], pv_p[wv], pv_c[wv]);
+                if (need[q])
+                    pava_v1_wave_c(yv[q], L[q], B[q], pv_y[wv], pv_p[wv], pv_c[wv], &Hn[q]);
+        }
+        if (hd) {
+#pragma unroll
+            for (int q = 0; q < K3_PPW; ++q)   // the new partition for the next call
+                if (need[q] && l == 0) hd[w0 + q * nw] = Hn[q];
         }
     }
 #pragma unroll
@@ -1013,9 +1055,38 @@ static void launch_k1_mode(const bsls_bb_problem &P, int64_t iter, const BBWork 
                                      st>>>(P, iter, w.tkrb, w.p1, w.tk1, rb0);
 }
 
+// Several-group K1 without the partials: r initialised (bb_k1_init), every
+// group's sums added by global f64 atomics, ||r||^2 and the stop test
+// (REDUCE) by bb_r_finish.  The default on a column shard's partial residual
+// (stage 1): the rehearsed 8-way C5 rank-0 iteration 162.6 -> 148.4 us -- no
+// bb_k1_sum, and no 4 x 8 MB of partials through the Infinity Cache ahead of
+// K2.  On one GPU it measured no faster (C3 83.0 / 85.7 us, C5 800 / 801: the
+// ||r||^2 pass reads r again), and the atomics' varying order moves the exact
+// zero sum(dg) exit of BB.py:22 (a tests/fast problem stopped at 967 instead
+// of ~770), so one GPU keeps the group sums.  BSLS_K1_ATOMIC (environment,
+// read per launch): 0 = never, 1 = wherever K1 has several groups.
+static bool k1_atomic(const bsls_bb_problem &P, bool reduce) {
+    const char *e = getenv("BSLS_K1_ATOMIC");
+    if (e) return atoi(e) != 0;
+    return P.shard_role != 0 && !reduce;
+}
+
 template <int MODE, bool ADD, bool REDUCE, bool ITER>
 static void launch_k1t_mode(const bsls_bb_problem &P, int64_t iter, const BBWork &w,
                             hipStream_t st, int64_t rb0, int64_t rb1) {
+    if (P.At.ngroups > 1 && k1_atomic(P, REDUCE)) {
+        const int64_t r0 = rb0 * P.At.H, r1 = (rb1 * P.At.H < P.m) ? rb1 * P.At.H : P.m;
+        const int gi = grid_for(r1 - r0, 256);
+        bb_k1_init<ITER, ADD><<<gi < 1024 ? gi : 1024, 256, 0, st>>>(P, r0, r1);
+        allow_lds(bb_k1t<MODE, ITER, ADD, false, true>);
+        bb_k1t<MODE, ITER, ADD, false, true><<<(int)((rb1 - rb0) * P.At.ngroups),
+                                               BSLS_TILE_THREADS, tile_lds_doubles(P.At, false) * 8,
+                                               st>>>(P, iter, w.tkrb, w.p1, w.tk1, rb0);
+        if (REDUCE)
+            bb_r_finish<<<(grid_for(P.m, 256) < R_FINISH_GRID ? grid_for(P.m, 256) : R_FINISH_GRID),
+                          256, 0, st>>>(P, iter, w.pf, w.tkf, 0);
+        return;
+    }
     allow_lds(bb_k1t<MODE, ITER, ADD, REDUCE>);
     bb_k1t<MODE, ITER, ADD, REDUCE><<<(int)((rb1 - rb0) * P.At.ngroups), BSLS_TILE_THREADS,
                                       tile_lds_doubles(P.At, false) * 8, st>>>(P, iter, w.tkrb,
@@ -1103,12 +1174,13 @@ static bool k3_merge(const bsls_bb_problem &P) {
 template <int CV>
 static void launch_k3_cv(const bsls_bb_problem &P, int64_t iter, const double *zc,
                          const double *g, double *zn, const BBWork &w, hipStream_t st, int rec) {
+    uint64_t *hd = P.pava_warm ? w.hd : nullptr;   // (bsls_bb_problem.pava_warm)
     if (k3_merge(P))
         bb_k3<2, true, CV><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc,
-                                                                   rec);
+                                                                   rec, hd);
     else
         bb_k3<1, false, CV><<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.dz,
-                                                                    w.wsc, rec);
+                                                                    w.wsc, rec, hd);
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
@@ -1195,7 +1267,7 @@ __device__ __forceinline__ void ls_next(double *st, double *S1, double *S2, doub
 
 __global__ __launch_bounds__(256) void ls_begin_kernel(const double *__restrict__ d,
                                                        const double *__restrict__ gx, int64_t nz,
-                                                       const double *__restrict__ fx, double *st,
+                                                       const double *fx, double *st,
                                                        double *S1, double *S2, double *part,
                                                        unsigned *tickets) {
     __shared__ double red[2 * 4];
@@ -1209,13 +1281,14 @@ __global__ __launch_bounds__(256) void ls_begin_kernel(const double *__restrict_
     block_sum<2>(v, red);
     double tot[2];
     if (last_block_sum<2>(v, part, tickets, tot, red) && threadIdx.x == 0) {
+        const double f0 = *fx;    // (fx may point into st: the last search's st[FT])
         for (int k = 0; k < BSLS_LS_COUNT; ++k) st[k] = 0.0;
         for (int k = 0; k < BSLS_S_COUNT; ++k) S1[k] = S2[k] = 0.0;
         st[BSLS_LS_T] = 1.0;
         st[BSLS_LS_HI] = INFINITY;
         st[BSLS_LS_SLOPE] = tot[0];
         st[BSLS_LS_DNORM] = sqrt(tot[1]);
-        st[BSLS_LS_FX] = *fx;
+        st[BSLS_LS_FX] = f0;
         S1[BSLS_S_SUMDG] = 1.0;      // K3's t = S1[DZDG] / S1[DGDG] = -t
         S1[BSLS_S_DZDG] = -1.0;
         S1[BSLS_S_DGDG] = 1.0;
@@ -1249,6 +1322,35 @@ __global__ void ls_curv_kernel(double *st, double *S1, double *S2, double c2) {
         ls_next(st, S1, S2, (hi == INFINITY) ? 2 * t : 0.5 * (t + hi));
     } else {
         ls_stop(st, S1, S2, BSLS_LS_ACCEPTED);                  // both conditions pass (:39)
+    }
+}
+
+// after an accepted search: y = g(pt) - gx, s = t d (LBFGS.py:100-106, the
+// same elementwise roundings), y.s and g(pt).g(pt); gated on the state
+__global__ __launch_bounds__(256) void ls_finish_kernel(const double *__restrict__ d,
+                                                        const double *__restrict__ gx,
+                                                        const double *__restrict__ gpt, int64_t nz,
+                                                        double *st, double *y_out, double *s_out,
+                                                        double *part, unsigned *tickets) {
+    __shared__ double red[2 * 4];
+    if (st[BSLS_LS_STOP] != (double)BSLS_LS_ACCEPTED || st[BSLS_LS_DONE] != 0.0) return;
+    const double t = st[BSLS_LS_T];
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    double v[2] = {0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nz; i += gs) {
+        const double gi = gpt[i];
+        const double y = gi - gx[i], s = t * d[i];
+        if (y_out) y_out[i] = y;
+        if (s_out) s_out[i] = s;
+        v[0] += y * s;
+        v[1] += gi * gi;
+    }
+    block_sum<2>(v, red);
+    double tot[2];
+    if (last_block_sum<2>(v, part, tickets, tot, red) && threadIdx.x == 0) {
+        st[BSLS_LS_YS] = tot[0];
+        st[BSLS_LS_GG] = tot[1];
+        st[BSLS_LS_DONE] = 1.0;
     }
 }
 
@@ -1514,6 +1616,18 @@ extern "C" int bsls_lbfgs_ls_trials(const bsls_bb_problem *p, const bsls_ls_stat
         ls_curv_kernel<<<1, 64, 0, st>>>(s->st, s->S1, s->S2, s->c2);
         BSLS_LAUNCH_CHECK();
     }
+    return BSLS_OK;
+}
+
+extern "C" int bsls_lbfgs_ls_finish(const bsls_bb_problem *p, const bsls_ls_state *s,
+                                    double *y_out, double *s_out, void *stream) {
+    int rc = check_problem(p);
+    if (rc != BSLS_OK || (rc = check_ls(s)) != BSLS_OK) return rc;
+    constexpr int LS_GRID = 512;
+    const int g = grid_for(p->nz, 256);
+    ls_finish_kernel<<<g < LS_GRID ? g : LS_GRID, 256, 0, (hipStream_t)stream>>>(
+        s->d, s->gx, s->gpt, p->nz, s->st, y_out, s_out, s->part, s->tickets);
+    BSLS_LAUNCH_CHECK();
     return BSLS_OK;
 }
 

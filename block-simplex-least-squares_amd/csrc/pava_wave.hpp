@@ -222,11 +222,12 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
 // expand: element e (< L) takes the value of the last run starting at or
 // before it (runs with first elements O - obase in [0, L))
 __device__ __forceinline__ double wave_expand(const WaveRuns &s, double y, int L, int obase,
-                                              int *ps) {
+                                              int *ps, uint64_t *heads = nullptr) {
     const int t = lane_id();
     ps[t] = 0;
     if (t < s.nh) ps[s.O - obase] = 1;
     const uint64_t RS = __ballot(t < L && ps[t] != 0);
+    if (heads) *heads = RS;
     const int idx = mbcnt64(RS) + (int)((RS >> t) & 1ull) - 1;
     const double v = shfl_d(s.Y, idx < 0 ? 0 : idx);
     return (t < L) ? v : y;
@@ -237,12 +238,12 @@ __device__ __forceinline__ double wave_expand(const WaveRuns &s, double y, int L
 // expanded fit.  (The pass is VALU-bound: chain bounds come from a chain-start
 // table in LDS, not from 64-bit mask searches.)
 __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, double *ys,
-                                               int *ps, int *cst) {
+                                               int *ps, int *cst, uint64_t *heads = nullptr) {
     WaveRuns s = wave_runs(y, L, B, 0);
     const int maxpass = BSLS_K3_KO >= 2 ? BSLS_K3_KO - 2 : L;
     for (int pass = 0; pass <= maxpass; ++pass)
         if (!wave_pass(s, ys, ps, cst)) break;
-    y = wave_expand(s, y, L, 0, ps);
+    y = wave_expand(s, y, L, 0, ps, heads);
 }
 
 // Two packs in one wave (La, Lb <= 64 elements, one each per lane in ya /
@@ -255,7 +256,8 @@ __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, dou
 // needs.  ps: 128 ints.
 __device__ __forceinline__ void pava_v1_wave_pair(double &ya, int La, uint64_t Ba, double &yb,
                                                   int Lb, uint64_t Bb, double *ys, int *ps,
-                                                  int *cst) {
+                                                  int *cst, uint64_t *ha = nullptr,
+                                                  uint64_t *hb = nullptr) {
     const int t = lane_id();
     WaveRuns a = wave_runs(ya, La, Ba, 0), b = wave_runs(yb, Lb, Bb, 64);
     bool pa = wave_pass(a, ys, ps, cst);
@@ -282,6 +284,8 @@ __device__ __forceinline__ void pava_v1_wave_pair(double &ya, int La, uint64_t B
         if (t < m.nh) ps[m.O] = 1;
         const uint64_t RA = __ballot(t < La && ps[t] != 0);
         const uint64_t RB = __ballot(t < Lb && ps[WAVE + t] != 0);
+        if (ha) *ha = RA;
+        if (hb) *hb = RB;
         const int ia = mbcnt64(RA) + (int)((RA >> t) & 1ull) - 1;
         const int ib = __popcll(RA) + mbcnt64(RB) + (int)((RB >> t) & 1ull) - 1;
         const double va = shfl_d(m.Y, ia < 0 ? 0 : ia);
@@ -292,8 +296,64 @@ __device__ __forceinline__ void pava_v1_wave_pair(double &ya, int La, uint64_t B
     }
     for (int pass = 0; pa && pass <= La; ++pass) pa = wave_pass(a, ys, ps, cst);
     for (int pass = 0; pb && pass <= Lb; ++pass) pb = wave_pass(b, ys, ps, cst);
-    ya = wave_expand(a, ya, La, 0, ps);
-    yb = wave_expand(b, yb, Lb, WAVE, ps);
+    ya = wave_expand(a, ya, La, 0, ps, ha);
+    yb = wave_expand(b, yb, Lb, WAVE, ps, hb);
+}
+
+// ---------------------------------------------------------------------------
+// Warm start (K3 inside an iteration; the north star's 1e-12 contract, not
+// bit-identity).  PAVA's fit is unique: a partition of the pack into runs
+// (every block start a run start) IS the fit's partition iff, within each
+// block, the runs' means do not decrease from run to run and no run can be
+// split -- every proper prefix of a run has a mean >= the run's.  Between BB
+// iterations the partition rarely changes (oracle replay on a C3-shaped
+// problem, /tools/k3_warm.py: 75 % of packs keep it by iteration 20, 97 % by
+// 200), so K3 keeps each pack's final run-head mask H and first tests the
+// new input against it: one segmented scan (DPP, log steps) gives every
+// lane its run's prefix sum, the run sum comes from the run's last lane, and
+// two comparisons per lane decide.  If every lane passes, the fit is the run
+// means (sums in a tree order: within ulps of the reference's pooled
+// roundings); otherwise the pack runs the reference passes.  Comparisons that
+// fail only by rounding send the pack to the reference passes (still exact);
+// comparisons that pass only by rounding give a fit within ulps of the exact
+// one.  H must contain B (bit 0 set) and no bit at or above L.
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_mov_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, RM, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, RM, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ bool pava_warm(double &y, int L, uint64_t B, uint64_t H) {
+    const int l = lane_id();
+    const bool act = l < L;
+    const int h = hi_bit(H & mask_le(l));                    // this lane's run head
+    const uint64_t Hg = H & ~mask_le(l);
+    const int e = (Hg != 0ull && lo_bit(Hg) < L) ? lo_bit(Hg) - 1 : L - 1;   // its last lane
+    // segmented inclusive scan: s = y_h + ... + y_l
+    double s = act ? y : 0.0;
+    double u;
+    u = dpp_mov_d<0x111, 0xF>(s);                            // row_shr:1
+    s += (l - 1 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x112, 0xF>(s);                            // row_shr:2
+    s += (l - 2 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x114, 0xF>(s);                            // row_shr:4
+    s += (l - 4 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x118, 0xF>(s);                            // row_shr:8
+    s += (l - 8 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x142, 0xA>(s);                            // row_bcast:15 -> rows 1, 3
+    s += ((l & 16) != 0 && h <= (l & ~15) - 1) ? u : 0.0;
+    u = dpp_mov_d<0x143, 0xC>(s);                            // row_bcast:31 -> rows 2, 3
+    s += (l >= 32 && h <= 31) ? u : 0.0;
+    const double S = shfl_d(s, e);
+    const double m = S / (double)(e - h + 1);
+    const double mp = dpp_shr1_d(m);                         // the previous lane's run mean
+    const bool split_ok = (l == e) | (s >= (double)(l - h + 1) * m);
+    const bool order_ok = (l != h) | (((B >> l) & 1ull) != 0ull) | (mp <= m);
+    const bool ok = !act | (split_ok & order_ok);
+    if (ballot_b(!ok) != 0ull) return false;
+    if (act) y = m;
+    return true;
 }
 
 }  // namespace bsls

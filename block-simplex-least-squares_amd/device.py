@@ -775,26 +775,41 @@ class LineSearch:
                                self.st.data_ptr(), self.S[0].data_ptr(), self.S[1].data_ptr(),
                                self.part.data_ptr(), self.tickets.data_ptr(), self.c1, self.c2)
 
-    def search(self, x, d, gx, fx):
+    def search(self, x, d, gx, fx, y_out=None, s_out=None):
         """x (projected), d, gx = nabla_f(x): contiguous device vectors of nz;
         fx: f(x) as a one-element device tensor.  Returns (t, exit, trials,
-        ||d||) after one host read per chunk of trials."""
+        ||d||) after one host read per chunk of trials.  On the accepted exit
+        the same read also brings f(x_next), y.s and g(x_next).g(x_next)
+        (self.last = (f, ys, gg); bsls_lbfgs_ls_finish), with y = g(x_next) -
+        gx and s = t d written into y_out / s_out when given."""
         L = _native.lib()
         S = self._state(x, d, gx, fx)
         P = self.eng.P
-        check(L.bsls_lbfgs_ls_begin(P, S, stream_handle()), 'bsls_lbfgs_ls_begin')
+        st_h = stream_handle()
+        yp = y_out.data_ptr() if y_out is not None else None
+        sp = s_out.data_ptr() if s_out is not None else None
+        self.last = None
+        check(L.bsls_lbfgs_ls_begin(P, S, st_h), 'bsls_lbfgs_ls_begin')
         while True:
-            check(L.bsls_lbfgs_ls_trials(P, S, self.CHUNK, stream_handle()), 'bsls_lbfgs_ls_trials')
+            check(L.bsls_lbfgs_ls_trials(P, S, self.CHUNK, st_h), 'bsls_lbfgs_ls_trials')
+            check(L.bsls_lbfgs_ls_finish(P, S, yp, sp, st_h), 'bsls_lbfgs_ls_finish')
             st = self.st.cpu().numpy()
             if st[_native.LS_STOP] != 0:
+                if st[_native.LS_DONE] != 0:
+                    self.last = (float(st[_native.LS_FT]), float(st[_native.LS_YS]),
+                                 float(st[_native.LS_GG]))
                 return (float(st[_native.LS_T]), int(st[_native.LS_STOP]),
                         int(st[_native.LS_NTRIAL]), float(st[_native.LS_DNORM]))
 
     def take(self):
         """(x_next, nabla_f(x_next), f(x_next) as a one-element device tensor)
-        of the accepted trial, as new tensors."""
-        return (self.pt.clone(), self.gpt.clone(),
-                self.S[0][_native.S_FX:_native.S_FX + 1].clone())
+        of the accepted trial: the search's own buffers, handed over (fresh
+        ones are allocated for the next search, no copies); f(x_next) is a
+        view of the state's f(pt) slot, which the next search reads first."""
+        torch = _torch()
+        pt, gpt = self.pt, self.gpt
+        self.pt, self.gpt = torch.empty_like(pt), torch.empty_like(gpt)
+        return pt, gpt, self.st[_native.LS_FT:_native.LS_FT + 1]
 
 
 class BlockLayout:
@@ -1007,6 +1022,10 @@ class BBEngine:
         P.max_iter = int(opts.get('max_iter', 300000))
         P.opt_tol = float(opts.get('opt_tol', 1e-6))
         P.early_exit = 1 if early_exit else 0
+        # K3's warm start (pava_wave.hpp pava_warm: within ulps of the reference
+        # PAVA, not bit-identical): on unless deterministic; BSLS_K3_WARM=0/1
+        warm = os.environ.get('BSLS_K3_WARM')
+        P.pava_warm = int(warm) if warm is not None else (0 if deterministic else 1)
         self.P = P
         self.z0 = None
         if xin is not None:

@@ -363,6 +363,12 @@ typedef struct bsls_bb_problem {
     /* Column-sharded sliced schedule (stage 10): the rows [rr_lo, rr_hi) of r
      * whose ||r||^2 this rank sums (1/world of m each; 0, 0: all of them). */
     int64_t rr_lo, rr_hi;
+    /* 1: K3 first tests each pack's run partition from its previous call (the
+     * fit's partition rarely changes between iterations) and skips the PAVA
+     * passes where it still holds -- results within ulps of the reference
+     * PAVA (the north star's 1e-12), not bit-identical; 0: the reference
+     * passes always (bit-identical). */
+    int64_t pava_warm;
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
@@ -434,6 +440,8 @@ enum {
     BSLS_LS_DNORM = 6,     /* ||d|| */
     BSLS_LS_NTRIAL = 7,    /* trials evaluated */
     BSLS_LS_TLAST = 8, BSLS_LS_FT = 9, BSLS_LS_DGT = 10,   /* last trial: t, f(pt), d.g(pt) */
+    BSLS_LS_YS = 11, BSLS_LS_GG = 12,   /* after bsls_lbfgs_ls_finish: y.s, g(pt).g(pt) */
+    BSLS_LS_DONE = 13,     /* 1 once bsls_lbfgs_ls_finish has run on the accepted trial */
     BSLS_LS_COUNT = 16
 };
 enum { BSLS_LS_ACCEPTED = 1, BSLS_LS_BRACKET = 2, BSLS_LS_SMALL = 3 };
@@ -452,6 +460,15 @@ size_t bsls_lbfgs_ls_work_size(int64_t nz);
 int bsls_lbfgs_ls_begin(const bsls_bb_problem *p, const bsls_ls_state *s, void *stream);
 int bsls_lbfgs_ls_trials(const bsls_bb_problem *p, const bsls_ls_state *s, int64_t count,
                          void *stream);
+/* What LBFGS.solve forms after an accepted search (LBFGS.py:100-106): y = g(pt)
+ * - gx and s = t d (into y_out / s_out, nz doubles each, when not NULL, with
+ * the reference's elementwise roundings), st[YS] = y.s and st[GG] = g(pt).g(pt)
+ * (fixed-order block sums), so one read of st[] after the search carries
+ * everything the iteration's stopping rule needs.  Gated like the trials:
+ * enqueue it after every chunk; it runs once, on the accepted exit only.
+ * st[FT] then holds f(pt), and may be passed as the next search's fx. */
+int bsls_lbfgs_ls_finish(const bsls_bb_problem *p, const bsls_ls_state *s, double *y_out,
+                         double *s_out, void *stream);
 
 /* ---- multi-GPU: one rank's column-sharded iterations, RCCL in the loop ----
  * The reference has no parallel code; this is the driver of

@@ -178,6 +178,7 @@ def test_k3_wave_pava_bit_exact(cuda, orc, monkeypatch, merge):
     longer than 64)."""
     import torch
     monkeypatch.setenv('BSLS_K3_MERGE', merge)
+    monkeypatch.setenv('BSLS_K3_WARM', '0')      # the reference passes always
     import _native
     from device import BBEngine
     rs = np.random.RandomState(7)
@@ -219,6 +220,44 @@ def test_k3_wave_pava_bit_exact(cuda, orc, monkeypatch, merge):
         off = _native.load().bsls_bb_dz_offset(eng.m, eng.n, nz)
         dz = eng.work[off:off + 8 * nz].view(torch.float64).cpu().numpy()
         assert np.array_equal(dz.view(np.int64), (got - zc).view(np.int64)), trial
+
+
+@pytest.mark.parametrize('merge', ['1', '0'])
+def test_k3_warm_start_within_ulps(cuda, orc, monkeypatch, merge):
+    """K3 with the warm start (pava_warm): blocks of 2..150 routes, both pack
+    forms; repeated and slightly moved inputs (the kept partitions hold),
+    then an unrelated input (they fail and the reference passes run) -- every
+    result within 1e-12 of the oracle's PAVA, x = N z exact on the kernel's z."""
+    import torch
+    monkeypatch.setenv('BSLS_K3_MERGE', merge)
+    monkeypatch.setenv('BSLS_K3_WARM', '1')
+    import _native
+    from device import BBEngine
+    rs = np.random.RandomState(11)
+    sizes = np.concatenate([rs.randint(2, 40, size=300), [66, 65, 130, 2, 150, 64, 3]])
+    rs.shuffle(sizes)
+    n = int(sizes.sum())
+    A = sps.random(200, n, density=0.02, random_state=rs, format='csr')
+    eng = BBEngine(A, rs.randn(200), sizes, options={'max_iter': 10, 'opt_tol': 1e-30})
+    assert eng.P.pava_warm == 1
+    nz = eng.nz
+    base, g = rs.randn(nz), rs.randn(nz) * 0.5
+    res = []
+    for k, zc in enumerate((base, base, base + 1e-7 * rs.randn(nz), rs.randn(nz))):
+        eng.z[0][:nz].copy_(torch.from_numpy(zc))
+        eng.g[1][:nz].copy_(torch.from_numpy(g))
+        sc = np.zeros(_native.S_COUNT)
+        sc[_native.S_SUMDG], sc[_native.S_DZDG], sc[_native.S_DGDG] = 1.0, 0.37, 1.0
+        eng.scal.copy_(torch.from_numpy(sc))
+        eng.stage(4, 1)
+        got = eng.z[1][:nz].cpu().numpy()
+        ref = zc - 0.37 * g
+        orc.isotonic_regression_multi_c(ref, eng.layout.zstarts_h)
+        ref = np.maximum(np.minimum(ref, 1.0), 0.0)
+        assert np.max(np.abs(got - ref)) <= 1e-12, (k, np.max(np.abs(got - ref)))
+        assert np.array_equal(eng.x.cpu().numpy(), orc.block_sizes_to_N(sizes).dot(got)), k
+        res.append(np.array_equal(got, ref))
+    assert res[0] and not res[1]          # cold: the reference passes; repeated: warm
 
 
 def test_dense_row_network_falls_back_to_tiles(cuda, orc, monkeypatch):

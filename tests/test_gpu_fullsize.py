@@ -101,13 +101,59 @@ def test_c3_k3_pava_bit_exact(c3, orc):
     s[_native.S_DZDG] = 0.25
     s[_native.S_DGDG] = 1.0
     eng.scal.copy_(torch.from_numpy(s))
-    eng.stage(4, 1)          # iteration 1 reads z[0], g[1], writes z[1]
+    warm, eng.P.pava_warm = eng.P.pava_warm, 0      # the reference passes: bit-identical
+    try:
+        eng.stage(4, 1)          # iteration 1 reads z[0], g[1], writes z[1]
+    finally:
+        eng.P.pava_warm = warm
     got = eng.z[1][:nz].cpu().numpy()
     y = zc - 0.25 * g
     zs = eng.layout.zstarts_h
     orc.isotonic_regression_multi_c(y, zs)
     want = np.maximum(np.minimum(y, 1.0), 0.0)
     assert np.array_equal(got.view(np.int64), want.view(np.int64))
+
+
+def test_c3_k3_warm_start_within_ulps(c3, orc):
+    """K3 with the warm start (bsls_bb_problem.pava_warm, the engine default):
+    on the full C3 z layout, a first call (cold masks: the reference passes,
+    bit-identical), the same input again (every pack's partition holds: the
+    run means, within ulps) and slightly moved inputs (most partitions hold,
+    the rest run the passes) -- all within the north star's 1e-12 of the
+    oracle's PAVA, with x = N z and dz = z - z_prev exact on the kernel's own z."""
+    import torch
+    import _native
+    sh, b, eng = c3
+    rs = np.random.RandomState(9)
+    nz = eng.nz
+    zs = eng.layout.zstarts_h
+    base = rs.rand(nz)
+    g = rs.randn(nz)
+    warm, eng.P.pava_warm = eng.P.pava_warm, 1
+    outs = []
+    try:
+        for k, eps in enumerate((0.0, 0.0, 1e-6, 1e-3)):
+            zc = base + eps * rs.randn(nz)
+            eng.z[0][:nz].copy_(torch.from_numpy(zc))
+            eng.g[1][:nz].copy_(torch.from_numpy(g))
+            s = np.zeros(_native.S_COUNT)
+            s[_native.S_SUMDG], s[_native.S_DZDG], s[_native.S_DGDG] = 1.0, 0.25, 1.0
+            eng.scal.copy_(torch.from_numpy(s))
+            eng.stage(4, 1)
+            got = eng.z[1][:nz].cpu().numpy()
+            y = zc - 0.25 * g
+            orc.isotonic_regression_multi_c(y, zs)
+            want = np.maximum(np.minimum(y, 1.0), 0.0)
+            assert np.max(np.abs(got - want)) <= 1e-12, (k, np.max(np.abs(got - want)))
+            off = _native.load().bsls_bb_dz_offset(eng.m, eng.n, nz)
+            dz = eng.work[off:off + 8 * nz].view(torch.float64).cpu().numpy()
+            assert np.array_equal(dz.view(np.int64), (got - zc).view(np.int64)), k
+            outs.append((got, want))
+    finally:
+        eng.P.pava_warm = warm
+    # the repeated input took the warm path: its means round differently
+    # somewhere from the reference's pooled sequence
+    assert not np.array_equal(outs[1][0], outs[1][1])
 
 
 def test_c3_xspace_operator(c3):

@@ -361,15 +361,28 @@ def test_lbfgs_line_search_kernels_vs_reference_ls(cuda, orc):
         dd = torch.from_numpy(d.copy()).cuda()
         gd = eng.nabla_f(xd)
         fx = torch.tensor([eng.f(xd)], dtype=torch.float64, device='cuda')
-        t, why, ntr, dn = ls.search(xd, dd, gd, fx)
+        yo, so = torch.full_like(dd, np.nan), torch.full_like(dd, np.nan)
+        t, why, ntr, dn = ls.search(xd, dd, gd, fx, y_out=yo, s_out=so)
         assert abs(t - t_ref) <= 1e-12 * max(1.0, abs(t_ref)), (scale, t, t_ref)
         seen.add((why, ntr > 1))
         if why == _native.LS_ACCEPTED:
+            # bsls_lbfgs_ls_finish: y = g(x_next) - gx, s = t d, y.s, g.g, f(x_next)
+            f_last, ys, gg = ls.last
             xn, gn, fn = ls.take()
             want = P['proj'](x + t_ref * d)
+            g_want = P['nabla_f'](want)
             assert rel(xn.cpu().numpy(), want) < 1e-12
-            assert rel(gn.cpu().numpy(), P['nabla_f'](want)) < 1e-10
+            assert rel(gn.cpu().numpy(), g_want) < 1e-10
             assert abs(float(fn) - P['f'](want)) <= 1e-10 * max(1.0, abs(P['f'](want)))
+            assert float(fn) == f_last
+            y_want, s_want = gn.cpu().numpy() - gd.cpu().numpy(), t * d
+            assert np.array_equal(yo.cpu().numpy(), y_want)
+            assert np.array_equal(so.cpu().numpy(), s_want)
+            assert abs(ys - y_want.dot(s_want)) <= 1e-12 * max(1e-300, np.abs(y_want * s_want).sum())
+            gg_want = float(gn.cpu().numpy().dot(gn.cpu().numpy()))
+            assert abs(gg - gg_want) <= 1e-13 * gg_want
+        else:
+            assert ls.last is None
     assert any(w == _native.LS_ACCEPTED for w, _ in seen)
 
 

@@ -1,0 +1,21 @@
+#!/bin/bash
+# K3 warm start + LBFGS line-search finish: the LBFGS trace (device vs host
+# line search), the K3 / BB / plugin tests, then C3 and C5 bench lines.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/lbfgs_debug.py > gpurun_out/d_lbfgs_debug.log 2>&1
+echo "lbfgs_debug rc=$?"; grep -v "^ *search" gpurun_out/d_lbfgs_debug.log | tail -30
+timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread \
+    tests/test_gpu_bb.py tests/test_gpu_fullsize.py tests/test_gpu_c5.py > gpurun_out/d_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/d_tests.log; [ $rc -eq 0 ] || exit 1
+for wl in C3 C5; do
+  timeout -k 10 300 python -u bench.py --legs main --workload $wl --steps 200 --warmup 20 \
+      > gpurun_out/d_bench_$wl.json 2> gpurun_out/d_bench_$wl.err || exit 1
+  python - $wl <<'PY'
+import json, sys
+t = open('gpurun_out/d_bench_%s.json' % sys.argv[1]).read()
+d = json.loads(t[t.index('{'):])
+print(sys.argv[1], round(d['value'], 1), 'it/s', round(d['ms_per_step'] * 1e3, 1), 'us/it',
+      {k: round(v['avg_us'], 1) for k, v in d['kernels'].items() if k != 'formats'}, flush=True)
+PY
+done
