@@ -280,7 +280,13 @@ __device__ __forceinline__ double chain_lambda(const Chain &c) {
 // KB > 16: top-16 selection networks (proj_net.hpp) + the early-settling
 // chain; a wave with an unsettled lane sorts fully (the networks only
 // permute, the -inf padding stays put).
-template <int N, int KB, bool BALL>
+// THR (the sort-free path, bsls_proj_multi_*_fast): no sort and no chain --
+// Michelot's threshold iteration on the lane's registers: from the lower
+// bound tau = max(M - 1, (S - 1) / k) (M the block max, S its sum) each pass
+// sums the entries above tau and sets tau = (sum - 1) / count; the active
+// set only shrinks, and once its count repeats tau is the projection's
+// threshold.  Within ulps of the sorted chain (the north star's 1e-12).
+template <int N, int KB, bool BALL, bool THR = false>
 __device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int lane) {
     double v[N];
     double acc = 0.0;
@@ -303,7 +309,37 @@ __device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int 
     }
     const bool need = BALL ? (acc > 1.0) : true;
     double lam = 0.0;
-    if (!BALL || __builtin_amdgcn_ballot_w64(need)) {
+    if constexpr (THR) {
+        if (!BALL || __builtin_amdgcn_ballot_w64(need)) {
+            double M = -INFINITY, S = 0.0;
+#pragma unroll
+            for (int j = 0; j < KB; ++j) {
+                M = fmax(M, v[j]);
+                S += (j < k) ? v[j] : 0.0;
+            }
+            double tau = fmax(M - 1.0, (S - 1.0) / (double)(k > 0 ? k : 1));
+            bool done = (k == 0) || !need;
+            int cp = -1;
+            for (int it = 0; it <= KB + 1; ++it) {
+                if (__builtin_amdgcn_ballot_w64(!done) == 0ull) break;
+                double sa = 0.0;
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < KB; ++j) {
+                    const bool a = v[j] > tau;
+                    sa += a ? v[j] : 0.0;
+                    c += a ? 1 : 0;
+                }
+                const double tn = (sa - 1.0) / (double)(c > 0 ? c : 1);
+                if (!done) {
+                    done = (c == cp);
+                    tau = tn;
+                    cp = c;
+                }
+            }
+            lam = -tau;
+        }
+    } else if (!BALL || __builtin_amdgcn_ballot_w64(need)) {
         bool full = true;
         if constexpr (KB > 16) {
             // level 1: the 16 largest, sorted, and the chain over them;
@@ -361,7 +397,7 @@ __device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int 
 // sort / store phases staggered instead of all together -- wave w's loads
 // stream while wave w - 1 sorts.  Every wave bumps the counter exactly once,
 // whatever path it takes, so no wave waits forever.
-template <bool BALL, int W>
+template <bool BALL, int W, bool THR = false>
 __device__ __forceinline__ void lds_group(double *__restrict__ y,
                                           const int64_t *__restrict__ starts, int64_t nb,
                                           int64_t n, int64_t *__restrict__ big_list,
@@ -448,13 +484,13 @@ __device__ __forceinline__ void lds_group(double *__restrict__ y,
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     const int off = (k > 0) ? (int)(s - s0) + sh : 0;
-    if (kmax <= 8) lane_block_lds<8, 8, BALL>(buf, off, k, lane);
-    else if (kmax <= 16) lane_block_lds<16, 16, BALL>(buf, off, k, lane);
-    else if (kmax <= 32) lane_block_lds<32, 32, BALL>(buf, off, k, lane);
-    else if (kmax <= 40) lane_block_lds<64, 40, BALL>(buf, off, k, lane);
-    else if (kmax <= 48) lane_block_lds<64, 48, BALL>(buf, off, k, lane);
-    else if (kmax <= 56) lane_block_lds<64, 56, BALL>(buf, off, k, lane);
-    else lane_block_lds<64, 64, BALL>(buf, off, k, lane);
+    if (kmax <= 8) lane_block_lds<8, 8, BALL, THR>(buf, off, k, lane);
+    else if (kmax <= 16) lane_block_lds<16, 16, BALL, THR>(buf, off, k, lane);
+    else if (kmax <= 32) lane_block_lds<32, 32, BALL, THR>(buf, off, k, lane);
+    else if (kmax <= 40) lane_block_lds<64, 40, BALL, THR>(buf, off, k, lane);
+    else if (kmax <= 48) lane_block_lds<64, 48, BALL, THR>(buf, off, k, lane);
+    else if (kmax <= 56) lane_block_lds<64, 56, BALL, THR>(buf, off, k, lane);
+    else lane_block_lds<64, 64, BALL, THR>(buf, off, k, lane);
     if constexpr (W == 1) __syncthreads();
     else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // out: 16-B write-through (sc1) stores of the aligned pairs -- the bytes
@@ -489,7 +525,7 @@ __device__ __forceinline__ void lds_group(double *__restrict__ y,
 
 // (64 W, 2): at most 256 VGPRs so two waves fit per SIMD -- the whole C2 grid
 // (~6 waves per CU) is then resident at once.
-template <bool BALL, int W>
+template <bool BALL, int W, bool THR = false>
 __global__ __launch_bounds__(64 * W, 2) void proj_lds_kernel(double *__restrict__ y,
                                                           const int64_t *__restrict__ starts,
                                                           int64_t nb, int64_t n,
@@ -508,8 +544,8 @@ __global__ __launch_bounds__(64 * W, 2) void proj_lds_kernel(double *__restrict_
         if (threadIdx.x == 0) landed = 0;
         __syncthreads();
     }
-    lds_group<BALL, W>(y, starts, nb, n, big_list, big_count, allow_big, buf[wv], &landed,
-                       (int64_t)blockIdx.x * W + wv, wv, lane);
+    lds_group<BALL, W, THR>(y, starts, nb, n, big_list, big_count, allow_big, buf[wv], &landed,
+                            (int64_t)blockIdx.x * W + wv, wv, lane);
 }
 
 // In-place descending bitonic sort of u[0..P) by the whole workgroup
@@ -974,14 +1010,19 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
         const int v = e ? atoi(e) : 2;
         return (v == 1 || v == 3) ? v : 2;
     }();
-    // the sort-free path: lanes per block (BSLS_PROJ_LPB, A/B), 4 by default
+    // the sort-free path: one lane per block (Michelot on the staged block,
+    // proj_lds_kernel<BALL, 2, true>) unless BSLS_PROJ_LPB (A/B) asks for
+    // proj_thr_kernel's 2 / 4 / 8 lanes per block
     static const int lpb = [] {
         const char *e = getenv("BSLS_PROJ_LPB");
-        const int v = e ? atoi(e) : 4;
-        return (v == 2 || v == 8) ? v : 4;
+        const int v = e ? atoi(e) : 0;
+        return (v == 2 || v == 4 || v == 8) ? v : 0;
     }();
     const int64_t ngrp = (nb + WAVE - 1) / WAVE;
-    if (fast) {
+    if (fast && lpb == 0) {
+        proj_lds_kernel<BALL, 2, true><<<(unsigned)((ngrp + 1) / 2), 2 * WAVE, 0, st>>>(
+            y, starts, nb, n, w.list, w.count, max_block > SMALL_MAX, gate);
+    } else if (fast) {
         const int64_t waves = (nb + WAVE / lpb - 1) / (WAVE / lpb);
         const unsigned grid = (unsigned)((waves + 3) / 4);
         if (lpb == 2)
