@@ -166,9 +166,9 @@ def bench_stored_values(sh, b, steps, warmup, codec=None):
 
 def bench_proj(reps=30, batch=16, fast=False):
     """C2 proj_multi_simplex (100k blocks x mean 32, 3.2M fp64) on the device,
-    every launch on fresh input: the sort-free path (bsls_proj_multi_simplex_fast,
-    the north star's 1e-12 contract) or, fast=False, the bit-identical sorting
-    path.  avg_us: `batch` launches back to back on `batch` distinct copies of
+    every launch on fresh input: the sort-free path (bsls_proj_multi_simplex_fast:
+    Michelot's threshold passes, one lane per block, the north star's 1e-12
+    contract) or, fast=False, the bit-identical sorting path.  avg_us: `batch` launches back to back on `batch` distinct copies of
     the input between two events on the launch stream (the stream held by a
     spin kernel while the host enqueues) -- the kernel time rocprofv3 reports,
     HBM-fed, dispatch gaps amortised; isolated_*: one launch per event pair
@@ -230,7 +230,7 @@ def bench_proj(reps=30, batch=16, fast=False):
     rel = float(np.max(np.abs(out - yc) / np.maximum(1.0, np.abs(yc))))
     return {'entry': name, 'n': n, 'blocks': p, 'avg_us': us, 'GB_s': byt / (us * 1e-6) / 1e9,
             'alg_bytes': byt, 'frac_hbm_peak': byt / (us * 1e-6) / HBM_PEAK,
-            'rocprof_kernels': ['proj_thr_kernel' if fast else 'proj_lds_kernel'],
+            'rocprof_kernels': ['proj_lds_kernel<false, 2, %s>' % ('true' if fast else 'false')],
             'isolated_median_us': med * 1e3, 'isolated_min_us': ms[0] * 1e3,
             'cpu_oracle_ms_1thread': cpu_s * 1e3,
             'max_rel_diff_vs_oracle': rel, 'within_1e-12': rel <= 1e-12,

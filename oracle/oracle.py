@@ -508,6 +508,35 @@ def sparse_parts(A, b, block_starts, lasso=False):
     return obj, proj, line_search
 
 
+def batch_solve(obj, proj, step_size, x_init, line_search=None, f_min=None, opt_tol=1e-6,
+                max_iter=2000, prog_tol=1e-12):
+    """BATCH.py:7-52, projected gradient descent with an optional line search
+    (progress times dropped: [k, f])."""
+    n = x_init.shape[0]
+    x = np.copy(x_init)
+    g, g_new, x_new = np.zeros(n), np.zeros(n), np.zeros(n)
+    f_old = np.inf
+    i = 1
+    f = obj(x, g)
+    progress = [f]
+    while True:
+        flag, stop = batch_stopping(i, max_iter, f, f_old, opt_tol, prog_tol, f_min)
+        if flag:
+            break
+        t = step_size(i)
+        np.add(x, -t * g, x_new)
+        proj(x_new)
+        f_new = obj(x_new, g_new)
+        if line_search is not None:
+            f_new = line_search(x, f, g, x_new, f_new, g_new, i)
+        f_old, f = f, f_new
+        np.copyto(x, x_new)
+        np.copyto(g, g_new)
+        i += 1
+        progress.append(f)
+    return {'f': f, 'x': x, 'stop': stop, 'iterations': i, 'progress': np.array(progress)}
+
+
 def batch_solve_bb(obj, proj, line_search, x_init, f_min=None, opt_tol=1e-6, max_iter=2000,
                    prog_tol=1e-12):
     """BATCH.py:55-106 (progress times dropped: [k, f])."""

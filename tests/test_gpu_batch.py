@@ -156,6 +156,37 @@ def test_fused_engine_larger_problem_matches_closure_loop(cuda, orc):
         assert np.max(np.abs(prog - r["progress"]) / np.abs(r["progress"])) < 1e-8
 
 
+@pytest.mark.parametrize('with_ls', [False, True])
+def test_batch_solve_sparse_vs_oracle(cuda, orc, with_ls):
+    """BATCH.solve (projected gradient descent, BATCH.py:7-52) on a sparse
+    100k-route problem (get_solver_parts(is_sparse=True): the device
+    objective and projection, the decreasing step of algorithm_utils.py:97-100,
+    with and without the backtracking line search) against the oracle's
+    restatement over SciPy (oracle.batch_solve / sparse_parts): the same
+    iteration count and stop, iterates within 1e-6, objective trace within
+    1e-8."""
+    import BATCH
+    from algorithm_utils import get_solver_parts
+    from synthetic import make_shard, add_noise
+    sh = make_shard(100_000, 5_000, 10_000, 16, seed=4)
+    b = add_noise(sh['Ax'], 0.02, seed=4)
+    sizes = sh['block_sizes']
+    starts = np.concatenate(([0], np.cumsum(sizes)[:-1]))
+    x0 = np.repeat(1.0 / sizes, sizes)
+    # (min_eig 1e7: steps t = 1 / (1e7 i + 1), small enough for the plain
+    # projected descent to make progress on this matrix)
+    step, proj, ls, obj = get_solver_parts((sh['A'], b), starts, 1e7, is_sparse=True)
+    sol = BATCH.solve(obj, proj, step, x0.copy(), ls if with_ls else None, max_iter=25)
+    o_obj, o_proj, o_ls = orc.sparse_parts(sh['A'], b, starts)
+    r = orc.batch_solve(o_obj, o_proj, step, x0.copy(), o_ls if with_ls else None, max_iter=25)
+    assert sol['iterations'] == r['iterations'] and sol['stop'] == r['stop'], (sol['stop'], r['stop'])
+    assert rel(sol['x'], r['x']) < 1e-6
+    prog = np.array([q[1] for q in sol['progress']])
+    assert prog.shape == r['progress'].shape
+    assert np.max(np.abs(prog - r['progress']) / np.abs(r['progress'])) < 1e-8
+    assert r['progress'][-1] < r['progress'][0]          # the run made progress
+
+
 LBFGS_RUNS = [(k, 50) for k in (2, 3, 6, 7, 10, 15, 40, 2000)] + [(30, 3)]
 
 

@@ -18,7 +18,7 @@ print('%-14s %8.1f it/s  %6.1f us/it  %s' % (sys.argv[1], d['value'], d['ms_per_
       flush=True)
 PY
 }
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   run default_$rep || exit 1
   run k2one_$rep BSLS_TILE_PLAN_AT=4883,1 || exit 1
   run nowarm_$rep BSLS_K3_WARM=0 || exit 1
