@@ -21,9 +21,14 @@ struct LsqWork {
     unsigned *tk;       // ||r||^2 hand-off
     unsigned *tkrb;     // one ticket per row block
     double *part;       // one partial per row block
-    double *xmax;       // fixed-point residual: max |x| (of colv * x when scaled), as bits
+    double *xmax;       // fixed-point residual: max |x| (of colv * x when scaled), as bits,
+                        //   in XMAX_SLOTS slots (the max over them)
     size_t bytes;
 };
+// one 64-bit atomic max per workgroup into slot blockIdx % XMAX_SLOTS: a
+// single word took every wave's atomic in turn (~11 ns each: 4096 waves made
+// the C3 x-space round 105 -> 148 us)
+constexpr int XMAX_SLOTS = 64;
 
 static size_t lal(size_t v) { return (v + 255) & ~(size_t)255; }
 
@@ -39,23 +44,24 @@ static LsqWork lsq_layout(void *base, int64_t A_npanels) {
     w.part = (double *)(p + off);
     off += lal((size_t)rbs * 8);
     w.xmax = (double *)(p + off);
-    off += lal(8);
+    off += lal(XMAX_SLOTS * 8);
     w.bytes = off;
     return w;
 }
 
 // max |x| over n entries (with colv: of xs = colv * x, written on the way):
 // the bit patterns of non-negative doubles order as unsigned integers (a NaN's
-// above inf's, as nan_max wants), so each wave's max goes to *xmax by one
-// 64-bit atomic max -- order-free, hence the same at the same x -- over a
-// grid as wide as the scaling pass (a last-block reduction over 512
-// workgroups took 9.9 us here against 5.7 for the plain scaling pass).
-// *xmax is 0 on entry: the workspace starts zeroed and lsq_t_sum, which runs
-// after the walk that reads it, clears it again.
+// above inf's, as nan_max wants), so each workgroup's max goes to one of
+// XMAX_SLOTS words by a 64-bit atomic max -- order-free, hence the same at
+// the same x -- over a grid as wide as the scaling pass (a last-block
+// reduction over 512 workgroups took 9.9 us here against 5.7 for the plain
+// scaling pass).  The slots are 0 on entry: the workspace starts zeroed and
+// lsq_t_sum, which runs after the walk that reads them, clears them again.
 __global__ __launch_bounds__(256) void lsq_xmax_kernel(double *__restrict__ xs,
                                                        const double *__restrict__ colv,
                                                        const double *__restrict__ x, int64_t n,
                                                        double *xmax) {
+    __shared__ unsigned long long wmax[4];
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     double mx = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -72,8 +78,22 @@ __global__ __launch_bounds__(256) void lsq_xmax_kernel(double *__restrict__ xs,
         const unsigned long long t = __shfl_xor(b, o);
         b = t > b ? t : b;
     }
-    if ((threadIdx.x & 63) == 0 && b != 0ull)
-        atomicMax(reinterpret_cast<unsigned long long *>(xmax), b);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) b = wmax[w] > b ? wmax[w] : b;
+        if (b != 0ull)
+            atomicMax(reinterpret_cast<unsigned long long *>(xmax) + blockIdx.x % XMAX_SLOTS, b);
+    }
+}
+
+// the max over the slots (every workgroup of the walk reads the 64 words)
+__device__ __forceinline__ double xmax_of(const double *xmax) {
+    unsigned long long b = 0ull;
+    const unsigned long long *w = reinterpret_cast<const unsigned long long *>(xmax);
+#pragma unroll 16
+    for (int k = 0; k < XMAX_SLOTS; ++k) b = w[k] > b ? w[k] : b;
+    return __longlong_as_double((long long)b);
 }
 
 __global__ __launch_bounds__(256) void lsq_scale_kernel(double *__restrict__ xs,
@@ -214,7 +234,7 @@ __global__ __launch_bounds__(1024) void lsq_k1t_fx(bsls_tiles T, int64_t m,
     extern __shared__ __attribute__((aligned(16))) double lds[];
     int64_t rb, g;
     tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, g);
-    const double B = amax * *xmax;
+    const double B = amax * xmax_of(xmax);
     int ex = 0;
     if (B > 0.0 && B <= 1.7976931348623157e308) (void)frexp(B, &ex);
     const double fxs = ldexp(1.0, 50 - ex), inv = ldexp(1.0, ex - 50);
@@ -238,8 +258,8 @@ __global__ __launch_bounds__(256) void lsq_t_sum(int64_t m, int64_t G, const dou
                                                  double *part, unsigned *ticket,
                                                  double *xmax_clear = nullptr) {
     __shared__ double red[4];
-    // the fixed-point walk that read *xmax has finished: ready for the next call
-    if (xmax_clear && blockIdx.x == 0 && threadIdx.x == 0) *xmax_clear = 0.0;
+    // the fixed-point walk that read the max has finished: ready for the next call
+    if (xmax_clear && blockIdx.x == 0 && threadIdx.x < XMAX_SLOTS) xmax_clear[threadIdx.x] = 0.0;
     const int64_t gs = (int64_t)gridDim.x * blockDim.x;
     double sq[1] = {0.0};
     for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < m; row += gs) {

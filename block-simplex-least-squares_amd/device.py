@@ -311,13 +311,12 @@ def tile_plan(rows, cols, halo=0, colv_lds=False, cus=256, l2_slice=None, env=No
         nrb = max(nmin, cus // G)
         nrb = -(-(nrb * G) // cus) * cus // G if nrb * G > cus else nrb
         H = max(64, -(-rows // nrb))
-        if halo and nnz and nrb % 2 == 0 and 2 * H <= hmax and cols >= 2 and \
-                nnz / nrb / cols < 0.15:
-            # K2 tiles this sparse (a C5 shard over 8 GPUs: 0.08 entries per
-            # column) take two groups of twice the rows, 4x the density: C5/8
-            # K2 78.0 -> 72.5 us (C3 at 0.62 and C5 at 0.31 entries per column
-            # stay at one group: 2 groups measured 45.7 / 510 against 35.6 / 358)
-            G, nrb, H = 2, nrb // 2, 2 * H
+        # (K2 tiles as sparse as a C5 shard over 8 GPUs, 0.08 entries per
+        # column, were given two groups of twice the rows until round 4: the
+        # kernel alone 78.0 -> 72.5 us, but the rehearsed iteration is faster
+        # with one group -- 160.7 against 149.6 us, 162.5 against 154.4 in an
+        # earlier session -- the groups' partial row sums (2 x 10 MB through the
+        # Infinity Cache) cost K1 and K3 more than K2 gains; tools/shard_ab_r04.sh)
         return int(H), int(G), 0
     if l2_slice is None:
         # measured on the C5 shard (tools/stage_time.py): K1 fastest with
