@@ -350,8 +350,9 @@ def bench_lbfgs(sh, b, rounds=16, reps=10, corrections=50):
 def bench_gd_lbfgs(sh, b, iters=20, reps=20, m=50):
     """LBFGS.solve (python/LBFGS.py:56-123) through GradientDescent('LBFGS') on
     the C3 z-space problem over the BBEngine closures: wall time per
-    iteration (weak Wolfe line search decisions on the host, as the
-    reference), and the device direction alone (csrc/lbfgs.hip: multi-dot
+    iteration (the weak Wolfe line search decided on the device,
+    device.LineSearch; its first iteration's search on the host, as
+    LBFGS.solve does before x is a projected point), and the device direction alone (csrc/lbfgs.hip: multi-dot
     of {g, y_new, s_new} against the 2m + 2 history columns, one-wave
     recursion, combine over 2m + 1 vectors, the push) on a full ring of m
     pairs, timed with HIP events on the stream it runs on.  Algorithmic
@@ -364,14 +365,26 @@ def bench_gd_lbfgs(sh, b, iters=20, reps=20, m=50):
     from gradient_descent import GradientDescent
     opts = {'max_iter': iters, 'verbose': 0, 'opt_tol': 1e-30}
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options=opts, AT=sh['AT'])
-    gd = GradientDescent(z0=np.zeros(eng.nz), method='LBFGS', options=dict(opts), engine=eng)
+    # z0 resident on the device, like every other input of a timed region (a
+    # numpy z0 costs GradientDescent a 7.6-MB pageable upload, ~26 ms here)
+    z0d = torch.zeros(eng.nz, dtype=torch.float64, device='cuda')
+    gd = GradientDescent(z0=z0d, method='LBFGS', options=dict(opts), engine=eng)
     gd.run()                                    # warm (allocations, first launches)
     torch.cuda.synchronize()
-    gd = GradientDescent(z0=np.zeros(eng.nz), method='LBFGS', options=dict(opts), engine=eng)
-    t0 = time.perf_counter()
-    iters_, _, _ = gd.run()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
+
+    def timed(k):
+        o = dict(opts, max_iter=k)
+        gd = GradientDescent(z0=z0d, method='LBFGS', options=o, engine=eng)
+        t0 = time.perf_counter()
+        it, _, _ = gd.run()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, int(it[-1])
+    wall, n1 = timed(iters)
+    # the marginal cost of an iteration: a run twice as long, minus this one
+    # (the first iteration's line search runs on the host over the closures --
+    # LBFGS.solve's x0 is not a projected point -- and weighs on a short run)
+    wall2, n2 = timed(2 * iters)
+    iters_ = [n1]
     n = eng.nz
     rs = np.random.RandomState(1)
     H = LBFGS._DeviceHistory(torch.zeros(n, dtype=torch.float64, device='cuda'), m)
@@ -394,6 +407,8 @@ def bench_gd_lbfgs(sh, b, iters=20, reps=20, m=50):
     torch.cuda.empty_cache()
     return {'n': n, 'corrections': m, 'iterations': int(iters_[-1]),
             'ms_per_iteration': wall * 1e3 / max(int(iters_[-1]), 1),
+            'ms_per_iteration_marginal': ((wall2 - wall) * 1e3 / (n2 - n1)) if n2 > n1 else None,
+            'iterations_long_run': n2,
             'direction': {'us': us, 'alg_bytes': byts, 'achieved_GB_s': byts / us * 1e-3,
                           'peak_GB_s': HBM_PEAK / 1e9, 'frac': byts / us * 1e-3 / (HBM_PEAK / 1e9),
                           'note': 'direction + push per iteration (multi-dot, coef, combine, '

@@ -163,23 +163,37 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
             Y = Y[1:] + [y_new]
             S = S[1:] + [s_new]
             rho = rho[1:] + [rho_new]
-        if ls is not None and fx_dev is not None:
-            # x = proj(x) (the last x_next) and g_new = nabla_f(x): the line
-            # search's proj(x) / nabla_f(proj(x)) (LBFGS.py:18-19) are these.
-            # On the accepted exit the search's one read per chunk also brings
-            # f(x_next), y.s and g.g, and y / s land in the history's buffers.
-            yb = hist.yn if hist is not None else None
-            sb = hist.sn if hist is not None else None
-            t, why, _, dnorm = ls.search(x, d, g_new, fx_dev, y_out=yb, s_out=sb)
+        if ls is not None:
+            # the search's proj(x), nabla_f(proj(x)), f(proj(x)) (LBFGS.py:18-20):
+            # after the first iteration x is the last x_next (projected) and
+            # g_new = nabla_f(x), f(x) already on the device; the first
+            # iteration's x0 is not projected, so they are formed here once
+            # (the trials project x + t d themselves).  On the accepted exit
+            # the search's one read per chunk also brings f(x_next), y.s and
+            # g.g, and y / s land in the history's buffers -- except on the
+            # first iteration, whose y = g(x_next) - nabla_f(x0) is not the
+            # search's g(x_next) - nabla_f(proj(x0)).
+            first = fx_dev is None
+            if first:
+                px = proj(x)
+                gx = nabla_f(px)
+                fx_dev = px.new_tensor([f(px)])
+            else:
+                gx = g_new
+            yb = hist.yn if (hist is not None and not first) else None
+            sb = hist.sn if (hist is not None and not first) else None
+            t, why, _, dnorm = ls.search(x, d, gx, fx_dev, y_out=yb, s_out=sb)
             g = g_new
             if why == 1 and ls.last is not None:     # accepted: the last trial is x_next
                 x_next, g_new, fx_dev = ls.take()
                 fx, ys, gg = ls.last
-                if hist is not None:
+                if yb is not None:
                     y_new, s_new = hist.yn, hist.sn
                 else:
                     s_new = t * d
                     y_new = g_new - g
+                    if first:
+                        ys, gg = _host_floats(y_new.dot(s_new), g_new.dot(g_new))
             else:              # t was never evaluated (the two other exits)
                 s_new = t * d
                 x_next = proj(x + s_new)
