@@ -702,13 +702,29 @@ def kernel_table(eng, it0, reps, world, m, n, nz, p, nnz):
     kern = {}
     for stg, nm in ((3, 'K2_spmvT_Nt_dots'), (4, 'K3_pava_clip_z2x'), (k1, 'K1_spmv_A')):
         torch.cuda._sleep(int(2e8))
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
-        for _ in range(reps):
-            eng.stage(stg, it0)
-        ev[1].record()
-        torch.cuda.synchronize()
-        us = ev[0].elapsed_time(ev[1]) * 1e3 / reps
+        if stg == 4 and world == 1:
+            # K3 keeps each pack's PAVA partition from its last call (the warm
+            # start): relaunched on one state every partition holds, so it is
+            # timed inside real iterations instead (K2, then K3 between two
+            # events, then K1, iteration after iteration), as the loop runs it
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(reps)]
+            for k in range(reps):
+                eng.stage(3, it0 + k)
+                evs[k][0].record()
+                eng.stage(4, it0 + k)
+                evs[k][1].record()
+                eng.stage(7, it0 + k)
+            torch.cuda.synchronize()
+            us = sum(a.elapsed_time(b) for a, b in evs) * 1e3 / reps
+        else:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(reps):
+                eng.stage(stg, it0)
+            ev[1].record()
+            torch.cuda.synchronize()
+            us = ev[0].elapsed_time(ev[1]) * 1e3 / reps
         kern[nm] = {'avg_us': us, 'alg_bytes': kb[nm], 'GB_s': kb[nm] / (us * 1e-6) / 1e9,
                     'frac': kb[nm] / (us * 1e-6) / HBM_PEAK, 'format_bytes': fb[nm],
                     'format_GB_s': fb[nm] / (us * 1e-6) / 1e9,
