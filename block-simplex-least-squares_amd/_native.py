@@ -117,7 +117,7 @@ class LsqOp(ctypes.Structure):
     """Mirror of struct bsls_lsq_op (include/bsls_hip.h)."""
     _fields_ = [('m', _i64), ('n', _i64), ('A', Panels), ('AT', Panels), ('colv', _vp),
                 ('rpart', _vp), ('xs', _vp), ('work', _vp), ('work_bytes', _sz),
-                ('At', Tiles), ('ATt', Tiles), ('fixed', _i64), ('fx_amax', _dbl)]
+                ('At', Tiles), ('ATt', Tiles), ('fixed', _i64), ('fx_amax', _dbl), ('x_bound', _dbl)]
 
 
 class XBBProblem(ctypes.Structure):

@@ -230,11 +230,12 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void lsq_k1t_fx(bsls_tiles T, int64_t m,
                                                    const double *__restrict__ x,
                                                    double *__restrict__ rpart,
-                                                   const double *__restrict__ xmax, double amax) {
+                                                   const double *__restrict__ xmax, double amax,
+                                                   double xb) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     int64_t rb, g;
     tile_map(T, blockIdx.x, gridDim.x / T.ngroups, rb, g);
-    const double B = amax * xmax_of(xmax);
+    const double B = amax * (xb > 0.0 ? xb : xmax_of(xmax));
     int ex = 0;
     if (B > 0.0 && B <= 1.7976931348623157e308) (void)frexp(B, &ex);
     const double fxs = ldexp(1.0, 50 - ex), inv = ldexp(1.0, ex - 50);
@@ -346,6 +347,7 @@ static bool lsq_ok(const bsls_lsq_op *op) {
     if (op->fixed && (!op->At.ent || (op->At.layout & 3) == 0 || !(op->fx_amax > 0.0) ||
                       op->fx_amax > 1e300 || (op->colv && !op->xs)))
         return false;
+    if (!(op->x_bound >= 0.0) || op->x_bound > 1e300) return false;
     if (op->colv && !op->xs) return false;
     if (!op->ATt.ent && (op->colv ? T.val != nullptr : !T.val)) return false;
     if (!op->At.ent && (op->colv ? A.val != nullptr : !A.val)) return false;
@@ -371,8 +373,16 @@ extern "C" int bsls_lsq_residual(const bsls_lsq_op *op, const double *d_x, const
     hipStream_t st = (hipStream_t)stream;
     if (op->At.ent && op->fixed) {
         const bsls_tiles &K = op->At;
-        lsq_xmax_kernel<<<grid_for(op->n < 262144 ? op->n : 262144, 256), 256, 0, st>>>(
-            op->xs, op->colv, d_x, op->n, w.xmax);
+        const double xb = op->x_bound;
+        if (xb > 0.0) {
+            // the caller's bound (bsls_lsq_op.x_bound): only colv * x to form
+            if (op->colv)
+                lsq_scale_kernel<<<grid_for(op->n < 262144 ? op->n : 262144, 256), 256, 0, st>>>(
+                    op->xs, op->colv, d_x, op->n);
+        } else {
+            lsq_xmax_kernel<<<grid_for(op->n < 262144 ? op->n : 262144, 256), 256, 0, st>>>(
+                op->xs, op->colv, d_x, op->n, w.xmax);
+        }
         BSLS_LAUNCH_CHECK();
         const double *xin = op->colv ? op->xs : d_x;
         const int grid = (int)(K.nrb * K.ngroups);
@@ -380,16 +390,17 @@ extern "C" int bsls_lsq_residual(const bsls_lsq_op *op, const double *d_x, const
         if (op->colv) {
             lsq_allow_lds(lsq_k1t_fx<0>);
             lsq_k1t_fx<0><<<grid, BSLS_TILE_THREADS, lds, st>>>(K, op->m, xin, op->rpart, w.xmax,
-                                                               op->fx_amax);
+                                                               op->fx_amax, xb);
         } else {
             lsq_allow_lds(lsq_k1t_fx<1>);
             lsq_k1t_fx<1><<<grid, BSLS_TILE_THREADS, lds, st>>>(K, op->m, xin, op->rpart, w.xmax,
-                                                               op->fx_amax);
+                                                               op->fx_amax, xb);
         }
         BSLS_LAUNCH_CHECK();
         const int gk = grid_for(op->m, 256);
         lsq_t_sum<<<gk < LSQ_SUM_GRID ? gk : LSQ_SUM_GRID, 256, 0, st>>>(
-            op->m, K.ngroups, op->rpart, d_add, d_r, d_sq_out, w.part, w.tk, w.xmax);
+            op->m, K.ngroups, op->rpart, d_add, d_r, d_sq_out, w.part, w.tk,
+            xb > 0.0 ? nullptr : w.xmax);
         BSLS_LAUNCH_CHECK();
         return BSLS_OK;
     }

@@ -624,6 +624,8 @@ class DeviceLSQ:
         self.k2 = k2
         dev = dict(dtype=torch.float64, device='cuda')
         self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
+        # max |colv| (1 unscaled): with |x| <= 1, the bound on the gathered colv * x
+        self.colv_max = float(np.max(np.abs(colv))) if (self.scaled and colv.size) else 1.0
         self.xs = torch.empty(self.n, **dev) if self.scaled else None
         self.rpart = torch.zeros(groups * self.m, **dev)
         self.work = torch.zeros(L.bsls_lsq_workspace_size(self.m, npanels),
@@ -966,6 +968,8 @@ class BBEngine:
             # + one slot per (group, row block): stage 8's r^2 slices
             self.wpart = torch.zeros(ti['ngroups'] * ti['nrb'] * (ti['H'] + 2), **dev)
         self.colv = torch.from_numpy(colv).cuda() if self.scaled else None
+        # max |colv| (1 unscaled): with |x| <= 1, the bound on the gathered colv * x
+        self.colv_max = float(np.max(np.abs(colv))) if (self.scaled and colv.size) else 1.0
         # the scales as the kernels read them every iteration: the narrowest
         # exact type (flows are integers: _Float16; value_codec)
         self.colv_codec, self.colv_n = 0, None
@@ -1290,6 +1294,7 @@ class XBBEngine:
         P.work, P.work_bytes = self.work.data_ptr(), self.work.numel()
         lsq = getattr(obj, 'lsq', None)
         P.lsq = ctypes.pointer(lsq.op) if lsq is not None else None
+        self._lsq, self._xb = lsq, 0.0
         self.lbfgs = int(lbfgs)
         if self.lbfgs < 0:
             raise ValueError('corrections must be >= 0')
@@ -1309,6 +1314,16 @@ class XBBEngine:
         if x0.numel() != self.n:
             raise ValueError('x_init has %d entries, expected %d' % (x0.numel(), self.n))
         self.x.copy_(x0)
+        # every iterate the rounds evaluate is x_init, a projection onto the
+        # simplex / l1 ball (entries within [-1, 1]) or a convex combination of
+        # those: its entries stay within max(1, max|x_init|), which lets a
+        # fixed-point residual skip its per-call max pass (bsls_lsq_op.x_bound)
+        self._xb = 0.0
+        lsq = self._lsq
+        if lsq is not None and lsq.op.fixed:
+            xm = float(x0.abs().max()) if x0.numel() else 0.0
+            if np.isfinite(xm):
+                self._xb = max(1.0, xm) * lsq.colv_max
         cap = int(hist_cap if hist_cap is not None else min(max(int(max_iter), 1) + 1, 1 << 22))
         if self.hist is None or self.hist.numel() < cap:
             self.hist = torch.zeros(cap, dtype=torch.float64, device='cuda')
@@ -1322,8 +1337,15 @@ class XBBEngine:
         check(_native.lib().bsls_xbb_init(P, stream_handle()), 'bsls_xbb_init')
 
     def rounds(self, count):
-        check(_native.lib().bsls_xbb_rounds(self.P, int(count), stream_handle()),
-              'bsls_xbb_rounds')
+        lsq = self._lsq
+        if lsq is not None and self._xb > 0.0:
+            lsq.op.x_bound = self._xb          # read by the launches enqueued below only
+        try:
+            check(_native.lib().bsls_xbb_rounds(self.P, int(count), stream_handle()),
+                  'bsls_xbb_rounds')
+        finally:
+            if lsq is not None:
+                lsq.op.x_bound = 0.0
 
     def scalars(self):
         return self.scal.cpu().numpy()

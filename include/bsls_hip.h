@@ -570,6 +570,11 @@ typedef struct bsls_lsq_op {
      * to 2^-50 of that bound. */
     int64_t fixed;
     double fx_amax;
+    /* fixed only: > 0 is the caller's guarantee that max|x| (of colv * x with a
+     * scaled incidence) <= x_bound for this call, so the per-call max pass is
+     * skipped (an x-space solver's projected iterates: |x| <= 1 per entry);
+     * 0 = the max is measured per call.  A violated bound corrupts r. */
+    double x_bound;
 } bsls_lsq_op;
 
 size_t bsls_lsq_workspace_size(int64_t m, int64_t A_npanels);
