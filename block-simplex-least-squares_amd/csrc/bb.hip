@@ -50,7 +50,9 @@ struct BBWork {
     double *p1, *p2, *pf;
     int32_t *wsc;
     double *dz;   // z - z_prev, written by K3 (and the prologue) for the next K2
-    uint64_t *hd; // K3's warm start: each pack's last run-head mask (<= n - nz packs)
+    uint64_t *hd; // K3's warm start: each pack's last run-head mask (<= n - nz packs),
+                  //   two sets (slot 1: DORE's second projection, the line search's trials)
+    int64_t hd_stride;
     size_t bytes;
 };
 
@@ -80,7 +82,8 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     w.dz = (double *)(p + off);
     off += al16((size_t)(nz > 0 ? nz : 1) * 8);
     w.hd = (uint64_t *)(p + off);
-    off += al16((size_t)(n - nz > 0 ? n - nz : 1) * 8);
+    w.hd_stride = n - nz > 0 ? n - nz : 1;
+    off += al16((size_t)w.hd_stride * 2 * 8);
     w.bytes = off;
     return w;
 }
@@ -1173,8 +1176,11 @@ static bool k3_merge(const bsls_bb_problem &P) {
 
 template <int CV>
 static void launch_k3_cv(const bsls_bb_problem &P, int64_t iter, const double *zc,
-                         const double *g, double *zn, const BBWork &w, hipStream_t st, int rec) {
-    uint64_t *hd = P.pava_warm ? w.hd : nullptr;   // (bsls_bb_problem.pava_warm)
+                         const double *g, double *zn, const BBWork &w, hipStream_t st, int rec,
+                         int slot) {
+    // (bsls_bb_problem.pava_warm; a second set of masks for a second
+    // projection whose inputs alternate with the first's)
+    uint64_t *hd = P.pava_warm ? w.hd + (slot ? w.hd_stride : 0) : nullptr;
     if (k3_merge(P))
         bb_k3<2, true, CV><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc,
                                                                    rec, hd);
@@ -1184,10 +1190,10 @@ static void launch_k3_cv(const bsls_bb_problem &P, int64_t iter, const double *z
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
-                      double *zn, const BBWork &w, hipStream_t st, int rec = 0) {
-    if (P.colv && P.colv_codec == 2) launch_k3_cv<2>(P, iter, zc, g, zn, w, st, rec);
-    else if (P.colv && P.colv_codec == 1) launch_k3_cv<1>(P, iter, zc, g, zn, w, st, rec);
-    else launch_k3_cv<0>(P, iter, zc, g, zn, w, st, rec);
+                      double *zn, const BBWork &w, hipStream_t st, int rec = 0, int slot = 0) {
+    if (P.colv && P.colv_codec == 2) launch_k3_cv<2>(P, iter, zc, g, zn, w, st, rec, slot);
+    else if (P.colv && P.colv_codec == 1) launch_k3_cv<1>(P, iter, zc, g, zn, w, st, rec, slot);
+    else launch_k3_cv<0>(P, iter, zc, g, zn, w, st, rec, slot);
     if (P.long_packs && P.nlong > 0)
         bb_k3_long<<<(int)P.nlong, LONG_T, 0, st>>>(P, iter, zc, g, zn, w.dz);
 }
@@ -1560,7 +1566,7 @@ extern "C" int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state
         dore_mid<<<gm, 256, 0, st>>>(PS, D, i, axo, axp);
         dore_ext<<<gb, 256, 0, st>>>(PS, D, axo, axp, axpp, x, xp, xn);
         // x_2 = proj(x_1 + a2 (x_1 - x_prev)), Ax_2 = linop(x_2), selection (DORE.py:55-69)
-        launch_k3(P2, i, d->X1, d->D, d->X2, w, st);
+        launch_k3(P2, i, d->X1, d->D, d->X2, w, st, 0, 1);
         launch_k1<false, false, true>(P2, i, w, st);
         dore_sel<<<gm, 256, 0, st>>>(P2, D);
         dore_copy<<<gb, 256, 0, st>>>(P2, D, xn, axo);
@@ -1606,7 +1612,7 @@ extern "C" int bsls_lbfgs_ls_trials(const bsls_bb_problem *p, const bsls_ls_stat
     P1.max_iter = P2.max_iter = INT64_MAX;
     P1.early_exit = P2.early_exit = 0;
     for (int64_t k = 0; k < count; ++k) {
-        launch_k3(P1, 1, s->x, s->d, s->pt, w, st);
+        launch_k3(P1, 1, s->x, s->d, s->pt, w, st, 0, 1);
         BSLS_LAUNCH_CHECK();
         launch_k1<true, true, true>(P1, 1, w, st);
         BSLS_LAUNCH_CHECK();
