@@ -847,6 +847,10 @@ def main():
     ap.add_argument('--rehearse-shard', type=int, default=0,
                     help='one GPU, one process: time rank 0 of an N-way C5 partition through '
                          'the sharded (RCCL) driver -- per-rank cost without the fabric')
+    ap.add_argument('--rehearse-workload', default='C5', choices=['C3', 'C5'],
+                    help='the rehearsed partition: C5 (rank 0 of N), or C3 (rank 0\'s C3-sized '
+                         'shard of the weak-scaled N-GPU headline; the rank count does not '
+                         'change its shard)')
     args = ap.parse_args()
     legs = set(LEGS) if args.legs == 'all' else set(args.legs.split(','))
     if legs - set(LEGS):
@@ -863,7 +867,7 @@ def main():
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
     if args.rehearse_shard:
-        legs, args.workload = {'main'}, 'C5'
+        legs, args.workload = {'main'}, args.rehearse_workload
     elif world > 1:
         legs &= {'main', 'c5'}
     # (modulo: the gloo rehearsal puts several ranks on one GPU)
