@@ -377,6 +377,17 @@ __device__ __forceinline__ void lane_block_lds(double *buf, int off, int k, int 
             }
         }
     }
+    if constexpr (THR) {
+        // nothing was sorted: v[j] (clamped for the ball, as the output wants)
+        // is still entry j, so no second read of the block
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+            const double t = v[j];
+            const double r = need ? relu_ref(lam + t) : t;
+            buf[(j < k) ? off + j : PCAP + WAVE + 2 + lane] = r;
+        }
+        return;
+    }
     asm volatile("" ::: "memory");   // keep the o[] loads after the sort (VGPRs)
     double o[KB];
 #pragma unroll
