@@ -751,7 +751,7 @@ class LineSearch:
     ||d||); after the accepted exit take() gives x_next, nabla_f(x_next) and
     f(x_next)."""
 
-    CHUNK = 4
+    CHUNK = int(os.environ.get('BSLS_LS_CHUNK', '4'))   # trials per state read
 
     def __init__(self, eng, c1=1e-3, c2=0.9):
         torch = _torch()
