@@ -449,7 +449,8 @@ typedef struct {
     const double *x, *d, *gx;   /* nz each: point (projected), direction, nabla_f(x) */
     double *pt, *gpt;           /* nz each: the trial point and its gradient */
     const double *zero;         /* nz zeros */
-    const double *fx;           /* f(x), one device double */
+    const double *fx;           /* f(x), one device double (may be the last search's
+                                   st[BSLS_LS_FT]: begin reads it before resetting st) */
     double *st;                 /* BSLS_LS_COUNT doubles */
     double *S1, *S2;            /* BSLS_S_COUNT doubles each */
     double *part;               /* bsls_lbfgs_ls_work_size(nz) bytes */
