@@ -1080,7 +1080,10 @@ static void launch_k1t_mode(const bsls_bb_problem &P, int64_t iter, const BBWork
     if (P.At.ngroups > 1 && k1_atomic(P, REDUCE)) {
         const int64_t r0 = rb0 * P.At.H, r1 = (rb1 * P.At.H < P.m) ? rb1 * P.At.H : P.m;
         const int gi = grid_for(r1 - r0, 256);
-        bb_k1_init<ITER, ADD><<<gi < 1024 ? gi : 1024, 256, 0, st>>>(P, r0, r1);
+        // one row per thread (the grid-stride form at 1024 workgroups gave each
+        // thread 4 rows at m = 1M; the rehearsed iteration measured the same
+        // either way, 149.3-149.8 us)
+        bb_k1_init<ITER, ADD><<<gi < 16384 ? gi : 16384, 256, 0, st>>>(P, r0, r1);
         allow_lds(bb_k1t<MODE, ITER, ADD, false, true>);
         bb_k1t<MODE, ITER, ADD, false, true><<<(int)((rb1 - rb0) * P.At.ngroups),
                                                BSLS_TILE_THREADS, tile_lds_doubles(P.At, false) * 8,
