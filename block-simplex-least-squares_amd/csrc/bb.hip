@@ -818,9 +818,23 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
                                              double *__restrict__ zn,
                                              double *__restrict__ dzo,
                                              int32_t *__restrict__ wsc, int rec,
-                                             uint64_t *__restrict__ hd) {
+                                             uint64_t *__restrict__ hd, int kinit) {
     const double sc[4] = {P.scal[BSLS_S_STOP], P.scal[BSLS_S_SUMDG], P.scal[BSLS_S_DZDG],
                           P.scal[BSLS_S_DGDG]};
+    // kinit (stage 15): the next K1's r initialisation folded in (its atomic
+    // group sums add into r): r = target on the shard_role 1 rank, 0 on the
+    // others; once stopped, role 1 keeps its r and the others write 0 -- as
+    // bb_k1_init, one launch fewer
+    auto init_r = [&](bool stopped) {
+        const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+        const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (stopped) {
+            k1_stopped_rows(P, 0, P.m, t0, gs);
+            return;
+        }
+        const bool add = P.shard_role == 1;
+        for (int64_t row = t0; row < P.m; row += gs) P.r[row] = add ? P.target[row] : 0.0;
+    };
     // rec (stage 13, the sliced sharded schedule): stage 12 folded in -- f and
     // the stopping test of iter - 1 from the all-reduced scal[RR] and the kept
     // scal[PGG] / scal[PDGDG], decided alike by every workgroup (the same
@@ -842,7 +856,10 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
                 for (int q = 0; q < 4; ++q) s[BSLS_S_SUMDG + q] = s[BSLS_S_PSUMDG + q];
             }
         }
-        if (reason) return;
+        if (reason) {
+            if (kinit) init_r(true);
+            return;
+        }
     }
     const int l = lane_id();
     const int wv = threadIdx.x / WAVE;
@@ -882,7 +899,9 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
         gv[q] = act ? g[z0[q] + l] : 0.0;
     }
     double t;
-    if (!bb_step_t(P, iter, sc, t)) return;
+    const bool go = bb_step_t(P, iter, sc, t);
+    if (kinit) init_r(!go);
+    if (!go) return;
     double yv[K3_PPW];
 #pragma unroll
     for (int q = 0; q < K3_PPW; ++q)   // x_next = x - t g (BB.py:29)
@@ -1074,16 +1093,23 @@ static bool k1_atomic(const bsls_bb_problem &P, bool reduce) {
     return P.shard_role != 0 && !reduce;
 }
 
+// stage 15 / 14: the atomic K1's r initialisation done by the K3 before it
+// (bb_k3 kinit) -- whole matrix only
+static bool k1_init_folded(const bsls_bb_problem &P) {
+    return P.At.ent && P.At.ngroups > 1 && k1_atomic(P, false);
+}
+
 template <int MODE, bool ADD, bool REDUCE, bool ITER>
 static void launch_k1t_mode(const bsls_bb_problem &P, int64_t iter, const BBWork &w,
-                            hipStream_t st, int64_t rb0, int64_t rb1) {
+                            hipStream_t st, int64_t rb0, int64_t rb1, bool skip_init) {
     if (P.At.ngroups > 1 && k1_atomic(P, REDUCE)) {
         const int64_t r0 = rb0 * P.At.H, r1 = (rb1 * P.At.H < P.m) ? rb1 * P.At.H : P.m;
         const int gi = grid_for(r1 - r0, 256);
         // one row per thread (the grid-stride form at 1024 workgroups gave each
         // thread 4 rows at m = 1M; the rehearsed iteration measured the same
         // either way, 149.3-149.8 us)
-        bb_k1_init<ITER, ADD><<<gi < 16384 ? gi : 16384, 256, 0, st>>>(P, r0, r1);
+        if (!skip_init)
+            bb_k1_init<ITER, ADD><<<gi < 16384 ? gi : 16384, 256, 0, st>>>(P, r0, r1);
         allow_lds(bb_k1t<MODE, ITER, ADD, false, true>);
         bb_k1t<MODE, ITER, ADD, false, true><<<(int)((rb1 - rb0) * P.At.ngroups),
                                                BSLS_TILE_THREADS, tile_lds_doubles(P.At, false) * 8,
@@ -1108,11 +1134,11 @@ static void launch_k1t_mode(const bsls_bb_problem &P, int64_t iter, const BBWork
 
 template <bool ADD, bool REDUCE, bool ITER>
 static void launch_k1(const bsls_bb_problem &P, int64_t iter, const BBWork &w, hipStream_t st,
-                      int64_t rb0 = 0, int64_t rb1 = -1) {
+                      int64_t rb0 = 0, int64_t rb1 = -1, bool skip_init = false) {
     if (rb1 < 0) rb1 = k1_row_blocks(P);
     if (P.At.ent) {
-        if (P.colv) launch_k1t_mode<0, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1);
-        else launch_k1t_mode<1, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1);
+        if (P.colv) launch_k1t_mode<0, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1, skip_init);
+        else launch_k1t_mode<1, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1, skip_init);
     } else if (P.colv) {
         launch_k1_mode<0, ADD, REDUCE, ITER>(P, iter, w, st, rb0, rb1);
     } else {
@@ -1180,23 +1206,25 @@ static bool k3_merge(const bsls_bb_problem &P) {
 template <int CV>
 static void launch_k3_cv(const bsls_bb_problem &P, int64_t iter, const double *zc,
                          const double *g, double *zn, const BBWork &w, hipStream_t st, int rec,
-                         int slot) {
+                         int slot, int kinit) {
     // (bsls_bb_problem.pava_warm; a second set of masks for a second
     // projection whose inputs alternate with the first's)
     uint64_t *hd = P.pava_warm ? w.hd + (slot ? w.hd_stride : 0) : nullptr;
     if (k3_merge(P))
         bb_k3<2, true, CV><<<grid_for(P.npacks, 8), 256, 0, st>>>(P, iter, zc, g, zn, w.dz, w.wsc,
-                                                                   rec, hd);
+                                                                   rec, hd, kinit);
     else
         bb_k3<1, false, CV><<<grid_for(P.npacks, 4), 256, 0, st>>>(P, iter, zc, g, zn, w.dz,
-                                                                    w.wsc, rec, hd);
+                                                                    w.wsc, rec, hd, kinit);
 }
 
 static void launch_k3(const bsls_bb_problem &P, int64_t iter, const double *zc, const double *g,
-                      double *zn, const BBWork &w, hipStream_t st, int rec = 0, int slot = 0) {
-    if (P.colv && P.colv_codec == 2) launch_k3_cv<2>(P, iter, zc, g, zn, w, st, rec, slot);
-    else if (P.colv && P.colv_codec == 1) launch_k3_cv<1>(P, iter, zc, g, zn, w, st, rec, slot);
-    else launch_k3_cv<0>(P, iter, zc, g, zn, w, st, rec, slot);
+                      double *zn, const BBWork &w, hipStream_t st, int rec = 0, int slot = 0,
+                      int kinit = 0) {
+    if (P.colv && P.colv_codec == 2) launch_k3_cv<2>(P, iter, zc, g, zn, w, st, rec, slot, kinit);
+    else if (P.colv && P.colv_codec == 1)
+        launch_k3_cv<1>(P, iter, zc, g, zn, w, st, rec, slot, kinit);
+    else launch_k3_cv<0>(P, iter, zc, g, zn, w, st, rec, slot, kinit);
     if (P.long_packs && P.nlong > 0)
         bb_k3_long<<<(int)P.nlong, LONG_T, 0, st>>>(P, iter, zc, g, zn, w.dz);
 }
@@ -1693,6 +1721,16 @@ extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, 
         case 13:  // stage 12 folded into stage 4's K3 (one launch fewer)
             if (iter <= 0) return BSLS_E_ARG;
             launch_k3(P, iter, P.z[zc], P.g[zn], P.z[zn], w, st, 1);
+            break;
+        case 15:  // stage 13 with the next stage 14's r initialisation folded in
+            if (iter <= 0) return BSLS_E_ARG;
+            launch_k3(P, iter, P.z[zc], P.g[zn], P.z[zn], w, st, 1, 0,
+                      k1_init_folded(P) ? 1 : 0);
+            break;
+        case 14:  // stage 1 after stage 15 (r already initialised when it folds)
+            if (iter <= 0) return BSLS_E_ARG;
+            if (P.shard_role == 1) launch_k1<true, false, true>(P, iter, w, st, 0, -1, k1_init_folded(P));
+            else launch_k1<false, false, true>(P, iter, w, st, 0, -1, k1_init_folded(P));
             break;
         case 12:  // f / stopping test of iteration iter - 1 (after the sums' all-reduce)
             if (iter <= 0) return BSLS_E_ARG;

@@ -5,9 +5,10 @@
 //     stage 10  K2 (g_g, the four local BB sums) + this rank's 1/world slice
 //               of ||r||^2 (r is the same all-reduced vector on every rank)
 //     RCCL      all-reduce(sum) of scal[SUMDG..RR]        40 B
-//     stage 13  K3: f and the stopping test of i - 1 (every workgroup alike),
-//               then t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = colv N_g z_g
-//     stage 1   K1: r_g = A_g x_g (+ target on the shard_role 1 rank)
+//     stage 15  K3: f and the stopping test of i - 1 (every workgroup alike),
+//               then t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = colv N_g z_g, and
+//               (atomic K1) r set to target / 0 for the next stage
+//     stage 14  K1: r_g = A_g x_g (+ target on the shard_role 1 rank)
 //     RCCL      all-reduce(sum) of r                      8 m B
 // and stage 9 (f / stop test) after the last iteration of a call; fuse 1
 // reads all of r for ||r||^2 in K2 (stage 8: the f of i - 1 in its last
@@ -132,9 +133,11 @@ extern "C" int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *c, int
             // then f and the stop test of i - 1
             // (stage 13: K3 with stage 12 -- f and the stop test of i - 1 --
             // folded in)
+            // (stage 15: 13 with the next K1's r initialisation folded in when
+            // K1 adds its group sums by atomics; stage 14 is then stage 1 without it)
             if ((rc = bsls_bb_stage(p, 10, i, stream)) != BSLS_OK) return rc;
             if ((rc = all_reduce(p->scal + BSLS_S_SUMDG, 5)) != BSLS_OK) return rc;
-            if ((rc = bsls_bb_stage(p, 13, i, stream)) != BSLS_OK) return rc;
+            if ((rc = bsls_bb_stage(p, 15, i, stream)) != BSLS_OK) return rc;
         } else {
             // K2 (+ the fused f / stop test of i - 1), then the BB sums over ranks
             if ((rc = bsls_bb_stage(p, fuse ? 8 : 3, i, stream)) != BSLS_OK) return rc;
@@ -142,7 +145,7 @@ extern "C" int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *c, int
             if ((rc = bsls_bb_stage(p, 4, i, stream)) != BSLS_OK) return rc;
         }
         // the partial residual, then r = the sum over ranks (the one real exchange)
-        if ((rc = bsls_bb_stage(p, 1, i, stream)) != BSLS_OK) return rc;
+        if ((rc = bsls_bb_stage(p, fuse == 2 ? 14 : 1, i, stream)) != BSLS_OK) return rc;
         if ((rc = all_reduce(p->r, (size_t)p->m)) != BSLS_OK) return rc;
         if (!fuse && (rc = bsls_bb_stage(p, 9, i, stream)) != BSLS_OK) return rc;
     }

@@ -407,11 +407,16 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  *      all-reduce, before stage 4)
  *  13  stage 12 folded into stage 4 (K3's workgroups all decide the stop of
  *      iter - 1 from the same scal values, workgroup 0 records it)
+ *  15  stage 13 that also sets r to target (shard_role 1) / 0 for stage 14
+ *      when K1 adds its column groups' sums by atomics (a column shard's
+ *      dealt K1 with several groups); otherwise stage 13
+ *  14  stage 1 after stage 15 (without its own r initialisation then)
  * One iteration i >= 1 = 3, [allreduce sums], 4, 1, [allreduce r], 2; on one GCD
  * bsls_bb_iterate runs 3, 4, 7.  The column-sharded driver (distributed.py,
  * shard_role 1 / 2) runs 8, [allreduce sums], 4, 1, [allreduce r] per
  * iteration and 9 after the last one (fuse 1), or the sliced form 10,
- * [allreduce 5 sums], 13, 1, [allreduce r] (fuse 2, the default). */
+ * [allreduce 5 sums], 13, 1, [allreduce r] (fuse 2, the default; the native
+ * driver bsls_bb_shard_iterate runs 15 and 14 in place of 13 and 1). */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 /* Stage 1 restricted to K1's row blocks [rb0, rb1) (rows rb0 * R .. rb1 * R - 1,
  * R = *rows_per_block from bsls_bb_row_blocks, which returns the block count):
