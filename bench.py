@@ -153,7 +153,7 @@ def bench_stored_values(sh, b, steps, warmup, codec=None):
             os.environ['BSLS_VAL_CODEC'] = old
     eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
     eng.prologue()
-    el = time_run(eng.iterate, steps, warmup, None)
+    el = float(np.median(time_run(eng.iterate, steps, warmup, None, windows=5)))
     m, n, nz, p, nnz = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
     ib = survey_iter_bytes(m, n, nz, nnz)
     its = steps / el
@@ -668,26 +668,34 @@ def build_engine(sh, b, world, dist, parts, sharded=False, slices=None):
     return eng, drv.iterate
 
 
-def time_run(run, steps, warmup, dist):
-    """W untimed iterations, then exactly K between barrier + synchronize on
-    both sides; max over ranks."""
+def time_run(run, steps, warmup, dist, windows=1):
+    """W untimed iterations, then `windows` windows of exactly K iterations,
+    each between barrier + synchronize on both sides, max over ranks per
+    window.  Returns the per-window seconds (the headline takes the median:
+    a 20-step window of C3 is ~1.7 ms of device time, so one window alone is
+    at the mercy of a single clock or launch hiccup)."""
     import torch
     run(1, warmup)
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(1 + warmup, steps)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    return el
+    els = []
+    first = 1 + warmup
+    for _ in range(max(1, windows)):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(first, steps)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64, device='cuda')
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        els.append(el)
+        first += steps
+    return els
 
 
 def kernel_table(eng, it0, reps, world, m, n, nz, p, nnz):
@@ -844,6 +852,9 @@ def main():
                     help='comma list of %s (N = 1; default all): one rocprofv3 run per leg '
                          'keeps each workload\'s kernel rows apart' % ','.join(LEGS))
     ap.add_argument('--profile-iters', type=int, default=20)
+    ap.add_argument('--windows', type=int, default=10,
+                    help='timed windows of --steps iterations each; the line reports the '
+                         'median window and the spread')
     ap.add_argument('--rehearse-shard', type=int, default=0,
                     help='one GPU, one process: time rank 0 of an N-way C5 partition through '
                          'the sharded (RCCL) driver -- per-rank cost without the fabric')
@@ -929,7 +940,8 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
         eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(shard_of),
                                 slices=shard_of)
     log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
-    el = time_run(run, steps, args.warmup, dist)
+    els = time_run(run, steps, args.warmup, dist, windows=args.windows)
+    el = float(np.median(els))
     it_s = steps / el
     sc = eng.scalars()
     finite = bool(np.isfinite(sc[4]))
@@ -938,7 +950,7 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
     m, n_g, nz_g, p_g, nnz_g = eng.m, eng.n, eng.nz, eng.layout.p, sh['A'].nnz
     kern = {}
     if args.profile_iters > 0 and rank == 0:
-        kern = kernel_table(eng, 1 + args.warmup + steps, args.profile_iters,
+        kern = kernel_table(eng, 1 + args.warmup + steps * len(els), args.profile_iters,
                             world if not shard_of else 2, m, n_g, nz_g, p_g, nnz_g)
         log('kernel table done')
     if dist:
@@ -947,7 +959,10 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
     if rank == 0:
         n_tot, p_tot = sh['n_total'], sh['p_total']
         nnz_tot = 16 * n_tot
-        key = ('%s_x%d' % (wl, shard_of)) if shard_of else wl
+        # the PMC traffic and kernel-trace key: the one-GPU workload, or the
+        # shard ('C5_x8': rank 0 of 8); a shard nobody profiled gets traffic
+        # null rather than the one-GPU kernels' bytes
+        key = ('%s_x%d' % (wl, shard_of or world)) if (shard_of or world > 1) else wl
         weak = wl == 'C3'
         # weak: the job is world C3-sized shards; its unit is the 1M-route
         # iteration, so the rate is world x iterations/s of the whole problem
@@ -961,6 +976,14 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
                      % (wl, n_tot, p_tot, m)),
             'iterations_per_s': it_s, 'steps': steps,
             'ms_per_step': el / steps * 1e3,
+            'windows': {'count': len(els), 'steps_each': steps,
+                        'ms_per_step': {'median': el / steps * 1e3,
+                                        'min': min(els) / steps * 1e3,
+                                        'max': max(els) / steps * 1e3},
+                        'iterations_per_s': {'median': it_s, 'min': steps / max(els),
+                                             'max': steps / min(els)},
+                        'note': 'value = the median window; every window K iterations '
+                                'between barrier + synchronize, max over ranks'},
             'scaling': 'weak' if weak else 'strong',
             'config': {'workload': ('C3 (BASELINE configs[2]): BB (z-space, PAVA projection) on '
                                     '%d x (1M routes / 50k blocks / 16M nnz), %d links, one '

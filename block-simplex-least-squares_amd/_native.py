@@ -31,6 +31,9 @@ STOP_TEXT = {STOP_NOCHANGE: 'Exiting... no change in gradient',
              STOP_DG: 'Exiting... no change in gradient'}
 
 _vp = ctypes.c_void_p
+# bsls_all_reduce_fn (include/bsls_hip.h): (d_buf, count, stream, user) -> 0 / error
+ALL_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                 ctypes.c_void_p)
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int32
 _dbl = ctypes.c_double
@@ -80,7 +83,7 @@ class BBProblem(ctypes.Structure):
                 ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz),
                 ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp),
                 ('colv_n', _vp), ('colv_codec', _i64), ('rr_lo', _i64), ('rr_hi', _i64),
-                ('pava_warm', _i64)]
+                ('pava_warm', _i64), ('k1_atomic', _i64), ('k3_merge', _i64)]
 
 
 class DoreState(ctypes.Structure):
@@ -194,6 +197,7 @@ _SIGS = {
     'bsls_comm_id_bytes': (_sz, []),
     'bsls_comm_unique_id': (_int, [_vp]),
     'bsls_comm_create': (_int, [_vp, _int, _int, ctypes.POINTER(_vp)]),
+    'bsls_comm_create_callback': (_int, [_int, _int, _vp, _vp, ctypes.POINTER(_vp)]),
     'bsls_comm_destroy': (_int, [_vp]),
     'bsls_comm_all_reduce': (_int, [_vp, _vp, _i64, _vp]),
     'bsls_bb_shard_iterate': (_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp]),

@@ -408,6 +408,17 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
 // rest), stored with the sums as scal[RR] for the all-reduce; the last
 // workgroup keeps iteration iter - 1's sums in scal[PSUMDG..PGG] for the
 // stop test that follows the all-reduce (stage 12), instead of testing.
+// K2 of a stopped sharded run: the driver still all-reduces scal[SUMDG..RR]
+// after every K2 it enqueues, so the shard_role 2 ranks zero their copy and
+// the sum leaves role 1's -- the stop iteration's sums -- instead of world
+// times them, growing with every iteration enqueued past the stop
+// (fuse 2 all-reduces scal[RR] with the four sums)
+template <int FUSE>
+__device__ __forceinline__ void k2_stopped_sums(const bsls_bb_problem &P) {
+    if (P.shard_role == 2 && blockIdx.x == 0 && threadIdx.x == 0)
+        for (int q = 0; q < (FUSE == 2 ? 5 : 4); ++q) P.scal[BSLS_S_SUMDG + q] = 0.0;
+}
+
 template <int MODE, bool ITER, int FUSE = 0, int CV = 0>
 __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
                                                const double *__restrict__ gp,
@@ -416,7 +427,10 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ double red[5 * 16];
     __shared__ int row_last;
-    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
+        k2_stopped_sums<FUSE>(P);
+        return;
+    }
     const bsls_tiles &T = P.ATt;
     int64_t rb, g;
     tile_map(T, blockIdx.x, T.nrb, rb, g);
@@ -575,7 +589,12 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
             // stopped at iter - 1: keep that iteration's sums (what the
             // unfused schedule leaves in scal); g[iter & 1], written above,
             // is the other buffer -- the stopping iterate's g is untouched
-            if (P.scal[BSLS_S_STOP] != 0.0) return;
+            if (P.scal[BSLS_S_STOP] != 0.0) {
+                // (the sums all-reduced after this launch: as k2_stopped_sums)
+                if (P.shard_role == 2)
+                    for (int q = 0; q < 4; ++q) P.scal[BSLS_S_SUMDG + q] = 0.0;
+                return;
+            }
         }
         if constexpr (FUSE == 2) {
             double *sc = P.scal;
@@ -652,7 +671,10 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
                                               double *__restrict__ gout, double *part,
                                               unsigned *ticket, int64_t iter) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    if (ITER && P.scal[BSLS_S_STOP] != 0.0) return;
+    if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
+        k2_stopped_sums<FUSE>(P);
+        return;
+    }
     const bsls_panels &M = P.AT;
     const int wv = threadIdx.x / WAVE, lane = lane_id();
     const int64_t panel = (int64_t)blockIdx.x * PANEL_WAVES + wv;
@@ -735,7 +757,12 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
     if (last_block_sum<NS>(sums, part, ticket, tot, lds) && threadIdx.x == 0) {
         if constexpr (FUSE == 1) {
             bb_record_f(P, iter - 1, tot[4], iter - 1 > 0);
-            if (P.scal[BSLS_S_STOP] != 0.0) return;   // as bb_k2t
+            if (P.scal[BSLS_S_STOP] != 0.0) {
+                // (the sums all-reduced after this launch: as k2_stopped_sums)
+                if (P.shard_role == 2)
+                    for (int q = 0; q < 4; ++q) P.scal[BSLS_S_SUMDG + q] = 0.0;
+                return;
+            }   // as bb_k2t
         }
         if constexpr (FUSE == 2) {
             double *sc = P.scal;
@@ -1085,11 +1112,11 @@ static void launch_k1_mode(const bsls_bb_problem &P, int64_t iter, const BBWork 
 // K2.  On one GPU it measured no faster (C3 83.0 / 85.7 us, C5 800 / 801: the
 // ||r||^2 pass reads r again), and the atomics' varying order moves the exact
 // zero sum(dg) exit of BB.py:22 (a tests/fast problem stopped at 967 instead
-// of ~770), so one GPU keeps the group sums.  BSLS_K1_ATOMIC (environment,
-// read per launch): 0 = never, 1 = wherever K1 has several groups.
+// of ~770), so one GPU keeps the group sums.  bsls_bb_problem.k1_atomic
+// (the engine's BSLS_K1_ATOMIC, read once): 1 = never, 2 = wherever K1 has
+// several groups, 0 = the default above.
 static bool k1_atomic(const bsls_bb_problem &P, bool reduce) {
-    const char *e = getenv("BSLS_K1_ATOMIC");
-    if (e) return atoi(e) != 0;
+    if (P.k1_atomic) return P.k1_atomic == 2;
     return P.shard_role != 0 && !reduce;
 }
 
@@ -1196,11 +1223,10 @@ static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
 // (pava_v1_wave_pair) pay where the grid runs many rounds of resident waves:
 // C5 (172k packs) K3 153 -> 141 us; C3 (16.7k packs, two rounds of 8 waves
 // per SIMD) 18.8 -> 20.6 us, the longer wave outlasting its rounds.  So from
-// 64k packs (8 rounds); BSLS_K3_MERGE (environment, read per launch: tests
-// switch it) forces 0 / 1.
+// 64k packs (8 rounds); bsls_bb_problem.k3_merge (the engine's
+// BSLS_K3_MERGE, read once) forces one (1) or two (2).
 static bool k3_merge(const bsls_bb_problem &P) {
-    const char *e = getenv("BSLS_K3_MERGE");
-    return e ? atoi(e) != 0 : P.npacks >= 65536;
+    return P.k3_merge ? P.k3_merge == 2 : P.npacks >= 65536;
 }
 
 template <int CV>
@@ -1246,6 +1272,8 @@ static bool panels_ok(const bsls_panels &M, int64_t rows, int64_t cols, int64_t 
 static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
     if (p->shard_role < 0 || p->shard_role > 2) return BSLS_E_ARG;
+    if (p->k1_atomic < 0 || p->k1_atomic > 2 || p->k3_merge < 0 || p->k3_merge > 2)
+        return BSLS_E_ARG;
     if (p->colv_codec < 0 || p->colv_codec > 2 || (p->colv_codec && (!p->colv_n || !p->colv)))
         return BSLS_E_ARG;
     const bool general = p->colv == nullptr;

@@ -225,7 +225,9 @@ __global__ __launch_bounds__(1024) void lsq_k1t(bsls_tiles T, int64_t m,
 // lsq_xmax_kernel), the integer row sums are order-free, so r -- and f --
 // repeat bit for bit at the same x (the exits of the x-space solvers need
 // that), at the dealt walk's speed.  Two words (tiles.hpp fx_add): each term
-// rounds by at most 2^-101 (fx_amax max|x|), the sum converts back once.
+// rounds by at most 2^-(51 + fx_lo_shift(n)) of fx_amax max|x| (~2^-89 at 10M
+// columns), the sum converts back once; the low word cannot overflow, however
+// many entries a row holds.
 template <int MODE>
 __global__ __launch_bounds__(1024) void lsq_k1t_fx(bsls_tiles T, int64_t m,
                                                    const double *__restrict__ x,
@@ -245,12 +247,14 @@ __global__ __launch_bounds__(1024) void lsq_k1t_fx(bsls_tiles T, int64_t m,
     tile_walk_any<MODE, true>(T, rb, g, x, lds, nullptr, fxs);
     __syncthreads();
     const int lo_off = (int)(T.H + T.halo + 1);
+    const double inv_lo = ldexp(inv, -fx_lo_shift(T.cols));
     const int64_t r0 = rb * T.H, r1 = (r0 + T.H < m) ? r0 + T.H : m;
     // a NaN / inf in x (no finite scale): the rows are NaN, as a float sum
     // would make them (the solvers' NaN checks must still see it)
     const bool bad = !(B <= 1.7976931348623157e308);
     for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
-        rpart[g * m + row] = bad ? __builtin_nan("") : fx_value(lds, (int)(row - r0), lo_off, inv);
+        rpart[g * m + row] = bad ? __builtin_nan("") : fx_value(lds, (int)(row - r0), lo_off, inv,
+                                                                  inv_lo);
 }
 
 __global__ __launch_bounds__(256) void lsq_t_sum(int64_t m, int64_t G, const double *rpart,

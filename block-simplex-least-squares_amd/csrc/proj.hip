@@ -963,6 +963,196 @@ __global__ __launch_bounds__(256, BSLS_PROJ_MINW) void proj_thr_kernel(double *_
     }
 }
 
+// ---- the pipelined sort-free kernel (the default fast form, round 5) --------
+//
+// The lane-per-block kernels above load, compute and store in lockstep: C2's
+// 100k blocks make 1563 waves, ~1.5 per SIMD, each one long serial chain, so
+// nothing overlaps the memory phases (with the compute knocked out the exact
+// kernel still takes ~14 us to stream C2, a copy 8).  Here a block gets
+// PIPE_LPB = 8 lanes (entry j + 8 e of the block in slot e of its lane j,
+// PIPE_EB = 8 slots: blocks of <= 64; longer ones go to the big list as in
+// lds_group), a GROUP of 8 consecutive blocks is one wave's unit, and a
+// persistent wave walks groups w, w + W, w + 2 W, ... with the next group's
+// entries and the block starts of the group after it already in flight while
+// it runs Michelot's passes on the current group and stores it: every wave
+// keeps loads outstanding through its compute, so HBM stays busy.  A load
+// instruction reads 8 runs of 8 consecutive doubles (one per block), a store
+// writes them back from registers: no LDS, ~60 VGPRs.
+//
+// Per pass a lane tests its 8 slots against tau, and the block's sum and
+// count of {v > tau} come from three DPP steps inside the 8-lane group
+// (grp_sum_*: every lane of the group ends with the same bits).  tau starts
+// at max(M - 1, (S - 1) / k) -- the thresholds of the sets {max} and of the
+// whole block, both lower bounds of the projection's (thr_solve's comment) --
+// so U[0,1) blocks of ~32 take ~3-4 passes and 5 N(0,1) blocks 1-2.  The
+// entries stay unchanged in registers (tau only grows, so {v > tau} shrinks
+// by itself) and the output is relu(lambda + v) from them: lambda = (1 -
+// S) / c, the reference's expression at rho = c - 1 with its members summed
+// in another order (1e-12 contract, as thr_solve).
+constexpr int PIPE_LPB = 8, PIPE_EB = 8, PIPE_BPG = WAVE / PIPE_LPB;
+
+struct PipeGroup {
+    __amdgpu_buffer_rsrc_t rs;   // the group's range [s0, e1) of y (scalar registers)
+    int base;                    // this lane's byte offset of its slot 0
+    int k;                       // this lane's block length (0: none, or a big block)
+};
+
+// lanes 0 .. PIPE_BPG: the starts of group q's blocks and the end of its last
+// (n past the last block).  One unconditional load per lane at a clamped
+// index: a load under a branch would make the count of outstanding memory
+// operations path-dependent, and the compiler's waits then conservative.
+__device__ __forceinline__ long long pipe_meta(const int64_t *__restrict__ starts, int64_t nb,
+                                               int64_t n, int64_t q, int lane) {
+    const int64_t b = q * PIPE_BPG + lane;
+    const long long v = (long long)starts[b < nb ? b : nb - 1];
+    return (lane <= PIPE_BPG && b < nb) ? v : (long long)n;
+}
+
+// group q's blocks from its starts (BIG: blocks > SMALL_MAX go to the big
+// list, once -- `real` is false for the clamped copy a wave loads past its
+// last group)
+template <bool BIG>
+__device__ __forceinline__ PipeGroup pipe_setup(double *y, long long st, int64_t q, int64_t nb,
+                                                int64_t *__restrict__ big_list,
+                                                unsigned *__restrict__ big_count, bool real,
+                                                int lane) {
+    const int g = lane / PIPE_LPB, j = lane % PIPE_LPB;
+    const int64_t s = (int64_t)__shfl(st, g, WAVE);
+    const int64_t e = (int64_t)__shfl(st, g + 1, WAVE);
+    const int64_t b = q * PIPE_BPG + g;
+    const int64_t kk = e - s;
+    const bool big = kk > SMALL_MAX;
+    if constexpr (BIG) {
+        if (big && real && b < nb && j == 0) {   // (a block > max_block breaks the contract: left as is)
+            const unsigned slot = atomicAdd(big_count, 1u);
+            big_list[slot] = b;
+        }
+    }
+    // the range in scalar registers (a resource built from VGPRs becomes a
+    // waterfall loop around every access); the host keeps it < 2 GB
+    const int64_t s0 = uni64((int64_t)st, 0);
+    const int nbw = __builtin_amdgcn_readfirstlane(
+        (int)((nb - q * PIPE_BPG < PIPE_BPG) ? nb - q * PIPE_BPG : PIPE_BPG));
+    const int64_t e1 = uni64((int64_t)st, nbw);
+    PipeGroup G;
+    G.rs = __builtin_amdgcn_make_buffer_rsrc(y + s0, 0, (int)((e1 - s0) * 8), 0x00020000);
+    G.base = (int)(s - s0 + j) * 8;
+    G.k = (b < nb && !big) ? (int)kk : 0;
+    return G;
+}
+
+// (slots past the block read the next block's entries or, past the range, 0:
+// masked by pipe_solve)
+__device__ __forceinline__ void pipe_load(const PipeGroup &G, double (&v)[PIPE_EB]) {
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e) v[e] = buf_ld(G.rs, G.base + 8 * PIPE_LPB * e);
+}
+
+template <bool BALL>
+__device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_EB], int j) {
+    constexpr double PAD = -1.7976931348623157e308;   // below every entry, finite
+    const int k = G.k;
+    const int ne = (k > j) ? (k - j + PIPE_LPB - 1) / PIPE_LPB : 0;
+    double S = 0.0;
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e) {
+        const bool ok = e < ne;
+        if (BALL) v[e] = (ok & (v[e] < 0.0)) ? 0.0 : v[e];   // proj_simplex.h:56-64
+        S += ok ? v[e] : 0.0;
+        v[e] = ok ? v[e] : PAD;
+    }
+    S = grp_sum_d<PIPE_LPB>(S);
+    const bool need = !BALL || S > 1.0;
+    double lam = 0.0;
+    if (__builtin_amdgcn_ballot_w64(need && k > 0)) {
+        double M = v[0];
+#pragma unroll
+        for (int e = 1; e < PIPE_EB; ++e) M = (v[e] > M) ? v[e] : M;
+        M = grp_max_d<PIPE_LPB>(M);
+        // tau stays below the max (clamped to the next double down: only a
+        // |y| ~ 1e12+ rounding could reach it), so the max never leaves the set
+        const double Mdn = next_down(M);
+        const double kd = (double)k;
+        const double t_all = (S - 1.0) / kd, t_max = M - 1.0;
+        const bool from_all = t_all >= t_max;
+        double tau = fmin(from_all ? t_all : t_max, Mdn);
+        double cprev = from_all ? kd : 1.0;   // the set tau was taken from
+        double c = cprev;
+        for (int pass = 0; pass <= PIPE_LPB * PIPE_EB; ++pass) {
+            double sl = 0.0, cl = 0.0;
+#pragma unroll
+            for (int e = 0; e < PIPE_EB; ++e) {
+                // sum and count by a 0 / 1 factor (fma: one rounding, = the add)
+                const double f = (v[e] > tau) ? 1.0 : 0.0;
+                sl = __builtin_fma(f, v[e], sl);
+                cl += f;
+            }
+            S = grp_sum_d<PIPE_LPB>(sl);
+            c = grp_sum_d<PIPE_LPB>(cl);
+            const bool more = (k > 0) & need & (c != cprev);
+            cprev = c;
+            tau = fmin((S - 1.0) / c, Mdn);
+            if (!__builtin_amdgcn_ballot_w64(more)) break;
+        }
+        lam = (1. - S) / c;
+    }
+    // out from the registers; padding slots' offsets past the range, so the
+    // hardware drops their stores (no per-slot branch)
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e) {
+        const double r = need ? relu_ref(lam + v[e]) : v[e];
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, r), G.rs,
+            (e < ne) ? G.base + 8 * PIPE_LPB * e : 0x7FFFFFF0, 0, 0);
+    }
+}
+
+// One wave: PIPE_G consecutive groups, straight-line (unrolled at compile
+// time): the starts of all of them first, then per group h the entries of
+// group h + 1 are loaded before the passes on group h (whose entries were
+// loaded one step earlier) and its stores.  Straight-line code keeps the
+// compiler's vmcnt waits exact -- a persistent loop merged its states at the
+// loop head and waited for the next group's loads before the compute -- and
+// every memory operation is unconditional: a group past the last is a
+// clamped copy with k = 0, whose stores the hardware drops.
+template <bool BALL, bool BIG, int PIPE_G>
+__global__ __launch_bounds__(256, 4) void proj_pipe_kernel(double *__restrict__ y,
+                                                          const int64_t *__restrict__ starts,
+                                                          int64_t nb, int64_t n,
+                                                          int64_t *__restrict__ big_list,
+                                                          unsigned *__restrict__ big_count,
+                                                          const double *__restrict__ gate) {
+    if (gate && *gate != 1.0) return;
+    const int lane = lane_id(), j = lane % PIPE_LPB;
+    const int64_t ngrp = (nb + PIPE_BPG - 1) / PIPE_BPG;
+    const int64_t q0 = (int64_t)__builtin_amdgcn_readfirstlane(
+                           (int)(blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE)) * PIPE_G;
+    if (q0 >= ngrp) return;
+    long long st[PIPE_G];
+#pragma unroll
+    for (int h = 0; h < PIPE_G; ++h)
+        st[h] = pipe_meta(starts, nb, n, (q0 + h < ngrp) ? q0 + h : ngrp - 1, lane);
+    asm volatile("" ::: "memory");
+    PipeGroup P[PIPE_G];
+    double v[PIPE_G][PIPE_EB];
+    P[0] = pipe_setup<BIG>(y, st[0], q0, nb, big_list, big_count, true, lane);
+    pipe_load(P[0], v[0]);
+#pragma unroll
+    for (int h = 0; h < PIPE_G; ++h) {
+        if (h + 1 < PIPE_G) {
+            const int64_t q = q0 + h + 1;
+            const bool real = q < ngrp;
+            P[h + 1] = pipe_setup<BIG>(y, st[h + 1], real ? q : ngrp - 1, nb, big_list, big_count,
+                                       real, lane);
+            if (!real) P[h + 1].k = 0;
+            pipe_load(P[h + 1], v[h + 1]);
+        }
+        // (keeps the compiler from sinking those loads past the passes)
+        asm volatile("" ::: "memory");
+        pipe_solve<BALL>(P[h], v[h], j);
+    }
+}
+
 struct ProjWork {
     unsigned *count;
     int64_t *list;
@@ -1029,8 +1219,35 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
         const int v = e ? atoi(e) : 0;
         return (v == 2 || v == 4 || v == 8) ? v : 0;
     }();
+    // the pipelined kernel's groups per wave (BSLS_PROJ_PIPE = 1, 2, 4 or 8,
+    // A/B; 0 = the lane-per-block Michelot form below)
+    static const int pipe = [] {
+        const char *e = getenv("BSLS_PROJ_PIPE");
+        const int v = e ? atoi(e) : 4;
+        return (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
+    }();
     const int64_t ngrp = (nb + WAVE - 1) / WAVE;
-    if (fast && lpb == 0) {
+    // (its group ranges must stay below 2 GB of y: max_block bounds them)
+    if (fast && lpb == 0 && pipe > 0 && max_block <= ((int64_t)1 << 24)) {
+        const int64_t groups = (nb + PIPE_BPG - 1) / PIPE_BPG;
+        const int64_t waves = (groups + pipe - 1) / pipe;
+        const unsigned grid = (unsigned)((waves + 3) / 4);
+        const bool big = max_block > SMALL_MAX;
+#define BSLS_PIPE_LAUNCH(G)                                                                     \
+    do {                                                                                        \
+        if (big)                                                                                \
+            proj_pipe_kernel<BALL, true, G><<<grid, 256, 0, st>>>(y, starts, nb, n, w.list,     \
+                                                                  w.count, gate);               \
+        else                                                                                    \
+            proj_pipe_kernel<BALL, false, G><<<grid, 256, 0, st>>>(y, starts, nb, n, w.list,    \
+                                                                   w.count, gate);              \
+    } while (0)
+        if (pipe == 1) BSLS_PIPE_LAUNCH(1);
+        else if (pipe == 2) BSLS_PIPE_LAUNCH(2);
+        else if (pipe == 8) BSLS_PIPE_LAUNCH(8);
+        else BSLS_PIPE_LAUNCH(4);
+#undef BSLS_PIPE_LAUNCH
+    } else if (fast && lpb == 0) {
         proj_lds_kernel<BALL, 2, true><<<(unsigned)((ngrp + 1) / 2), 2 * WAVE, 0, st>>>(
             y, starts, nb, n, w.list, w.count, max_block > SMALL_MAX, gate);
     } else if (fast) {

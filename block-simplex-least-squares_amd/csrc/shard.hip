@@ -66,6 +66,8 @@ using namespace bsls;
 struct bsls_comm {
     ncclComm_t comm;
     int world, rank;
+    bsls_all_reduce_fn fn;   // set: the host callback replaces RCCL
+    void *user;
 };
 
 // RCCL failures map to BSLS_E_COMM - ncclResult (distinct from hip errors)
@@ -89,7 +91,7 @@ extern "C" int bsls_comm_create(const void *id, int world, int rank, bsls_comm *
     if (!R.ok) return BSLS_E_COMM;
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
-    bsls_comm *c = new bsls_comm{nullptr, world, rank};
+    bsls_comm *c = new bsls_comm{nullptr, world, rank, nullptr, nullptr};
     const int rc = comm_rc(R.init(&c->comm, world, uid, rank));
     if (rc != BSLS_OK) {
         delete c;
@@ -99,32 +101,42 @@ extern "C" int bsls_comm_create(const void *id, int world, int rank, bsls_comm *
     return BSLS_OK;
 }
 
+extern "C" int bsls_comm_create_callback(int world, int rank, bsls_all_reduce_fn fn, void *user,
+                                         bsls_comm **out) {
+    if (!fn || !out || world < 1 || rank < 0 || rank >= world) return BSLS_E_ARG;
+    *out = new bsls_comm{nullptr, world, rank, fn, user};
+    return BSLS_OK;
+}
+
 extern "C" int bsls_comm_destroy(bsls_comm *c) {
     if (!c) return BSLS_OK;
-    const int rc = comm_rc(rccl().destroy(c->comm));
+    const int rc = c->fn ? BSLS_OK : comm_rc(rccl().destroy(c->comm));
     delete c;
     return rc;
 }
 
+// the one all-reduce of both transports: in place, sum, on `stream`
+static int comm_sum(bsls_comm *c, double *buf, size_t count, hipStream_t st) {
+    if (c->fn) return c->fn(buf, (int64_t)count, (void *)st, c->user) == 0 ? BSLS_OK : BSLS_E_COMM;
+    return comm_rc(rccl().all_reduce(buf, buf, count, ncclFloat64, ncclSum, c->comm, st));
+}
+
 extern "C" int bsls_comm_all_reduce(bsls_comm *c, double *buf, int64_t count, void *stream) {
     if (!c || !buf || count < 0) return BSLS_E_ARG;
-    return comm_rc(rccl().all_reduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->comm,
-                                     (hipStream_t)stream));
+    return comm_sum(c, buf, (size_t)count, (hipStream_t)stream);
 }
 
 extern "C" int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *c, int64_t first_iter,
                                      int64_t count, int fuse, void *stream) {
     if (!p || !c || first_iter < 1 || count < 0 || fuse < 0 || fuse > 2) return BSLS_E_ARG;
     if (p->shard_role != (c->rank == 0 ? 1 : 2)) return BSLS_E_ARG;   // target added once
-    const RcclApi &R = rccl();
     hipStream_t st = (hipStream_t)stream;
     // a sum over one rank is the identity: a one-rank communicator (the
     // rehearsal of one rank's share on one GPU) skips the collectives, whose
     // one-rank form is RCCL's own copies and flag fills (~17 us an iteration)
     const bool comm = c->world > 1;
     auto all_reduce = [&](double *buf, size_t cnt) -> int {
-        if (!comm) return BSLS_OK;
-        return comm_rc(R.all_reduce(buf, buf, cnt, ncclFloat64, ncclSum, c->comm, st));
+        return comm ? comm_sum(c, buf, cnt, st) : BSLS_OK;
     };
     int rc;
     for (int64_t i = first_iter; i < first_iter + count; ++i) {

@@ -215,14 +215,25 @@ __device__ __forceinline__ void tile_vals4(const double *__restrict__ val, int64
 // land in).  fxs = 2^k puts every term * fxs within [-2^50, 2^50]; the high
 // word takes it rounded to an integer (the 1.5 * 2^52 trick: one add, one
 // 64-bit subtract), the low word the exact remainder scaled by 2^50 and
-// rounded: 100 bits below the bound, two ds_add_u64 per entry.  The low
-// words sit H + halo + 1 slots after the high ones (twice the LDS).
+// rounded (2^-s of the unit, s = fx_lo_shift: ~100 bits below the bound),
+// two ds_add_u64 per entry.  The low words sit H + halo + 1 slots after the
+// high ones (twice the LDS).
 constexpr double FX_MAGIC = 6755399441055744.0;   // 1.5 * 2^52: ulp 1 over +-2^51
 
-__device__ __forceinline__ void fx_add(double *rows, int lr, int lo_off, double v) {
+// The low word's scale 2^s: a row of N <= cols entries adds at most N 2^(s-1)
+// to it (every remainder |v - h| <= 1/2, all of one sign at worst -- e.g.
+// x = 1/3 on a dense link), so 2^s <= 2^62 / 2^bit_width(cols) keeps the sum
+// inside int64 whatever the remainders: s = 50 up to 4095 columns, 38 at 10M
+// (a term then rounds by 2^-(s+1) of the unit = bound 2^-(s+51), still ~2^-89).
+__host__ __device__ inline int fx_lo_shift(int64_t cols) {
+    const int bw = cols > 0 ? 64 - __builtin_clzll((unsigned long long)cols) : 0;
+    return 62 - bw < 50 ? 62 - bw : 50;
+}
+
+__device__ __forceinline__ void fx_add(double *rows, int lr, int lo_off, double v, double los) {
     const double t = v + FX_MAGIC;
     const double h = t - FX_MAGIC;                  // v rounded to an integer, exactly
-    const double l = (v - h) * 0x1p50;              // |v - h| <= 1/2: exact, then scaled
+    const double l = (v - h) * los;                 // |v - h| <= 1/2: exact, then scaled
     const double tl = l + FX_MAGIC;
     atomicAdd(reinterpret_cast<unsigned long long *>(&rows[lr]),
               (unsigned long long)(__double_as_longlong(t) - __double_as_longlong(FX_MAGIC)));
@@ -230,11 +241,12 @@ __device__ __forceinline__ void fx_add(double *rows, int lr, int lo_off, double 
               (unsigned long long)(__double_as_longlong(tl) - __double_as_longlong(FX_MAGIC)));
 }
 
-// a row's two words back to a double: hi 2^-k + lo 2^-(k+50)
-__device__ __forceinline__ double fx_value(const double *rows, int lr, int lo_off, double inv) {
+// a row's two words back to a double: hi 2^-k + lo 2^-(k+s), inv_lo = 2^-(k+s)
+__device__ __forceinline__ double fx_value(const double *rows, int lr, int lo_off, double inv,
+                                           double inv_lo) {
     const long long hi = reinterpret_cast<const long long *>(rows)[lr];
     const long long lo = reinterpret_cast<const long long *>(rows)[lr + lo_off];
-    return (double)hi * inv + (double)lo * (inv * 0x1p-50);
+    return (double)hi * inv + (double)lo * inv_lo;
 }
 
 template <int MODE, bool NT, bool PK3 = false, int VT = 0, int P = BSLS_TILE_P,
@@ -268,6 +280,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
     const int64_t v0 = 4 * l0;   // first value of this lane (MODE 1)
     const double *xb = src + T.group_col[g];
     const int lo_off = (int)(T.H + T.halo + 1);     // FX: the low words
+    const double fxl = FX ? ldexp(1.0, fx_lo_shift(T.cols)) : 0.0;
     ent_t ring[P];
     int4 bring[P];
 #pragma unroll
@@ -310,7 +323,7 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
 #elif BSLS_TILE_KO == 2
                     ko += term;                       // (knock-out: no LDS)
 #else
-                    if constexpr (FX) fx_add(rows, lr, lo_off, term * fxs);
+                    if constexpr (FX) fx_add(rows, lr, lo_off, term * fxs, fxl);
                     else atomicAdd(&rows[lr], term);
 #endif
                 }

@@ -1029,6 +1029,12 @@ class BBEngine:
         # PAVA, not bit-identical): on unless deterministic; BSLS_K3_WARM=0/1
         warm = os.environ.get('BSLS_K3_WARM')
         P.pava_warm = int(warm) if warm is not None else (0 if deterministic else 1)
+        # K1's group sums by atomics (column shards) / K3's pack form: the
+        # defaults unless BSLS_K1_ATOMIC / BSLS_K3_MERGE = 0 / 1 (read here,
+        # once, not per launch)
+        for field, env in (('k1_atomic', 'BSLS_K1_ATOMIC'), ('k3_merge', 'BSLS_K3_MERGE')):
+            v = os.environ.get(env)
+            setattr(P, field, 0 if v is None else (2 if int(v) else 1))
         self.P = P
         self.z0 = None
         if xin is not None:

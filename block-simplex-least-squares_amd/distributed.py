@@ -11,15 +11,21 @@ z, g, x.  Per BB iteration:
               1/world slice of ||r||^2 (r is the same all-reduced vector on
               every rank)
     all-reduce(sum) of the 4 BB sums and ||r||^2  (40 bytes)
-    stage 13  f and the stopping test of the previous iteration (every rank
+    stage 15  f and the stopping test of the previous iteration (every rank
               tests the same summed values, so every rank decides alike), then
-              t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = x0_g + N_g z_g  (K3)
-    stage 1   r_g = A_g x_g, + target on rank 0 (partial residual, length m)
+              t, z_g <- clip01(PAVA(z_g - t g_g)), x_g = x0_g + N_g z_g  (K3),
+              and -- where K1 adds its column groups' sums by atomics -- r set
+              to target (rank 0) / 0 for them
+    stage 14  r_g = A_g x_g, + target on rank 0 (partial residual, length m)
     all-reduce(sum) of r_g  (8 m bytes: the one real exchange of the algorithm)
 and after the last iteration of a call stage 9 (||r||^2, f, stopping test of
-that iteration).  Once the run has stopped, ranks other than 0 write r = 0 in
-stage 1 and rank 0 leaves its r (the final residual) alone, so the all-reduce
-keeps the final residual intact (csrc/bb.hip k1_stopped_rows).
+that iteration).  Once the run has stopped, ranks other than 0 write r = 0 and
+rank 0 leaves its r (the final residual) alone, so the all-reduce keeps the
+final residual intact (csrc/bb.hip k1_stopped_rows), and ranks other than 0
+zero their BB sums before the five-sum all-reduce (k2_stopped_sums).  The
+Python loop below and the C++ driver (bsls_bb_shard_iterate) enqueue the same
+stages; the C++ one takes RCCL (RcclComm) or any transport through a callback
+(CallbackComm).
 
 The collectives go through torch.distributed: backend "nccl" is RCCL over xGMI
 on MI355X; "gloo" runs the same orchestration in CPU tests with a fake stage
@@ -149,7 +155,8 @@ class ShardedBB:
         """r = sum over ranks of A_g x_g (before stage 2)."""
         e = self.e
         if not self._slices:
-            e.stage(1, it)
+            # (stage 14: K1 after stage 15, which may have initialised r)
+            e.stage(14 if (self.fuse == 2 and it > 0) else 1, it)
             self.all_reduce(e.r)
             return
         works = []
@@ -175,16 +182,23 @@ class ShardedBB:
             import _native
             from _native import check, stream_handle
             if count > 0:
-                check(_native.lib().bsls_bb_shard_iterate(e.P, self.native.handle, int(first),
-                                                          int(count), int(self.fuse),
-                                                          stream_handle()),
-                      'bsls_bb_shard_iterate')
+                rc = _native.lib().bsls_bb_shard_iterate(e.P, self.native.handle, int(first),
+                                                         int(count), int(self.fuse),
+                                                         stream_handle())
+                err = getattr(self.native, 'error', None)
+                if rc != 0 and err is not None:
+                    raise RuntimeError('bsls_bb_shard_iterate: all-reduce callback failed') from err
+                check(rc, 'bsls_bb_shard_iterate')
             return
         for i in range(first, first + count):
             if self.fuse == 2:
                 e.stage(10, i)   # K2 + this rank's slice of ||r||^2
                 self.all_reduce(e.scal[self.SUMS_RR])
-                e.stage(13, i)   # K3 after f / the stopping test of iteration i - 1
+                # K3 after f / the stopping test of iteration i - 1; stage 15
+                # also sets r to target / 0 for stage 14's atomic K1 where the
+                # library folds that in (what bsls_bb_shard_iterate enqueues);
+                # row parts keep stage 13 (each part initialises its rows)
+                e.stage(13 if self._slices else 15, i)
             else:
                 e.stage(8 if self.fuse else 3, i)   # (8: + f / stop test of i - 1)
                 self.all_reduce(e.scal[self.SUMS])
@@ -210,6 +224,58 @@ def torch_all_reduce_async(group=None):
     def f(t):
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
     return f
+
+
+class CallbackComm:
+    """A C-ABI communicator whose all-reduce is a Python callable
+    (bsls_comm_create_callback, csrc/shard.hip): the native driver
+    bsls_bb_shard_iterate then runs its world > 1 loop -- both shard roles, the
+    five-sum and r all-reduces between its stages -- over any transport, e.g.
+    gloo ranks sharing one GPU in the tests.  `all_reduce(t)` sums a float64
+    device tensor in place across the ranks; `views` are the tensors the
+    driver reduces (the engine's scal and r), found by their device address.
+    The callback synchronises the stream before reducing, so the sum sees the
+    stages enqueued before it, and returns before the next stage is enqueued."""
+
+    def __init__(self, all_reduce, views, rank=None, world=None):
+        import ctypes
+        import _native
+        from _native import check
+        self.rank = _shard_rank(rank)
+        self.world = int(world) if world is not None else _world_size()
+        self._views = [(int(v.data_ptr()), v) for v in views]
+        self._fn = all_reduce
+        self.error = None
+
+        def cb(buf, count, stream, user):
+            try:
+                import torch
+                t = None
+                for base, v in self._views:
+                    off = (int(buf) - base) // 8
+                    if 0 <= off and off + count <= v.numel() and int(buf) == base + 8 * off:
+                        t = v[off:off + count]
+                        break
+                if t is None:
+                    raise ValueError('all-reduce of an unknown buffer 0x%x' % int(buf))
+                torch.cuda.synchronize()
+                self._fn(t)
+                return 0
+            except Exception as exc:      # reported as BSLS_E_COMM by the driver
+                self.error = exc
+                return 1
+        self._cb = _native.ALL_REDUCE_FN(cb)    # kept alive with the communicator
+        h = ctypes.c_void_p()
+        check(_native.lib().bsls_comm_create_callback(self.world, self.rank, self._cb, None,
+                                                      ctypes.byref(h)),
+              'bsls_comm_create_callback')
+        self.handle = h
+
+    def close(self):
+        import _native
+        if self.handle is not None:
+            _native.lib().bsls_comm_destroy(self.handle)
+            self.handle = None
 
 
 class RcclComm:

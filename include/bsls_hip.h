@@ -369,6 +369,16 @@ typedef struct bsls_bb_problem {
      * PAVA (the north star's 1e-12), not bit-identical; 0: the reference
      * passes always (bit-identical). */
     int64_t pava_warm;
+    /* K1's column-group sums (tile images with several groups): 0 = auto --
+     * global f64 atomics into r on a column shard (shard_role 1 / 2), the
+     * ordered group partials on one GCD; 1 = always the partials; 2 = atomics
+     * wherever K1 has several groups.  (BSLS_K1_ATOMIC=0 / 1 of the Python
+     * engine map to 1 / 2, read once when the problem is built.) */
+    int64_t k1_atomic;
+    /* K3's pack form: 0 = auto (two packs per wave sharing their later PAVA
+     * passes from 64k packs on), 1 = one pack per wave, 2 = always two
+     * (BSLS_K3_MERGE=0 / 1 of the Python engine). */
+    int64_t k3_merge;
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
@@ -415,8 +425,11 @@ int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int64_t count,
  * bsls_bb_iterate runs 3, 4, 7.  The column-sharded driver (distributed.py,
  * shard_role 1 / 2) runs 8, [allreduce sums], 4, 1, [allreduce r] per
  * iteration and 9 after the last one (fuse 1), or the sliced form 10,
- * [allreduce 5 sums], 13, 1, [allreduce r] (fuse 2, the default; the native
- * driver bsls_bb_shard_iterate runs 15 and 14 in place of 13 and 1). */
+ * [allreduce 5 sums], 15, 14, [allreduce r] (fuse 2, the default; both the
+ * native driver bsls_bb_shard_iterate and the Python loop; 13 and 1 where K1
+ * runs in row parts, bsls_bb_residual_rows).  After a stop, stage 3 / 8 / 10
+ * on a shard_role 2 rank zero its scal[SUMDG..RR], so the all-reduces the
+ * driver still enqueues keep the stop iteration's sums (role 1's copy). */
 int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
 /* Stage 1 restricted to K1's row blocks [rb0, rb1) (rows rb0 * R .. rb1 * R - 1,
  * R = *rows_per_block from bsls_bb_row_blocks, which returns the block count):
@@ -488,10 +501,21 @@ size_t bsls_comm_id_bytes(void);
 int bsls_comm_unique_id(void *id_out);
 int bsls_comm_create(const void *id, int world, int rank, bsls_comm **out);
 int bsls_comm_destroy(bsls_comm *comm);
+/* A communicator whose all-reduce is a host callback instead of RCCL (a
+ * different transport -- MPI, gloo, a test double -- under the same C++
+ * driver loop).  fn(d_buf, count, stream, user) must leave the sum over the
+ * ranks in d_buf (device memory) ordered after the work already enqueued on
+ * `stream` and before the work enqueued after the call returns (e.g.
+ * synchronise the stream, reduce, copy back); it returns 0 or nonzero on
+ * failure (-> BSLS_E_COMM).  Called on the enqueueing thread, in order.
+ * bsls_comm_destroy frees it (no RCCL involved). */
+typedef int (*bsls_all_reduce_fn)(double *d_buf, int64_t count, void *stream, void *user);
+int bsls_comm_create_callback(int world, int rank, bsls_all_reduce_fn fn, void *user,
+                              bsls_comm **out);
 /* in-place sum of `count` doubles over the ranks, on `stream` */
 int bsls_comm_all_reduce(bsls_comm *comm, double *d_buf, int64_t count, void *stream);
 /* Iterations first_iter .. first_iter+count-1 of the sharded schedule (fuse 2:
- * per iteration stage 10, all-reduce scal[SUMDG..RR], stage 13, stage 1,
+ * per iteration stage 10, all-reduce scal[SUMDG..RR], stage 15, stage 14,
  * all-reduce r; fuse 1: stage 8, all-reduce scal[SUMDG..GG], 4, 1,
  * all-reduce r; fuse 0: stage 3 instead of 8 and a stage 9 after every r
  * exchange; stage 9 after the last iteration in all three).  p->shard_role

@@ -23,8 +23,13 @@ PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
 class FakeStages:
     """NumPy model of bsls_bb_stage for one column shard."""
 
-    def __init__(self, A, AT, sizes, target, orc, max_iter):
+    def __init__(self, A, AT, sizes, target, orc, max_iter, fold=True):
         self.A, self.AT, self.sizes, self.target = A, AT, np.asarray(sizes), target
+        # fold: K1 adds its column groups' sums by atomics into an r that
+        # stage 15 (the K3 before it) initialised -- a column shard's dealt K1
+        # with several groups (csrc/bb.hip k1_init_folded); else stage 15 / 14
+        # are stages 13 / 1
+        self.fold = fold
         self.orc, self.max_iter = orc, max_iter
         self.n = int(self.sizes.sum())
         self.nz = self.n - len(self.sizes)
@@ -76,6 +81,28 @@ class FakeStages:
             v = v + self.target[r0:r1]
         self.r[r0:r1] = torch.from_numpy(v)
 
+    def _init_r(self):
+        """stage 15's r initialisation (bb_k3 kinit): target on role 1, 0 on
+        role 2; once stopped role 1 keeps r and role 2 writes 0."""
+        if float(self.scal[0]) != 0:
+            if self.role == 2:
+                self.r.zero_()
+            return
+        self.r[:] = torch.from_numpy(self.target.copy()) if self.role == 1 else 0.0
+
+    def _add_partial(self, it):
+        """stage 14 after a folding stage 15: the groups' sums add into r
+        (nothing once stopped: stage 15 already left r as it must be)."""
+        if float(self.scal[0]) != 0:
+            return
+        self.r += torch.from_numpy(self.A.dot(self.x))
+
+    def _stopped_sums(self, k):
+        """K2 of a stopped run (k2_stopped_sums): role 2 zeroes the sums the
+        driver all-reduces next, so the sum keeps role 1's."""
+        if self.role == 2:
+            self.scal[5:10 if k == 10 else 9] = 0.0
+
     def residual_rows(self, it, rb0, rb1):
         self._partial(it, rb0 * self.ROWS, min(rb1 * self.ROWS, self.A.shape[0]))
 
@@ -100,8 +127,19 @@ class FakeStages:
             self._partial(it, 0, self.A.shape[0])
         elif k == 9:
             self._record(it)
+        elif k == 14:
+            if self.fold:
+                self._add_partial(it)
+            else:
+                self._partial(it, 0, self.A.shape[0])
+        elif k == 15:             # stage 13 with stage 14's r initialisation
+            self.stage(12, it)
+            if self.fold:
+                self._init_r()
+            self.stage(4, it)
         elif k in (3, 8, 10):
             if it > 0 and float(s[0]) != 0:
+                self._stopped_sums(k)
                 return
             g = self.Ntw(self.AT.dot(self.r.numpy()))
             if it == 0:
@@ -112,6 +150,9 @@ class FakeStages:
             dz = self.z[zc] - self.z[zn]
             if k == 8:
                 self._record(it - 1)     # before this iteration's sums land
+                if float(s[0]) != 0:     # stopped at it - 1: its sums stay
+                    self._stopped_sums(k)
+                    return
             if k == 10:
                 s[11:15] = s[5:9].clone()            # iteration it - 1's sums, for stage 12
                 rs = self.r[self.rr_lo:self.rr_hi] if self.rr_hi > self.rr_lo else self.r
@@ -160,7 +201,7 @@ class _Done:
         pass
 
 
-def _run(rank, world, iters, out_q, parts=1, stop_at=None):
+def _run(rank, world, iters, out_q, parts=1, stop_at=None, fold=True):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, PKG)
     from oracle import oracle as orc
@@ -184,7 +225,7 @@ def _run(rank, world, iters, out_q, parts=1, stop_at=None):
     part = torch.from_numpy(A_g.dot(x0))
     red(part)
     target = part.numpy() - b
-    eng = FakeStages(A_g, A_g.T.tocsr(), sz_g, target, orc, stop_at or iters)
+    eng = FakeStages(A_g, A_g.T.tocsr(), sz_g, target, orc, stop_at or iters, fold=fold)
     drv = ShardedBB(eng, red, parts=parts, all_reduce_async=red_async, rank=rank)
     drv.prologue()
     traj = {}
@@ -200,12 +241,13 @@ def _run(rank, world, iters, out_q, parts=1, stop_at=None):
         dist.destroy_process_group()
 
 
-def _spawn(world, iters, parts=1, stop_at=None):
+def _spawn(world, iters, parts=1, stop_at=None, fold=True):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
-    os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000) + 7 * parts + (stop_at or 0))
+    os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000) + 7 * parts + (stop_at or 0)
+                                    + 3 * int(fold))
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_run, args=(r, world, iters, q, parts, stop_at))
+    procs = [ctx.Process(target=_run, args=(r, world, iters, q, parts, stop_at, fold))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -219,10 +261,11 @@ def _spawn(world, iters, parts=1, stop_at=None):
 
 
 @pytest.mark.timeout(600)
-def test_two_rank_sharded_bb_matches_single_and_oracle(orc):
+@pytest.mark.parametrize('fold', [True, False])
+def test_two_rank_sharded_bb_matches_single_and_oracle(orc, fold):
     iters = 20
-    one = _spawn(1, iters)
-    two = _spawn(2, iters)
+    one = _spawn(1, iters, fold=fold)
+    two = _spawn(2, iters, fold=fold)
     for i in one:
         d = np.max(np.abs(one[i] - two[i])) / max(1.0, np.max(np.abs(one[i])))
         assert d < 1e-10, (i, d)
@@ -246,17 +289,24 @@ def test_two_rank_overlapped_residual_matches_single(orc):
 
 
 @pytest.mark.timeout(600)
-def test_two_rank_stop_keeps_final_residual(orc):
+@pytest.mark.parametrize('fold', [True, False])
+def test_two_rank_stop_keeps_final_residual(orc, fold):
     """Iterations enqueued past the stop (max_iter 5, 9 enqueued) leave r the
     final residual on both ranks -- rank 0 keeps its r, rank 1 writes 0 before
-    each all-reduce -- and the stop is reported at iteration 5 on both."""
-    one = _spawn(1, 9, stop_at=5)
-    two = _spawn(2, 9, stop_at=5)
+    each all-reduce (in stage 15's r initialisation where it folds, fold=True,
+    the library's choice for a dealt K1 with several column groups; in stage
+    1 / 14 otherwise) -- the stop is reported at iteration 5 on both, and the
+    BB sums stay iteration 5's (rank 1 zeroes its copy before each five-sum
+    all-reduce past the stop, k2_stopped_sums, instead of doubling them)."""
+    one = _spawn(1, 9, stop_at=5, fold=fold)
+    two = _spawn(2, 9, stop_at=5, fold=fold)
     r1 = one[0]['r']
     for rank in (0, 1):
         assert two[rank]['scal'][0] == 2 and two[rank]['scal'][1] == 5
         d = np.max(np.abs(two[rank]['r'] - r1)) / max(1.0, np.max(np.abs(r1)))
         assert d < 1e-10, (rank, d)
+        s1, s2 = one[0]['scal'][5:9], two[rank]['scal'][5:9]
+        assert np.max(np.abs(s2 - s1)) <= 1e-9 * max(1.0, np.max(np.abs(s1))), (rank, s1, s2)
 
 
 @pytest.mark.timeout(600)
@@ -267,6 +317,10 @@ def test_two_rank_unfused_schedule(orc, monkeypatch):
     trajectory, and the same stop."""
     iters = 10
     fused = _spawn(2, iters)                    # the sliced schedule (fuse 2, default)
+    base = _spawn(2, 9, stop_at=5)
+    for rank in (0, 1):
+        assert base[rank]['scal'][0] == 2 and base[rank]['scal'][1] == 5
+    s5 = base[0]['scal'][5:9]
     for mode in ('0', '1'):
         monkeypatch.setenv('BSLS_SHARD_FUSE', mode)
         plain = _spawn(2, iters)
@@ -277,10 +331,9 @@ def test_two_rank_unfused_schedule(orc, monkeypatch):
         for rank in (0, 1):
             assert two[rank]['scal'][0] == 2 and two[rank]['scal'][1] == 5, mode
             # the stopping iteration's sums stay in scal whatever the schedule
+            d = np.max(np.abs(two[rank]['scal'][5:9] - s5)) / max(1.0, np.max(np.abs(s5)))
+            assert d < 1e-9, (mode, rank, d)
         monkeypatch.delenv('BSLS_SHARD_FUSE')
-    base = _spawn(2, 9, stop_at=5)
-    for rank in (0, 1):
-        assert base[rank]['scal'][0] == 2 and base[rank]['scal'][1] == 5
 
 
 def test_row_parts():

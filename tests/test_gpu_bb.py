@@ -19,6 +19,12 @@ def rel_err(a, b):
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
 
 
+def elem_err(a, b):
+    """max over elements of |a - b| / max(1, |b|)."""
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
+
+
 @pytest.mark.parametrize('tag', ['bbs', 'bbc'])
 def test_bb_trajectory_vs_reference(cuda, golden, tag):
     from device import BBEngine
@@ -108,8 +114,11 @@ def test_bb_fixed_iterations_match_oracle_at_scale(cuda, shard100k, general, fmt
         rec[i] = s
         return 0.0
     eng.solve(log=log, record_every=1, poll=1)
+    # per element: the fixed-order formats at 1e-10 (measured ~1e-13), the
+    # run-dependent ones (LDS / global atomics) at the north star's 1e-6
+    tol = 1e-10 if fmt in DETERMINISTIC else 1e-6
     for i in (1, 10, 50):
-        assert rel_err(rec[i], ref[i]) < 1e-6, (i, rel_err(rec[i], ref[i]))
+        assert elem_err(rec[i], ref[i]) <= tol, (i, elem_err(rec[i], ref[i]))
 
 
 @pytest.mark.parametrize('fmt', sorted(FORMATS))

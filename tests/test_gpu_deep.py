@@ -26,8 +26,9 @@ PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
 
 
 def rel_err(a, b):
-    a, b = np.asarray(a), np.asarray(b)
-    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+    """max over elements of |a - b| / max(1, |b|)."""
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
 
 
 def _run_engine(eng, iters):
@@ -58,8 +59,11 @@ def test_c3_noise_free_iterates_1_10_50_200(c3_clean, deterministic):
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 200, 'opt_tol': 1e-30},
                    AT=sh['AT'], deterministic=deterministic)
     rec = _run_engine(eng, 200)
+    # per element: the fixed-order engine at 1e-10 (measured ~1e-13), the
+    # default one (run-dependent atomic sums) at the north star's 1e-6
+    tol = 1e-10 if deterministic else 1e-6
     for i in (1, 10, 50, 200):
-        assert rel_err(rec[i], ref[i]) < 1e-6, (deterministic, i, rel_err(rec[i], ref[i]))
+        assert rel_err(rec[i], ref[i]) <= tol, (deterministic, i, rel_err(rec[i], ref[i]))
 
 
 @pytest.mark.timeout(1200)

@@ -204,3 +204,32 @@ def test_lsq_fixed_point_residual_edges(cuda):
         op.residual(torch.from_numpy(x).cuda(), r, add=add)
         outs.append(r.cpu().numpy().copy())
     assert all(exact(o, outs[0]) for o in outs)
+
+
+def test_lsq_fixed_point_dense_row_lined_up_remainders(cuda):
+    """k1='tiles_fixed' on a link that every route crosses (one row holding all
+    600k columns) with x = 1/3 everywhere (blocks of 3 at their uniform
+    point): every term has the same rounding remainder, so a low word scaled
+    by 2^50 per term would take 75k x 2^48 > 2^63 in one tile row and wrap
+    (ADVICE r04).  The low word's scale now follows the column count
+    (tiles.hpp fx_lo_shift): r matches SciPy to 1e-12, and repeats bit for bit."""
+    import torch
+    from device import DeviceLSQ
+    rs = np.random.RandomState(SEED + 10)
+    m, n = 64, 600_000
+    rows = [np.arange(n)]                                    # row 0: dense
+    for _ in range(1, m):
+        rows.append(np.sort(rs.choice(n, 4000, replace=False)))
+    indptr = np.concatenate(([0], np.cumsum([len(r) for r in rows])))
+    A = sps.csr_matrix((np.ones(indptr[-1]), np.concatenate(rows), indptr), shape=(m, n))
+    op = DeviceLSQ(A, A.T.tocsr(), k1='tiles_fixed', k2='panels')
+    assert op.k1 == 'tiles_fixed'
+    x = np.full(n, 1.0 / 3.0)
+    r = torch.empty(m, dtype=torch.float64, device='cuda')
+    ref = A.dot(x)
+    outs = []
+    for _ in range(2):
+        op.residual(torch.from_numpy(x).cuda(), r)
+        outs.append(r.cpu().numpy().copy())
+    np.testing.assert_allclose(outs[0], ref, rtol=1e-12, atol=0)
+    assert exact(outs[0], outs[1])

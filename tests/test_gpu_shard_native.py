@@ -1,0 +1,281 @@
+"""The native sharded driver at world 2 (bsls_bb_shard_iterate, csrc/shard.hip),
+i.e. the schedule bench.py ships at N > 1, on one MI355X.
+
+RCCL refuses two ranks on one device, so the two ranks share the GPU and
+their all-reduces go through gloo: distributed.CallbackComm hands the C++
+loop a host callback (bsls_comm_create_callback) in place of RCCL.  That
+runs the driver's world > 1 branch as shipped -- stage 10, the five-sum
+all-reduce, stage 15 (K3 + the atomic K1's r initialisation: target on
+shard_role 1, 0 on shard_role 2), stage 14 (the atomic K1), the r
+all-reduce -- with both shard roles.  The reference has no parallel code
+(SURVEY.md §2); the split is blockify's contiguous blocks
+(python/bsls_matrices.py:109-126) and the oracle is the
+one-process BB trajectory (python/BB.py:7-45 over main.py:53-65).
+
+* iterates at 1 / 5 / 20 on make_partitioned's C5-density 2-way split
+  (1.2M routes, 120k links: the entries-per-link density of an 8-way C5
+  shard) against the oracle;
+* the stop: iterations enqueued past max_iter change nothing, r stays the
+  final residual and the BB sums stay the stop iteration's on both ranks;
+* convergence (python/BB.py:21-24, tests/fast/test_main.py:31-47): the three
+  tests/fast problems run to their own exit on the sharded driver (atomic
+  K1: run-dependent summation order) -- 0.5||Ax - b||^2 < 1e-16 and the exit
+  iteration within the band the one-GPU test holds around the reference's
+  454 / 569 / 745.
+
+Tolerance: the north star's 1e-6 per element (|d| <= 1e-6 max(1, |ref|)):
+the atomic K1 and the dealt tiles' LDS atomics sum in a run-dependent order.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, 'block-simplex-least-squares_amd')
+SEED = 237423433
+
+N5, P5, M5 = 1_200_000, 60_000, 120_000
+CHECK5 = (1, 5, 20)
+
+
+def elem_err(a, b):
+    """max over elements of |a - b| / max(1, |b|)."""
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
+
+
+def _setup(rank, world, port):
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+
+
+def _engine(A_g, sizes_g, b, x0_g, max_iter, early_exit, **kw):
+    """The rank's BBEngine with target = sum over ranks of A_g x0_g - b."""
+    import torch
+    import torch.distributed as dist
+    from device import BBEngine
+    part = torch.from_numpy(A_g.dot(x0_g))
+    dist.all_reduce(part)
+    target = torch.from_numpy(part.numpy() - b).cuda()
+    eng = BBEngine(A_g, None, sizes_g, options={'max_iter': max_iter, 'opt_tol': 1e-30},
+                   early_exit=early_exit, target=target, **kw)
+    return eng
+
+
+def _driver(eng, rank):
+    from distributed import ShardedBB, CallbackComm, torch_all_reduce
+    comm = CallbackComm(torch_all_reduce(), [eng.scal, eng.r], rank=rank)
+    drv = ShardedBB(eng, torch_all_reduce(), rank=rank, native=comm)
+    assert drv.native is comm and drv.fuse == 2
+    return drv, comm
+
+
+def _finish(comm):
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    comm.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_c5(rank, world, port, out_q):
+    _setup(rank, world, port)
+    import torch
+    from synthetic import make_partitioned
+    full = make_partitioned(N5, P5, M5)
+    sh = make_partitioned(N5, P5, M5, rank=rank, world=world)
+    x0 = np.zeros(sh['n'])
+    x0[np.cumsum(sh['block_sizes']) - 1] = 1.0
+    eng = _engine(sh['A'], sh['block_sizes'], full['Ax'], x0, 10 ** 9, False,
+                  AT=sh['AT'], colv=sh['colv'])
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    drv, comm = _driver(eng, rank)
+    drv.prologue()
+    traj = {}
+    done = 0
+    for i in CHECK5:
+        drv.iterate(done + 1, i - done)          # several iterations per C++ call
+        done = i
+        traj[i] = eng.current_z(i & 1).cpu().numpy().copy()
+    info = dict(role=int(eng.P.shard_role), groups=int(eng.A_til.img['ngroups']),
+                fmt=(eng.fmt_A, eng.fmt_AT))
+    out_q.put((rank, traj, info))
+    _finish(comm)
+
+
+def _spawn(target, world, *args, timeout=600):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 32100 + (os.getpid() % 700) + 7 * len(target.__name__)
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        item = q.get(timeout=timeout)
+        res[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.timeout(900)
+def test_native_driver_two_ranks_c5_density_vs_oracle(cuda, orc):
+    from synthetic import make_partitioned
+    res = _spawn(_run_c5, 2)
+    for r in (0, 1):
+        traj, info = res[r]
+        # both shard roles, the C5 kernels, a K1 with several column groups
+        # (so K1 adds by atomics into the r stage 15 initialised)
+        assert info['role'] == (1 if r == 0 else 2)
+        assert info['fmt'] == ('tiles', 'tiles') and info['groups'] > 1, info
+    full = make_partitioned(N5, P5, M5)
+    ref = orc.bb_trace(full['A'], full['Ax'], full['block_sizes'], max(CHECK5), record_every=1)
+    for i in CHECK5:
+        got = np.concatenate([res[0][0][i], res[1][0][i]])
+        assert elem_err(got, ref[i]) < 1e-6, (i, elem_err(got, ref[i]))
+
+
+# ---- the stop ---------------------------------------------------------------
+
+def _small():
+    from synthetic import make_partitioned, add_noise
+    kw = dict(per_col=8, seed=33, gen_chunks=8)
+    full = make_partitioned(40_000, 2_000, 3_000, **kw)
+    return full, add_noise(full['Ax'], 0.02, seed=33), kw
+
+
+def _run_stop(rank, world, port, out_q, max_iter, enq):
+    _setup(rank, world, port)
+    import torch
+    from synthetic import make_partitioned
+    full, b, kw = _small()
+    sh = make_partitioned(40_000, 2_000, 3_000, rank=rank, world=world, **kw)
+    x0 = np.zeros(sh['n'])
+    x0[np.cumsum(sh['block_sizes']) - 1] = 1.0
+    eng = _engine(sh['A'], sh['block_sizes'], b, x0, max_iter, True, fmt='tiles')
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    drv, comm = _driver(eng, rank)
+    drv.prologue()
+    drv.iterate(1, enq)
+    s = eng.scalars()
+    zb = int(s[2])
+    out_q.put((rank, dict(z=eng.current_z(zb).cpu().numpy().copy(), r=eng.r.cpu().numpy().copy(),
+                          scal=s.copy(), groups=int(eng.A_til.img['ngroups']))))
+    _finish(comm)
+
+
+@pytest.mark.timeout(600)
+def test_native_driver_two_ranks_stop(cuda, orc):
+    """max_iter 7, 30 iterations enqueued in one C++ call: both ranks report the
+    stop at 7 with iteration 7's z, r = the residual of z_7 on both (role 1
+    keeps its r, role 2 writes 0 in stage 15), and the BB sums of iteration 7
+    on both (role 2 zeroes its copy before each all-reduce past the stop)."""
+    res = _spawn(_run_stop, 2, 7, 30)
+    full, b, _ = _small()
+    sizes = full['block_sizes']
+    ref = orc.bb_trace(full['A'], b, sizes, 7, record_every=1)
+    z = np.concatenate([res[0][0]['z'], res[1][0]['z']])
+    assert elem_err(z, ref[7]) < 1e-6
+    from bsls_utils import particular_x0, block_sizes_to_N
+    r7 = full['A'].dot(particular_x0(sizes) + block_sizes_to_N(sizes).dot(ref[7])) - b
+    s0 = res[0][0]['scal']
+    for r in (0, 1):
+        d = res[r][0]
+        assert d['groups'] > 1
+        assert d['scal'][0] == 2 and d['scal'][1] == 7, d['scal'][:3]
+        assert np.max(np.abs(d['r'] - r7)) <= 1e-9 * max(1.0, np.max(np.abs(r7)))
+        # every rank holds the same summed sums -- not world^k times them
+        assert np.array_equal(d['scal'][5:9], s0[5:9]), (d['scal'][5:9], s0[5:9])
+    # ... and they are iteration 7's: the one-GPU engine's sums at its stop
+    from device import BBEngine
+    one = BBEngine(full['A'], b, sizes, options={'max_iter': 7, 'opt_tol': 1e-30}, fmt='tiles')
+    one.solve(poll=30)
+    s1 = one.scalars()
+    assert s1[0] == 2 and s1[1] == 7
+    assert elem_err(s0[5:9], s1[5:9]) < 1e-8, (s0[5:9], s1[5:9])
+
+
+# ---- convergence to the reference's own exit ---------------------------------
+
+def _run_exit(rank, world, port, out_q, path):
+    _setup(rank, world, port)
+    import torch
+    from distributed import partition_blocks
+    P = np.load(path)
+    import scipy.sparse as sps
+    A = sps.csr_matrix((P['data'], P['indices'], P['indptr']), shape=tuple(P['shape']))
+    b, sizes, x0 = P['b'], P['sizes'], P['x0']
+    bounds = partition_blocks(sizes, sizes.astype(np.float64), world)
+    xst = np.concatenate(([0], np.cumsum(sizes)))
+    c0, c1 = xst[bounds[rank]], xst[bounds[rank + 1]]
+    A_g = A[:, c0:c1].tocsr()
+    sz_g = sizes[bounds[rank]:bounds[rank + 1]]
+    # main.py's options (gradient_descent.py:29-31); early exits on
+    eng = _engine(A_g, sz_g, b, x0[c0:c1], 300000, True, fmt='tiles')
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))   # x2z(particular_x0) = 0
+    drv, comm = _driver(eng, rank)
+    drv.prologue()
+    i = 0
+    while True:
+        drv.iterate(i + 1, 25)
+        i += 25
+        s = eng.scalars()
+        if s[0] != 0 or i >= 300000:
+            break
+    out_q.put((rank, dict(z=eng.current_z(int(s[2])).cpu().numpy().copy(), scal=s.copy(),
+                          groups=int(eng.A_til.img['ngroups']), role=int(eng.P.shard_role))))
+    _finish(comm)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('vi', [0, 1, 2])
+def test_native_driver_two_ranks_runs_to_exit(cuda, golden, tmp_path, vi):
+    import bsls_utils
+    from bsls_matrices import BSLSMatrices
+    from bsls_utils import particular_x0, block_sizes_to_N
+    G = golden('solvers.npz')
+    kw = [{}, {'alpha': 0.5}, {'A_sparse': 0.05}][vi]
+    np.random.seed(SEED)
+    fname = os.path.join(str(tmp_path), 'test_main.mat')
+    bsls_utils.generate_data(fname=fname, **kw)
+    bm = BSLSMatrices(fname=fname, full=True, L=True, OD=True, CP=True, LP=True, eq='CP',
+                      init=False)
+    bm.degree_reduced_form()
+    AA, bb, N, sizes, x_split, nz, scaling, rsort_index, x0 = bm.get_LS()
+    sizes = np.asarray(sizes, dtype=np.int64)
+    assert np.array_equal(x0, particular_x0(sizes))
+    import scipy.sparse as sps
+    A = sps.csr_matrix(AA)
+    path = os.path.join(str(tmp_path), 'prob.npz')
+    np.savez(path, data=A.data, indices=A.indices, indptr=A.indptr, shape=np.array(A.shape),
+             b=np.asarray(bb, dtype=np.float64), sizes=sizes, x0=np.asarray(x0, dtype=np.float64))
+    res = _spawn(_run_exit, 2, path)
+    s0, s1 = res[0][0]['scal'], res[1][0]['scal']
+    for r in (0, 1):
+        assert res[r][0]['groups'] > 1 and res[r][0]['role'] == (1 if r == 0 else 2)
+    # both ranks decide alike: same reason, same iteration
+    assert s0[0] != 0 and s0[0] == s1[0] and s0[1] == s1[1], (s0[:3], s1[:3])
+    it = int(s0[1])
+    z = np.concatenate([res[0][0]['z'], res[1][0]['z']])
+    x = x0 + block_sizes_to_N(sizes).dot(z)
+    err = 0.5 * float(np.sum((A.dot(x) - bb) ** 2))
+    assert err < 1e-16, err                                # tests/fast/test_main.py:31-47
+    ref_it = int(G['main%d_iters' % vi][-1])               # 454 / 569 / 745
+    assert abs(it - ref_it) <= max(10, ref_it // 16), (it, ref_it)
