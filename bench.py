@@ -42,7 +42,7 @@ import numpy as np  # noqa: E402
 
 # BASELINE.json's metric text, verbatim; `value` is its 1M-route (C3) rate
 METRIC = 'BB solver iterations/sec (1M-route block-LSQ) + proj_simplex HBM GB/s'
-ROUND = 'r04'
+ROUND = 'r05'
 HBM_PEAK = 8.0e12   # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -630,11 +630,15 @@ def build_problem(name, world, rank, dist, shard_of=None):
     return sh, b
 
 
-def build_engine(sh, b, world, dist, parts, sharded=False, slices=None):
+def build_engine(sh, b, world, dist, parts, sharded=False, slices=None, model=None):
     """(engine, run(first, count)) for one rank: the fused single-GPU loop, or
     the column-sharded stages with the RCCL all-reduces (distributed.ShardedBB;
     `sharded` forces them at world 1 -- the per-rank host and launch path of
-    an N-GPU run, rehearsed on one GPU)."""
+    an N-GPU run, rehearsed on one GPU).  parts > 1: the exchange pipelined
+    behind both walks (link parts, bsls_bb_shard_iterate_parts).  model
+    (us_per_mb, fixed_us), rehearsal only: every exchange a spin of that cost
+    on its stream instead of the skipped one-rank collectives
+    (distributed.ModelComm) -- how much of such an exchange the schedule hides."""
     import torch
     from device import BBEngine
     opts = {'max_iter': 10 ** 12, 'opt_tol': 1e-30}
@@ -647,7 +651,8 @@ def build_engine(sh, b, world, dist, parts, sharded=False, slices=None):
     from distributed import ShardedBB, torch_all_reduce, torch_all_reduce_async
     eng = BBEngine(sh['A'], None, sh['block_sizes'], options=opts, early_exit=False,
                    AT=sh['AT'], colv=sh.get('colv'),
-                   target=torch.zeros(sh['m'], dtype=torch.float64))
+                   target=torch.zeros(sh['m'], dtype=torch.float64),
+                   link_parts=parts if parts > 1 else None)
     # target = sum_g A_g x0_g - b (main.py:48 over the shards)
     eng.x.copy_(eng.colv * eng.x0 if eng.scaled else eng.x0)
     eng.stage(1, 0)
@@ -657,7 +662,10 @@ def build_engine(sh, b, world, dist, parts, sharded=False, slices=None):
     # the schedule enqueued from C++ with RCCL in the loop (BSLS_SHARD_NATIVE=0:
     # the Python loop over torch.distributed, for A/B)
     comm = None
-    if os.environ.get('BSLS_SHARD_NATIVE', '1') != '0' and dist.get_backend() == 'nccl':
+    if model is not None and world == 1:
+        from distributed import ModelComm
+        comm = ModelComm(slices or 1, 0, fixed_us=model[1], us_per_mb=model[0])
+    elif os.environ.get('BSLS_SHARD_NATIVE', '1') != '0' and dist.get_backend() == 'nccl':
         from distributed import RcclComm
         comm = RcclComm()
     drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
@@ -852,6 +860,9 @@ def main():
                     help='comma list of %s (N = 1; default all): one rocprofv3 run per leg '
                          'keeps each workload\'s kernel rows apart' % ','.join(LEGS))
     ap.add_argument('--profile-iters', type=int, default=20)
+    ap.add_argument('--model-exchange', default=None,
+                    help='US_PER_MB[,FIXED_US]: with --rehearse-shard, model every exchange '
+                         'as a spin of that cost on its stream (timing only)')
     ap.add_argument('--windows', type=int, default=10,
                     help='timed windows of --steps iterations each; the line reports the '
                          'median window and the spread')
@@ -937,8 +948,12 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
         log('%s shard %d/%d: %d routes, %d blocks, %d links, %d nnz'
             % (wl, rank, world, sh['n'], sh['p'], sh['m'],
                sh['nnz'] if 'nnz' in sh else sh['A'].nnz))
+        model = None
+        if shard_of and args.model_exchange:
+            v = [float(a) for a in args.model_exchange.split(',')]
+            model = (v[0], v[1] if len(v) > 1 else 0.0)
         eng, run = build_engine(sh, b, world, dist, args.parts, sharded=bool(shard_of),
-                                slices=shard_of)
+                                slices=shard_of, model=model)
     log('engine up (K1 %s, K2 %s)' % (eng.fmt_A, eng.fmt_AT))
     els = time_run(run, steps, args.warmup, dist, windows=args.windows)
     el = float(np.median(els))
@@ -1009,6 +1024,11 @@ def bench_workload(wl, args, world, rank, dist, tfile, steps, shard_of=None):
                                           '(||r||^2 over its 1/%d slice), the collectives of a '
                                           'one-rank communicator skipped -- per-rank compute, '
                                           'no fabric' % (shard_of, shard_of))
+            if args.model_exchange:
+                res['config']['rehearsal'] += (
+                    '; every exchange modelled as a spin of %s (us per MB[, fixed us]) on its '
+                    'stream, %d link part(s)' % (args.model_exchange, args.parts))
+            res['config']['link_parts'] = args.parts
     if getattr(eng, '_comm', None) is not None:
         torch.cuda.synchronize()
         eng._comm.close()

@@ -83,7 +83,7 @@ class BBProblem(ctypes.Structure):
                 ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz),
                 ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp),
                 ('colv_n', _vp), ('colv_codec', _i64), ('rr_lo', _i64), ('rr_hi', _i64),
-                ('pava_warm', _i64), ('k1_atomic', _i64), ('k3_merge', _i64)]
+                ('pava_warm', _i64), ('k1_atomic', _i64), ('k3_merge', _i64), ('r_fx', _dbl)]
 
 
 class DoreState(ctypes.Structure):
@@ -201,6 +201,11 @@ _SIGS = {
     'bsls_comm_destroy': (_int, [_vp]),
     'bsls_comm_all_reduce': (_int, [_vp, _vp, _i64, _vp]),
     'bsls_bb_shard_iterate': (_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp]),
+    'bsls_bb_k2_part': (_int, [ctypes.POINTER(BBProblem), _i64, _int, _vp]),
+    'bsls_bb_k1_rows': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _i64, _vp]),
+    'bsls_bb_shard_iterate_parts': (_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp,
+                                           _vp, _vp]),
+    'bsls_comm_create_model': (_int, [_int, _int, _dbl, _dbl, ctypes.POINTER(_vp)]),
     'bsls_bb_row_blocks': (_i64, [ctypes.POINTER(BBProblem), _vp]),
     'bsls_bb_residual_rows': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _i64, _vp]),
     'bsls_md_update_gated': (_int, [_vp, _vp, _vp, _i64, _i64, _dbl, _dbl, _i64, _vp, _vp, _sz,

@@ -140,6 +140,16 @@ __device__ __forceinline__ void bb_record_f(const bsls_bb_problem &P, int64_t it
     }
 }
 
+// A column shard's r in 64-bit fixed point (bsls_bb_problem.r_fx > 0): the
+// stored word is the int64 llrint(r * r_fx).  r_fx_of(v): v as that word.
+__device__ __forceinline__ double r_fx_of(const bsls_bb_problem &P, double v) {
+    return __longlong_as_double(__double2ll_rn(v * P.r_fx));
+}
+__device__ __forceinline__ double r_load(const bsls_bb_problem &P, int64_t i) {
+    if (P.r_fx > 0.0) return (double)__double_as_longlong(P.r[i]) * (1.0 / P.r_fx);
+    return P.r[i];
+}
+
 // A column-sharded rank other than the one adding target (shard_role 2)
 // writes r = 0 for its rows once the run has stopped: its K1 no longer forms a
 // partial, and the all-reduce must leave the final residual (held by the
@@ -318,7 +328,10 @@ __global__ __launch_bounds__(256) void bb_k1_init(bsls_bb_problem P, int64_t r0,
         k1_stopped_rows(P, r0, r1, t0, gs);
         return;
     }
-    for (int64_t row = r0 + t0; row < r1; row += gs) P.r[row] = ADD ? P.target[row] : 0.0;
+    for (int64_t row = r0 + t0; row < r1; row += gs) {
+        const double v = ADD ? P.target[row] : 0.0;
+        P.r[row] = (P.r_fx > 0.0) ? r_fx_of(P, v) : v;
+    }
 }
 
 // K1 on a tile image (tiles.hpp): workgroup (rb, g) sums its rows over group
@@ -359,8 +372,15 @@ __global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, 
         // r was set to target / 0 by bb_k1_init: every group adds its sums
         // (global f64 atomics; the order over groups varies run to run, as the
         // dealt walk's LDS sums do)
-        for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
-            unsafeAtomicAdd(&P.r[row], lds[row - r0]);
+        // (r_fx: the sums as int64 words, added as integers -- order-free)
+        if (P.r_fx > 0.0) {
+            for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+                atomicAdd(reinterpret_cast<unsigned long long *>(&P.r[row]),
+                          (unsigned long long)__double2ll_rn(lds[row - r0] * P.r_fx));
+        } else {
+            for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+                unsafeAtomicAdd(&P.r[row], lds[row - r0]);
+        }
         return;
     }
     if (BSLS_K1_SPLIT) {
@@ -419,21 +439,35 @@ __device__ __forceinline__ void k2_stopped_sums(const bsls_bb_problem &P) {
         for (int q = 0; q < (FUSE == 2 ? 5 : 4); ++q) P.scal[BSLS_S_SUMDG + q] = 0.0;
 }
 
+// gsel >= 0 (bsls_bb_k2_part): only column group gsel, one workgroup per row
+// block -- the link-part pipeline of the sharded schedule launches the groups
+// one by one, each as soon as its rows of r are all-reduced.  The launches
+// are ordered on one stream, so the roles are fixed: groups < G - 1 leave
+// their partial row sums (and r^2 slices) in wpart and return; the last group
+// adds them in group order and runs the epilogue -- no tickets.  Its slice of
+// ||r||^2 stays inside its own link range (rows of r the earlier parts'
+// exchanges have not finished may not be read).
 template <int MODE, bool ITER, int FUSE = 0, int CV = 0>
 __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *__restrict__ dzv,
                                                const double *__restrict__ gp,
                                                double *__restrict__ gout, double *part,
-                                               unsigned *ticket, unsigned *tk2rb, int64_t iter) {
+                                               unsigned *ticket, unsigned *tk2rb, int64_t iter,
+                                               int gsel) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ double red[5 * 16];
     __shared__ int row_last;
     if (ITER && P.scal[BSLS_S_STOP] != 0.0) {
-        k2_stopped_sums<FUSE>(P);
+        if (gsel < 0 || gsel == P.ATt.ngroups - 1) k2_stopped_sums<FUSE>(P);
         return;
     }
     const bsls_tiles &T = P.ATt;
     int64_t rb, g;
-    tile_map(T, blockIdx.x, T.nrb, rb, g);
+    if (gsel >= 0) {
+        rb = blockIdx.x;
+        g = gsel;
+    } else {
+        tile_map(T, blockIdx.x, T.nrb, rb, g);
+    }
     const int HR = (int)tile_lds_doubles(T, false);
     double *rows = lds;
     double *rc = lds + HR;
@@ -449,14 +483,22 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
             constexpr int RR = 4;
             const int64_t ns = T.nrb * G, sl = rb * G + g;
             const bool cut = FUSE == 2 && P.rr_hi > P.rr_lo;
-            const int64_t lo = cut ? P.rr_lo : 0, span = (cut ? P.rr_hi : P.m) - lo;
-            const int64_t q0 = lo + sl * span / ns, q1 = lo + (sl + 1) * span / ns;
+            int64_t lo = cut ? P.rr_lo : 0, span = (cut ? P.rr_hi : P.m) - lo;
+            int64_t q0 = lo + sl * span / ns, q1 = lo + (sl + 1) * span / ns;
+            if (gsel >= 0) {
+                // this part's link range, cut to the rank's slice, over the row blocks
+                const int64_t a = T.group_col[g] > lo ? T.group_col[g] : lo;
+                const int64_t b = T.group_col[g + 1] < lo + span ? T.group_col[g + 1] : lo + span;
+                const int64_t w = b > a ? b - a : 0;
+                q0 = a + rb * w / T.nrb;
+                q1 = a + (rb + 1) * w / T.nrb;
+            }
             for (int64_t i0 = q0 + threadIdx.x; i0 < q1; i0 += RR * (int64_t)blockDim.x) {
                 double v[RR];
 #pragma unroll
                 for (int q = 0; q < RR; ++q) {
                     const int64_t i = i0 + (int64_t)q * blockDim.x;
-                    v[q] = (i < q1) ? P.r[i] : 0.0;
+                    v[q] = (i < q1) ? r_load(P, i) : 0.0;
                 }
 #pragma unroll
                 for (int q = 0; q < RR; ++q) rr[0] += v[q] * v[q];
@@ -468,7 +510,11 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
         if (MODE == 2) rc[i] = (i < nloc) ? colv_t<CV>(P, i0 + i) : 0.0;
     }
     __syncthreads();
-    tile_walk_any<(MODE == 3 ? 0 : MODE)>(T, rb, g, P.r, rows, rc);
+    if (P.r_fx > 0.0)
+        tile_walk_any<(MODE == 3 ? 0 : MODE), false, true>(T, rb, g, P.r, rows, rc, 1.0,
+                                                            1.0 / P.r_fx);
+    else
+        tile_walk_any<(MODE == 3 ? 0 : MODE)>(T, rb, g, P.r, rows, rc);
     __syncthreads();
     // wpart's tail: one slot per (group, row block) for the slices' r^2 sums
     double *rrp = P.wpart + G * T.nrb * (T.H + 1);
@@ -483,7 +529,23 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     // one product per row (the sums' order is not fixed anyway), formed in the
     // epilogue below; several groups: by the finishing workgroup
     const bool scale_epi = MODE == 3 && G == 1;
-    if (G > 1) {
+    if (G > 1 && gsel >= 0) {
+        // the part pipeline: fixed roles (see above)
+        if (gsel < G - 1) {
+            double *wp = P.wpart + (g * T.nrb + rb) * (T.H + 1);
+            for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x) wp[i] = rows[i];
+            return;
+        }
+        for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x) {
+            double o = 0.0;
+            for (int64_t c = 0; c < G - 1; ++c)
+                o += __hip_atomic_load(&P.wpart[(c * T.nrb + rb) * (T.H + 1) + i], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            o += rows[i];
+            rows[i] = (MODE == 3) ? colv_t<CV>(P, i0 + i) * o : o;
+        }
+        __syncthreads();
+    } else if (G > 1) {
         double *wp = P.wpart + (g * T.nrb + rb) * (T.H + 1);
         for (int64_t i = threadIdx.x; i < nloc; i += blockDim.x)
             __hip_atomic_store(&wp[i], rows[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -642,10 +704,10 @@ __global__ __launch_bounds__(256) void bb_r_finish(bsls_bb_problem P, int64_t it
     const int64_t gs = (int64_t)gridDim.x * blockDim.x;
     double sq[1] = {0.0};
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.m; i += gs) {
-        double o = P.r[i];
+        double o = r_load(P, i);
         if (add_target) {
             o += P.target[i];
-            P.r[i] = o;
+            P.r[i] = (P.r_fx > 0.0) ? r_fx_of(P, o) : o;
         }
         sq[0] += o * o;
     }
@@ -860,7 +922,10 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
             return;
         }
         const bool add = P.shard_role == 1;
-        for (int64_t row = t0; row < P.m; row += gs) P.r[row] = add ? P.target[row] : 0.0;
+        for (int64_t row = t0; row < P.m; row += gs) {
+            const double v = add ? P.target[row] : 0.0;
+            P.r[row] = (P.r_fx > 0.0) ? r_fx_of(P, v) : v;
+        }
     };
     // rec (stage 13, the sliced sharded schedule): stage 12 folded in -- f and
     // the stopping test of iter - 1 from the all-reduced scal[RR] and the kept
@@ -1185,33 +1250,35 @@ static void launch_k2_mode(const bsls_bb_problem &P, const double *gp, double *g
 
 template <int MODE, bool ITER, int FUSE, int CV>
 static void launch_k2t_cv(const bsls_bb_problem &P, const double *gp, double *gout,
-                          const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
+                          const BBWork &w, hipStream_t st, int64_t iter, const double *dz,
+                          int gsel) {
     allow_lds(bb_k2t<MODE, ITER, FUSE, CV>);
-    bb_k2t<MODE, ITER, FUSE, CV><<<(int)(P.ATt.nrb * P.ATt.ngroups), BSLS_TILE_THREADS,
-                                   tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(
-        P, dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter);
+    bb_k2t<MODE, ITER, FUSE, CV><<<(int)(gsel >= 0 ? P.ATt.nrb : P.ATt.nrb * P.ATt.ngroups),
+                                   BSLS_TILE_THREADS, tile_lds_doubles(P.ATt, MODE == 2) * 8, st>>>(
+        P, dz, gp, gout, w.p2, w.tk2, w.tk2rb, iter, gsel);
 }
 
 template <int MODE, bool ITER, int FUSE>
 static void launch_k2t_mode(const bsls_bb_problem &P, const double *gp, double *gout,
-                            const BBWork &w, hipStream_t st, int64_t iter, const double *dz) {
+                            const BBWork &w, hipStream_t st, int64_t iter, const double *dz,
+                            int gsel) {
     if (MODE != 1 && P.colv_codec == 2)
-        launch_k2t_cv<MODE, ITER, FUSE, 2>(P, gp, gout, w, st, iter, dz);
+        launch_k2t_cv<MODE, ITER, FUSE, 2>(P, gp, gout, w, st, iter, dz, gsel);
     else if (MODE != 1 && P.colv_codec == 1)
-        launch_k2t_cv<MODE, ITER, FUSE, 1>(P, gp, gout, w, st, iter, dz);
-    else launch_k2t_cv<MODE, ITER, FUSE, 0>(P, gp, gout, w, st, iter, dz);
+        launch_k2t_cv<MODE, ITER, FUSE, 1>(P, gp, gout, w, st, iter, dz, gsel);
+    else launch_k2t_cv<MODE, ITER, FUSE, 0>(P, gp, gout, w, st, iter, dz, gsel);
 }
 
 template <bool ITER, int FUSE = 0>
 static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
                       const BBWork &w, hipStream_t st, int64_t iter = 0,
-                      const double *dz = nullptr) {
+                      const double *dz = nullptr, int gsel = -1) {
     if (!dz) dz = w.dz;
     if (P.ATt.ent) {
-        if (!P.colv) launch_k2t_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
+        if (!P.colv) launch_k2t_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter, dz, gsel);
         else if (P.ATt.ngroups == 1 && P.ATt.layout == 0)
-            launch_k2t_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
-        else launch_k2t_mode<3, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
+            launch_k2t_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter, dz, gsel);
+        else launch_k2t_mode<3, ITER, FUSE>(P, gp, gout, w, st, iter, dz, gsel);
     } else if (P.colv) {
         launch_k2_mode<2, ITER, FUSE>(P, gp, gout, w, st, iter, dz);
     } else {
@@ -1273,6 +1340,11 @@ static int check_problem(const bsls_bb_problem *p) {
     if (!p || p->m <= 0 || p->n <= 0 || p->nblocks <= 0 || p->nz != p->n - p->nblocks) return BSLS_E_ARG;
     if (p->shard_role < 0 || p->shard_role > 2) return BSLS_E_ARG;
     if (p->k1_atomic < 0 || p->k1_atomic > 2 || p->k3_merge < 0 || p->k3_merge > 2)
+        return BSLS_E_ARG;
+    // the fixed-point r: every writer of r is the atomic K1 (+ its init) and
+    // every K2 reader the dealt walk
+    if (!(p->r_fx >= 0.0) || p->r_fx > 1e300) return BSLS_E_ARG;
+    if (p->r_fx > 0.0 && !(k1_init_folded(*p) && p->ATt.ent && (p->ATt.layout & 3) != 0))
         return BSLS_E_ARG;
     if (p->colv_codec < 0 || p->colv_codec > 2 || (p->colv_codec && (!p->colv_n || !p->colv)))
         return BSLS_E_ARG;
@@ -1851,5 +1923,39 @@ extern "C" int bsls_bb_iterate(const bsls_bb_problem *p, int64_t first_iter, int
         launch_k1<true, true, true>(P, i, w, st);
         BSLS_LAUNCH_CHECK();
     }
+    return BSLS_OK;
+}
+
+// ---- the link-part pipeline of the column-sharded schedule -------------------
+// (include/bsls_hip.h bsls_bb_k2_part / bsls_bb_k1_rows; csrc/shard.hip
+// bsls_bb_shard_iterate_parts drives them with the exchange of each part's
+// rows of r on a second stream)
+extern "C" int bsls_bb_k2_part(const bsls_bb_problem *p, int64_t iter, int part, void *stream) {
+    const int rc = check_problem(p);
+    if (rc != BSLS_OK) return rc;
+    const bsls_bb_problem &P = *p;
+    if (iter <= 0 || !P.ATt.ent || (P.ATt.layout & 3) == 0 || P.ATt.ngroups < 2 || part < 0 ||
+        part >= P.ATt.ngroups || !P.wpart)
+        return BSLS_E_ARG;
+    if (P.rr_lo < 0 || P.rr_hi > P.m || P.rr_lo > P.rr_hi) return BSLS_E_ARG;
+    const BBWork w = bb_layout(P);
+    const int zc = (int)((iter - 1) & 1), zn = (int)(iter & 1);
+    launch_k2<true, 2>(P, P.g[zc], P.g[zn], w, (hipStream_t)stream, iter, nullptr, part);
+    BSLS_LAUNCH_CHECK();
+    return BSLS_OK;
+}
+
+extern "C" int bsls_bb_k1_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
+                               void *stream) {
+    const int rc = check_problem(p);
+    if (rc != BSLS_OK) return rc;
+    const bsls_bb_problem &P = *p;
+    if (iter <= 0 || rb0 < 0 || rb1 <= rb0 || rb1 > k1_row_blocks(P)) return BSLS_E_ARG;
+    const BBWork w = bb_layout(P);
+    hipStream_t st = (hipStream_t)stream;
+    const bool folded = k1_init_folded(P);
+    if (P.shard_role == 1) launch_k1<true, false, true>(P, iter, w, st, rb0, rb1, folded);
+    else launch_k1<false, false, true>(P, iter, w, st, rb0, rb1, folded);
+    BSLS_LAUNCH_CHECK();
     return BSLS_OK;
 }

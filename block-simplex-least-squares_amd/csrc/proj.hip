@@ -1108,15 +1108,17 @@ __device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_
 }
 
 // One wave: PIPE_G consecutive groups, straight-line (unrolled at compile
-// time): the starts of all of them first, then per group h the entries of
-// group h + 1 are loaded before the passes on group h (whose entries were
-// loaded one step earlier) and its stores.  Straight-line code keeps the
-// compiler's vmcnt waits exact -- a persistent loop merged its states at the
-// loop head and waited for the next group's loads before the compute -- and
-// every memory operation is unconditional: a group past the last is a
-// clamped copy with k = 0, whose stores the hardware drops.
+// time): the starts of all of them in one load, then the entries of every
+// group, then the passes and stores group by group -- so a wave has all its
+// bytes in flight at once and computes on the first group while the others
+// land (round 5, measured at C2: one group ahead per step was slower than no
+// pipelining at all, 23.9 against 19.1 us -- what the kernel is short of is
+// bytes in flight per CU, not overlap inside a wave).  Straight-line code keeps
+// the compiler's vmcnt waits exact; every memory operation is unconditional:
+// a group past the last is a clamped copy with k = 0, whose stores the
+// hardware drops.
 template <bool BALL, bool BIG, int PIPE_G>
-__global__ __launch_bounds__(256, 4) void proj_pipe_kernel(double *__restrict__ y,
+__global__ __launch_bounds__(256, 2) void proj_pipe_kernel(double *__restrict__ y,
                                                           const int64_t *__restrict__ starts,
                                                           int64_t nb, int64_t n,
                                                           int64_t *__restrict__ big_list,
@@ -1135,22 +1137,18 @@ __global__ __launch_bounds__(256, 4) void proj_pipe_kernel(double *__restrict__ 
     asm volatile("" ::: "memory");
     PipeGroup P[PIPE_G];
     double v[PIPE_G][PIPE_EB];
-    P[0] = pipe_setup<BIG>(y, st[0], q0, nb, big_list, big_count, true, lane);
-    pipe_load(P[0], v[0]);
 #pragma unroll
     for (int h = 0; h < PIPE_G; ++h) {
-        if (h + 1 < PIPE_G) {
-            const int64_t q = q0 + h + 1;
-            const bool real = q < ngrp;
-            P[h + 1] = pipe_setup<BIG>(y, st[h + 1], real ? q : ngrp - 1, nb, big_list, big_count,
-                                       real, lane);
-            if (!real) P[h + 1].k = 0;
-            pipe_load(P[h + 1], v[h + 1]);
-        }
-        // (keeps the compiler from sinking those loads past the passes)
-        asm volatile("" ::: "memory");
-        pipe_solve<BALL>(P[h], v[h], j);
+        const int64_t q = q0 + h;
+        const bool real = q < ngrp;
+        P[h] = pipe_setup<BIG>(y, st[h], real ? q : ngrp - 1, nb, big_list, big_count, real, lane);
+        if (!real) P[h].k = 0;
+        pipe_load(P[h], v[h]);
     }
+    // (keeps the compiler from sinking those loads past the passes)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < PIPE_G; ++h) pipe_solve<BALL>(P[h], v[h], j);
 }
 
 struct ProjWork {
@@ -1223,8 +1221,8 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
     // A/B; 0 = the lane-per-block Michelot form below)
     static const int pipe = [] {
         const char *e = getenv("BSLS_PROJ_PIPE");
-        const int v = e ? atoi(e) : 4;
-        return (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
+        const int v = e ? atoi(e) : 1;
+        return (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) ? v : 1;
     }();
     const int64_t ngrp = (nb + WAVE - 1) / WAVE;
     // (its group ranges must stay below 2 GB of y: max_block bounds them)

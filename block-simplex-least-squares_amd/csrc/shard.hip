@@ -29,6 +29,10 @@
 #include "bsls_common.hpp"
 
 extern "C" int bsls_bb_stage(const bsls_bb_problem *p, int stage, int64_t iter, void *stream);
+extern "C" int bsls_bb_k2_part(const bsls_bb_problem *p, int64_t iter, int part, void *stream);
+extern "C" int bsls_bb_k1_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
+                               void *stream);
+extern "C" int64_t bsls_bb_row_blocks(const bsls_bb_problem *p, int64_t *rows_per_block);
 
 namespace bsls {
 
@@ -63,12 +67,29 @@ static const RcclApi &rccl() {
 
 using namespace bsls;
 
+constexpr int MAX_PARTS = 16;
+
 struct bsls_comm {
     ncclComm_t comm;
     int world, rank;
     bsls_all_reduce_fn fn;   // set: the host callback replaces RCCL
     void *user;
+    // a modelled exchange (bsls_comm_create_model): no data moves, a spin
+    // kernel of fixed_us + us_per_mb per MB holds the stream instead
+    bool model;
+    double fixed_us, us_per_mb;
+    // the part pipeline's events (created on first use)
+    bool events;
+    hipEvent_t ev_k1[MAX_PARTS], ev_ar[MAX_PARTS];
 };
+
+namespace bsls {
+// one wave sleeping until `ticks` of the constant wall clock have passed
+__global__ void comm_model_spin(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+}  // namespace bsls
 
 // RCCL failures map to BSLS_E_COMM - ncclResult (distinct from hip errors)
 static int comm_rc(ncclResult_t r) { return r == ncclSuccess ? BSLS_OK : BSLS_E_COMM - (int)r; }
@@ -91,7 +112,9 @@ extern "C" int bsls_comm_create(const void *id, int world, int rank, bsls_comm *
     if (!R.ok) return BSLS_E_COMM;
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
-    bsls_comm *c = new bsls_comm{nullptr, world, rank, nullptr, nullptr};
+    bsls_comm *c = new bsls_comm{};
+    c->world = world;
+    c->rank = rank;
     const int rc = comm_rc(R.init(&c->comm, world, uid, rank));
     if (rc != BSLS_OK) {
         delete c;
@@ -104,21 +127,61 @@ extern "C" int bsls_comm_create(const void *id, int world, int rank, bsls_comm *
 extern "C" int bsls_comm_create_callback(int world, int rank, bsls_all_reduce_fn fn, void *user,
                                          bsls_comm **out) {
     if (!fn || !out || world < 1 || rank < 0 || rank >= world) return BSLS_E_ARG;
-    *out = new bsls_comm{nullptr, world, rank, fn, user};
+    bsls_comm *c = new bsls_comm{};
+    c->world = world;
+    c->rank = rank;
+    c->fn = fn;
+    c->user = user;
+    *out = c;
+    return BSLS_OK;
+}
+
+extern "C" int bsls_comm_create_model(int world, int rank, double fixed_us, double us_per_mb,
+                                      bsls_comm **out) {
+    if (!out || world < 1 || rank < 0 || rank >= world || !(fixed_us >= 0.0) ||
+        !(us_per_mb >= 0.0))
+        return BSLS_E_ARG;
+    bsls_comm *c = new bsls_comm{};
+    c->world = world;
+    c->rank = rank;
+    c->model = true;
+    c->fixed_us = fixed_us;
+    c->us_per_mb = us_per_mb;
+    *out = c;
     return BSLS_OK;
 }
 
 extern "C" int bsls_comm_destroy(bsls_comm *c) {
     if (!c) return BSLS_OK;
-    const int rc = c->fn ? BSLS_OK : comm_rc(rccl().destroy(c->comm));
+    const int rc = (c->fn || c->model) ? BSLS_OK : comm_rc(rccl().destroy(c->comm));
+    if (c->events)
+        for (int q = 0; q < MAX_PARTS; ++q) {
+            (void)hipEventDestroy(c->ev_k1[q]);
+            (void)hipEventDestroy(c->ev_ar[q]);
+        }
     delete c;
     return rc;
 }
 
-// the one all-reduce of both transports: in place, sum, on `stream`
-static int comm_sum(bsls_comm *c, double *buf, size_t count, hipStream_t st) {
+// the one all-reduce of every transport: in place, sum, on `stream`; i64:
+// the words are int64 (a fixed-point r, bsls_bb_problem.r_fx: summed exactly)
+static int comm_sum(bsls_comm *c, double *buf, size_t count, hipStream_t st, bool i64 = false) {
     if (c->fn) return c->fn(buf, (int64_t)count, (void *)st, c->user) == 0 ? BSLS_OK : BSLS_E_COMM;
-    return comm_rc(rccl().all_reduce(buf, buf, count, ncclFloat64, ncclSum, c->comm, st));
+    if (c->model) {
+        static const double ticks_per_us = [] {
+            int dev = 0, khz = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+                khz <= 0)
+                khz = 100000;
+            return khz / 1000.0;
+        }();
+        const double us = c->fixed_us + c->us_per_mb * (double)count * 8.0 / 1e6;
+        comm_model_spin<<<1, 64, 0, st>>>((uint64_t)(us * ticks_per_us));
+        return hipGetLastError() == hipSuccess ? BSLS_OK : BSLS_E_COMM;
+    }
+    return comm_rc(rccl().all_reduce(buf, buf, count, i64 ? ncclInt64 : ncclFloat64, ncclSum,
+                                     c->comm, st));
 }
 
 extern "C" int bsls_comm_all_reduce(bsls_comm *c, double *buf, int64_t count, void *stream) {
@@ -158,9 +221,70 @@ extern "C" int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *c, int
         }
         // the partial residual, then r = the sum over ranks (the one real exchange)
         if ((rc = bsls_bb_stage(p, fuse == 2 ? 14 : 1, i, stream)) != BSLS_OK) return rc;
-        if ((rc = all_reduce(p->r, (size_t)p->m)) != BSLS_OK) return rc;
+        if (comm && (rc = comm_sum(c, p->r, (size_t)p->m, st, p->r_fx > 0.0)) != BSLS_OK)
+            return rc;
         if (!fuse && (rc = bsls_bb_stage(p, 9, i, stream)) != BSLS_OK) return rc;
     }
     if (count > 0 && fuse) return bsls_bb_stage(p, 9, first_iter + count - 1, stream);
+    return BSLS_OK;
+}
+
+// The link-part pipeline (include/bsls_hip.h): K1 by row-block parts, each
+// part's rows of r all-reduced on `comm_stream` as soon as the part is done,
+// the next iteration's K2 by the matching column groups, each waiting only
+// for its own part's exchange -- so part q's exchange runs under K1's later
+// parts and K2's earlier ones instead of after the whole walk.
+extern "C" int bsls_bb_shard_iterate_parts(const bsls_bb_problem *p, bsls_comm *c,
+                                           int64_t first_iter, int64_t count, int nparts,
+                                           const int64_t *rb_bounds, void *comm_stream,
+                                           void *stream) {
+    if (!p || !c || !rb_bounds || first_iter < 1 || count < 0 || nparts < 2 ||
+        nparts > MAX_PARTS || !comm_stream || comm_stream == stream)
+        return BSLS_E_ARG;
+    if (p->shard_role != (c->rank == 0 ? 1 : 2)) return BSLS_E_ARG;
+    if (p->ATt.ngroups != nparts || !p->ATt.ent) return BSLS_E_ARG;
+    int64_t R = 0;
+    const int64_t nrb = bsls_bb_row_blocks(p, &R);
+    if (nrb < 0) return (int)nrb;
+    if (rb_bounds[0] != 0 || rb_bounds[nparts] != nrb) return BSLS_E_ARG;
+    for (int q = 0; q < nparts; ++q)
+        if (rb_bounds[q + 1] <= rb_bounds[q]) return BSLS_E_ARG;
+    if (!c->events) {
+        for (int q = 0; q < MAX_PARTS; ++q) {
+            BSLS_CHECK(hipEventCreateWithFlags(&c->ev_k1[q], hipEventDisableTiming));
+            BSLS_CHECK(hipEventCreateWithFlags(&c->ev_ar[q], hipEventDisableTiming));
+        }
+        c->events = true;
+    }
+    hipStream_t st = (hipStream_t)stream, cs = (hipStream_t)comm_stream;
+    const bool comm = c->world > 1;
+    int rc;
+    for (int64_t i = first_iter; i < first_iter + count; ++i) {
+        // K2 by link parts: part q needs only its rows of r
+        for (int q = 0; q < nparts; ++q) {
+            if (comm && i > first_iter) BSLS_CHECK(hipStreamWaitEvent(st, c->ev_ar[q], 0));
+            if ((rc = bsls_bb_k2_part(p, i, q, stream)) != BSLS_OK) return rc;
+        }
+        if (comm && (rc = comm_sum(c, p->scal + BSLS_S_SUMDG, 5, st)) != BSLS_OK) return rc;
+        if ((rc = bsls_bb_stage(p, 15, i, stream)) != BSLS_OK) return rc;
+        // K1 by the same parts, each part's exchange started behind it
+        for (int q = 0; q < nparts; ++q) {
+            if ((rc = bsls_bb_k1_rows(p, i, rb_bounds[q], rb_bounds[q + 1], stream)) != BSLS_OK)
+                return rc;
+            if (!comm) continue;
+            const int64_t r0 = rb_bounds[q] * R;
+            const int64_t r1 = rb_bounds[q + 1] * R < p->m ? rb_bounds[q + 1] * R : p->m;
+            BSLS_CHECK(hipEventRecord(c->ev_k1[q], st));
+            BSLS_CHECK(hipStreamWaitEvent(cs, c->ev_k1[q], 0));
+            if ((rc = comm_sum(c, p->r + r0, (size_t)(r1 - r0), cs, p->r_fx > 0.0)) != BSLS_OK)
+                return rc;
+            BSLS_CHECK(hipEventRecord(c->ev_ar[q], cs));
+        }
+    }
+    if (count > 0) {
+        if (comm)
+            for (int q = 0; q < nparts; ++q) BSLS_CHECK(hipStreamWaitEvent(st, c->ev_ar[q], 0));
+        return bsls_bb_stage(p, 9, first_iter + count - 1, stream);
+    }
     return BSLS_OK;
 }

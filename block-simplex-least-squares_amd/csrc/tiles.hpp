@@ -249,11 +249,15 @@ __device__ __forceinline__ double fx_value(const double *rows, int lr, int lo_of
     return (double)hi * inv + (double)lo * inv_lo;
 }
 
+// FXIN: the gathered vector is in 64-bit fixed point (a column shard's r,
+// bsls_bb_problem.r_fx): each gathered word is an int64, its value that times
+// fxin (the inverse scale)
 template <int MODE, bool NT, bool PK3 = false, int VT = 0, int P = BSLS_TILE_P,
-          int D = BSLS_TILE_D, bool FX = false>
+          int D = BSLS_TILE_D, bool FX = false, bool FXIN = false>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
-                                                const double *rcol, double fxs = 1.0) {
+                                                const double *rcol, double fxs = 1.0,
+                                                double fxin = 1.0) {
     static_assert(D >= 1 && D < P, "gathers run ahead of the entry loads");
     if (BSLS_TILE_KO == 3) return;
     typedef typename TileEnt<PK3>::type ent_t;
@@ -298,6 +302,12 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
         o[3] = xb[b.w + (ent(u, 3) & cmask)];
         if (MODE == 1) tile_vals4<VT, NT>(T.val, v0 + q * 4096, w);
     };
+    // (FXIN: the int64 words to doubles where used, not where gathered, so
+    // the conversion does not wait on the gathers in flight)
+    auto gval = [&](double o) -> double {
+        if constexpr (FXIN) return (double)__double_as_longlong(o) * fxin;
+        else return o;
+    };
 #pragma unroll
     for (int d = 0; d < D; ++d)
         if (d < nq) gat(ring[d], bring[d], d, v[d], a[d]);
@@ -315,9 +325,9 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
                 for (int j = 0; j < 4; ++j) {
                     const int lr = (int)(ent(cur, j) >> cb);
                     double term;
-                    if (MODE == 0) term = v[0][j];
-                    else if (MODE == 1) term = a[0][j] * v[0][j];
-                    else term = rcol[lr] * v[0][j];
+                    if (MODE == 0) term = gval(v[0][j]);
+                    else if (MODE == 1) term = a[0][j] * gval(v[0][j]);
+                    else term = rcol[lr] * gval(v[0][j]);
 #if BSLS_TILE_KO == 1
                     rows[lr] += term;                 // (knock-out: racy plain add)
 #elif BSLS_TILE_KO == 2
@@ -341,35 +351,40 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
 }
 
 // the dealt walk with its value type (MODE 1 only: the other modes store none)
-template <int MODE, bool NT, bool PK3, bool FX = false>
+template <int MODE, bool NT, bool PK3, bool FX = false, bool FXIN = false>
 __device__ __forceinline__ void tile_walk_dealt_vt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                    const double *__restrict__ src, double *rows,
-                                                   const double *rcol, double fxs = 1.0) {
+                                                   const double *rcol, double fxs = 1.0,
+                                                   double fxin = 1.0) {
     constexpr int P = BSLS_TILE_P, D = BSLS_TILE_D;
     if constexpr (MODE == 1) {
         if (T.layout & BSLS_TILE_VAL16)
-            tile_walk_dealt<MODE, NT, PK3, 2, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
+            tile_walk_dealt<MODE, NT, PK3, 2, P, D, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
         else if (T.layout & BSLS_TILE_VAL32)
-            tile_walk_dealt<MODE, NT, PK3, 1, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
-        else tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
+            tile_walk_dealt<MODE, NT, PK3, 1, P, D, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
+        else
+            tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
     } else {
-        tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX>(T, rb, g, src, rows, rcol, fxs);
+        tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
     }
 }
 
-// the walk of either layout (FX: dealt layouts only)
-template <int MODE, bool FX = false>
+// the walk of either layout (FX, FXIN: dealt layouts only)
+template <int MODE, bool FX = false, bool FXIN = false>
 __device__ __forceinline__ void tile_walk_any(const bsls_tiles &T, int64_t rb, int64_t g,
                                               const double *__restrict__ src, double *rows,
-                                              const double *rcol, double fxs = 1.0) {
+                                              const double *rcol, double fxs = 1.0,
+                                              double fxin = 1.0) {
     const int64_t lay = T.layout & ~(int64_t)(BSLS_TILE_VAL32 | BSLS_TILE_VAL16);
-    if (lay == 1) tile_walk_dealt_vt<MODE, false, false, FX>(T, rb, g, src, rows, rcol, fxs);
+    if (lay == 1)
+        tile_walk_dealt_vt<MODE, false, false, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
     else if (lay == (1 | BSLS_TILE_NT))
-        tile_walk_dealt_vt<MODE, true, false, FX>(T, rb, g, src, rows, rcol, fxs);
-    else if (lay == 2) tile_walk_dealt_vt<MODE, false, true, FX>(T, rb, g, src, rows, rcol, fxs);
+        tile_walk_dealt_vt<MODE, true, false, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
+    else if (lay == 2)
+        tile_walk_dealt_vt<MODE, false, true, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
     else if (lay == (2 | BSLS_TILE_NT))
-        tile_walk_dealt_vt<MODE, true, true, FX>(T, rb, g, src, rows, rcol, fxs);
-    else if constexpr (!FX) tile_walk<MODE>(T, rb, g, src, rows, rcol);
+        tile_walk_dealt_vt<MODE, true, true, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
+    else if constexpr (!FX && !FXIN) tile_walk<MODE>(T, rb, g, src, rows, rcol);
 }
 
 // Host-side validation of a tile image against the matrix it claims to hold

@@ -496,7 +496,8 @@ def self_bytes(img):
 class DeviceTiles:
     """A tile image on the device + the ctypes struct pointing at it."""
 
-    def __init__(self, M, halo=0, values=True, colv_lds=False, plan=None, layout=0):
+    def __init__(self, M, halo=0, values=True, colv_lds=False, plan=None, layout=0,
+                 group_col=None):
         torch = _torch()
         M = sps.csr_matrix(M)
         M.sort_indices()
@@ -504,7 +505,15 @@ class DeviceTiles:
         H, G, order = plan or tile_plan(R, C, halo, colv_lds,
                                         env='BSLS_TILE_PLAN_AT' if halo else 'BSLS_TILE_PLAN_A',
                                         layout=layout, nnz=M.nnz)
-        gc = np.round(np.linspace(0, C, G + 1)).astype(np.int64)
+        if group_col is not None:
+            # the caller's column groups (the sharded K2's link parts, aligned
+            # with K1's row-block parts)
+            gc = np.asarray(group_col, dtype=np.int64)
+            G = gc.shape[0] - 1
+            if gc[0] != 0 or gc[-1] != C:
+                raise ValueError('column groups must cover [0, %d)' % C)
+        else:
+            gc = np.round(np.linspace(0, C, G + 1)).astype(np.int64)
         if np.any(np.diff(gc) < 1):
             raise ValueError('more column groups than columns')
         if layout in (1, 2):
@@ -876,7 +885,8 @@ class BBEngine:
 
     def __init__(self, A, b, block_sizes, options=None, early_exit=True, A_dev=None,
                  AT_dev=None, AT=None, target=None, x0=None, general=False, fmt=None,
-                 tile_plans=(None, None), colv=None, deterministic=False, tile_layouts=None):
+                 tile_plans=(None, None), colv=None, deterministic=False, tile_layouts=None,
+                 link_parts=None):
         torch = _torch()
         L = _native.lib()
         self.layout = lay = BlockLayout(block_sizes)
@@ -928,13 +938,34 @@ class BBEngine:
                                            values=not self.scaled)
             except PanelOverflow:
                 self.fmt_AT = 'tiles'
+        # link parts (the sharded schedule's exchange pipelined behind the
+        # walks, bsls_bb_shard_iterate_parts): K1's row blocks cut into
+        # `link_parts` runs, and K2's image in as many column groups over the
+        # same link ranges, so K2 part q reads only the rows of r part q's
+        # exchange delivered
+        self.k1_part_bounds = None
+        k2_gc = None
+        if link_parts is not None and int(link_parts) > 1:
+            if self.fmt_A != 'tiles' or self.fmt_AT != 'tiles' or tile_layouts[1] not in (1, 2):
+                raise ValueError('link parts need dealt tile images for K1 and K2')
+            from distributed import row_parts
+            nrb, H = self.A_til.img['nrb'], self.A_til.img['H']
+            self.k1_part_bounds = np.array(row_parts(nrb, int(link_parts)), dtype=np.int64)
+            if len(self.k1_part_bounds) - 1 != int(link_parts):
+                raise ValueError('%d link parts need as many K1 row blocks (%d)'
+                                 % (int(link_parts), nrb))
+            k2_gc = np.minimum(self.k1_part_bounds * H, self.m)
         if self.fmt_AT == 'tiles':
             # (the thread-stream K2 keeps each row's colv in LDS beside its sum:
             # every term colv_i * r_j, SciPy's product; the dealt K2 scales
             # the row sum once, so its LDS holds twice the rows)
+            plan_at = tile_plans[1]
+            if k2_gc is not None and plan_at is None:
+                H2, _, _ = tile_plan(self.n, self.m, 1, False, layout=tile_layouts[1], nnz=AT.nnz)
+                plan_at = (H2, len(k2_gc) - 1, 0)
             self.AT_til = DeviceTiles(AT, 1, values=not self.scaled,
                                       colv_lds=self.scaled and tile_layouts[1] == 0,
-                                      plan=tile_plans[1], layout=tile_layouts[1])
+                                      plan=plan_at, layout=tile_layouts[1], group_col=k2_gc)
         opts = options or {}
         self.options = dict(opts)
         dev = dict(dtype=torch.float64, device='cuda')
@@ -1082,6 +1113,41 @@ class BBEngine:
             raise ValueError('slice out of range')
         self.P.rr_lo, self.P.rr_hi = int(lo), int(hi)
 
+    def fixed_r_ok(self):
+        """Whether this column shard can keep r in 64-bit fixed point
+        (bsls_bb_problem.r_fx): its K1 adds its column groups' sums by
+        atomics with the init folded into K3 (a dealt K1 image of several
+        groups on shard_role 1 / 2) and its K2 walks a dealt image."""
+        P = self.P
+        atomic = (P.k1_atomic == 2) if P.k1_atomic else P.shard_role != 0
+        return bool(self.A_til is not None and self.A_til.img['ngroups'] > 1 and atomic
+                    and self.AT_til is not None and self.tile_layouts[1] in (1, 2)
+                    and P.shard_role != 0)
+
+    def set_r_fixed(self, scale):
+        """r in 64-bit fixed point at `scale` (a power of two; 0: doubles):
+        the atomic K1's group sums then add as integers (order-free) and the
+        r exchange sums int64 words (exact) -- the same r bits however the
+        groups and ranks land.  Every |partial sum of r| must stay below
+        2^62 / scale (distributed.ShardedBB sizes it)."""
+        scale = float(scale)
+        if scale < 0 or (scale > 0 and not self.fixed_r_ok()):
+            raise ValueError('fixed-point r needs an atomic sharded K1 (fixed_r_ok)')
+        self.P.r_fx = scale
+
+    @property
+    def r_exchange(self):
+        """r as the exchange sums it: int64 words under a fixed-point r."""
+        torch = _torch()
+        return self.r.view(torch.int64) if self.P.r_fx > 0 else self.r
+
+    def residual_value(self):
+        """r as doubles (a copy), whatever its representation."""
+        torch = _torch()
+        if self.P.r_fx > 0:
+            return self.r.view(torch.int64).to(torch.float64) / self.P.r_fx
+        return self.r.clone()
+
     def set_shard_role(self, role):
         """bsls_bb_problem.shard_role: 0 the whole problem here, 1 a column
         shard that adds target to its partial residual, 2 another column shard
@@ -1097,6 +1163,16 @@ class BBEngine:
         if nb < 0:
             check(int(nb), 'bsls_bb_row_blocks')
         return int(nb), int(R.value)
+
+    def k2_part(self, it, part, stream=None):
+        """Stage 10 on K2 column group `part` (bsls_bb_k2_part; link-part engines)."""
+        check(_native.lib().bsls_bb_k2_part(self.P, int(it), int(part), stream_handle(stream)),
+              'bsls_bb_k2_part')
+
+    def k1_rows(self, it, rb0, rb1, stream=None):
+        """Stage 14 on K1 row blocks [rb0, rb1) (bsls_bb_k1_rows)."""
+        check(_native.lib().bsls_bb_k1_rows(self.P, int(it), int(rb0), int(rb1),
+                                            stream_handle(stream)), 'bsls_bb_k1_rows')
 
     def residual_rows(self, it, rb0, rb1, stream=None):
         """Stage 1 on K1 row blocks [rb0, rb1) (bsls_bb_residual_rows)."""

@@ -114,10 +114,18 @@ class ShardedBB:
                  fuse=None, native=None, slices=None):
         self.e = engine
         rank = _shard_rank(rank)
-        # native: an RcclComm -- iterate() then enqueues the whole schedule from
-        # C++ (bsls_bb_shard_iterate: the stages and the two RCCL all-reduces of
-        # an iteration, no Python per iteration); parts > 1 stays Python-driven
-        self.native = native if (native is not None and int(parts) <= 1) else None
+        # link parts: an engine built with link_parts = parts (K2's image in
+        # column groups over K1's row-block parts) runs the exchange pipelined
+        # behind both walks (bsls_bb_shard_iterate_parts); other engines with
+        # parts > 1 pipeline it behind K1 only, from Python
+        lb = getattr(engine, 'k1_part_bounds', None)
+        self.link = (lb is not None and int(parts) > 1 and len(lb) - 1 == int(parts))
+        # native: an RcclComm / CallbackComm / ModelComm -- iterate() then
+        # enqueues the whole schedule from C++ (bsls_bb_shard_iterate[_parts]:
+        # the stages and the all-reduces of an iteration, no Python per
+        # iteration); row parts without link parts stay Python-driven
+        self.native = native if (native is not None and (int(parts) <= 1 or self.link)) else None
+        self._cstream = None
         # fuse 2 (default): K2 sums this rank's slice of ||r||^2 beside the BB
         # sums (stage 10), all-reduced with them, then f / stopping test
         # (stage 12); 1: K2 reads all of r for it and tests in its last
@@ -140,10 +148,14 @@ class ShardedBB:
         # rank 0 adds target to its partial residual; the others zero theirs
         # once the run has stopped (bsls_bb_problem.shard_role)
         engine.set_shard_role(1 if rank == 0 else 2)
+        self._rank = rank
         self.all_reduce = all_reduce
         self.all_reduce_async = all_reduce_async
-        self.parts = int(parts) if all_reduce_async is not None else 1
+        self.parts = int(parts) if (all_reduce_async is not None or self.native) else 1
+        if self.link and self.fuse != 2:
+            raise ValueError('link parts run the sliced schedule (fuse 2)')
         self._slices = None
+        self._works = []
         if self.parts > 1:
             nb, R = engine.row_blocks()
             m = engine.r.shape[0]
@@ -151,23 +163,55 @@ class ShardedBB:
             self._slices = [(b[k], b[k + 1], b[k] * R, min(b[k + 1] * R, m))
                             for k in range(len(b) - 1)]
 
+    def _rx(self):
+        """r as exchanged: the int64 words of a fixed-point r."""
+        return getattr(self.e, 'r_exchange', self.e.r)
+
     def residual(self, it):
         """r = sum over ranks of A_g x_g (before stage 2)."""
         e = self.e
-        if not self._slices:
+        if not self._slices or self.all_reduce_async is None:
             # (stage 14: K1 after stage 15, which may have initialised r)
             e.stage(14 if (self.fuse == 2 and it > 0) else 1, it)
-            self.all_reduce(e.r)
+            self.all_reduce(self._rx())
             return
         works = []
         for rb0, rb1, r0, r1 in self._slices:
             e.residual_rows(it, rb0, rb1)
-            works.append(self.all_reduce_async(e.r[r0:r1]))
+            works.append(self.all_reduce_async(self._rx()[r0:r1]))
         for w in works:
             w.wait()
 
+    def _fix_r(self):
+        """The fixed-point r (bsls_bb_problem.r_fx) of an atomic-K1 shard:
+        every |partial sum| of a row is at most |target_i| + |N z|max * sum_j
+        |A_ij| over all ranks' columns (|N z| <= 2 (max|z0| + 1) in the
+        prologue, <= 1 once K3 has clipped z), so the scale 2^k puts that bound
+        B below 2^61.  Collective: every rank computes the same B.
+        BSLS_SHARD_RFX=0 keeps r in doubles."""
+        e = self.e
+        if os.environ.get('BSLS_SHARD_RFX', '1') == '0' or not hasattr(e, 'fixed_r_ok'):
+            return
+        if not e.fixed_r_ok():
+            return
+        import math
+        import torch
+        A = e._A_host
+        S = np.asarray(abs(A).sum(axis=1)).ravel()
+        t = torch.from_numpy(S).to(e.r.device)
+        self.all_reduce(t)
+        world, rank = max(1, _world_size()), self._rank
+        zv = torch.zeros(world, dtype=torch.float64, device=e.r.device)
+        zv[rank % world] = float(e.z0.abs().max()) if e.z0 is not None and e.z0.numel() else 0.0
+        self.all_reduce(zv)
+        nzb = 2.0 * (float(zv.max()) + 1.0)
+        B = float((e.target.abs() + nzb * t).max()) if t.numel() else 0.0
+        k = 61 - int(math.ceil(math.log2(B))) if B > 0 else 61
+        e.set_r_fixed(math.ldexp(1.0, max(-1000, min(1000, k))))
+
     def prologue(self):
         e = self.e
+        self._fix_r()
         e.stage(0, 0)
         e.stage(5, 0)            # z[1] = z0 + 1, x = x0 + N z[1]
         self.residual(0)         # r(z0 + 1)
@@ -179,16 +223,29 @@ class ShardedBB:
     def iterate(self, first, count):
         e = self.e
         if self.native is not None:
+            import ctypes
             import _native
             from _native import check, stream_handle
-            if count > 0:
+            if count > 0 and self.link:
+                import torch
+                if self._cstream is None:
+                    self._cstream = torch.cuda.Stream()
+                lb = (ctypes.c_int64 * (self.parts + 1))(*[int(v) for v in e.k1_part_bounds])
+                rc = _native.lib().bsls_bb_shard_iterate_parts(
+                    e.P, self.native.handle, int(first), int(count), self.parts, lb,
+                    ctypes.c_void_p(self._cstream.cuda_stream), stream_handle())
+            elif count > 0:
                 rc = _native.lib().bsls_bb_shard_iterate(e.P, self.native.handle, int(first),
                                                          int(count), int(self.fuse),
                                                          stream_handle())
+            if count > 0:
                 err = getattr(self.native, 'error', None)
                 if rc != 0 and err is not None:
                     raise RuntimeError('bsls_bb_shard_iterate: all-reduce callback failed') from err
                 check(rc, 'bsls_bb_shard_iterate')
+            return
+        if self.link:
+            self._iterate_link(first, count)
             return
         for i in range(first, first + count):
             if self.fuse == 2:
@@ -208,6 +265,28 @@ class ShardedBB:
                 e.stage(9, i)    # f / stopping test of iteration i
         if count > 0 and self.fuse:
             e.stage(9, first + count - 1)   # f / stopping test of the last one
+
+    def _iterate_link(self, first, count):
+        """The link-part pipeline from Python: what bsls_bb_shard_iterate_parts
+        enqueues, with torch.distributed's asynchronous all-reduces."""
+        e = self.e
+        lb = e.k1_part_bounds
+        for i in range(first, first + count):
+            for q in range(self.parts):
+                if self._works:
+                    self._works[q].wait()     # this part's rows of r are summed
+                e.k2_part(i, q)
+            self._works = []
+            self.all_reduce(e.scal[self.SUMS_RR])
+            e.stage(15, i)
+            for q, (rb0, rb1, r0, r1) in enumerate(self._slices):
+                e.k1_rows(i, rb0, rb1)
+                self._works.append(self.all_reduce_async(self._rx()[r0:r1]))
+        if count > 0:
+            for w in self._works:
+                w.wait()
+            self._works = []
+            e.stage(9, first + count - 1)
 
 
 def torch_all_reduce(group=None):
@@ -237,13 +316,17 @@ class CallbackComm:
     The callback synchronises the stream before reducing, so the sum sees the
     stages enqueued before it, and returns before the next stage is enqueued."""
 
-    def __init__(self, all_reduce, views, rank=None, world=None):
+    def __init__(self, all_reduce, views=None, rank=None, world=None, engine=None):
         import ctypes
         import _native
         from _native import check
         self.rank = _shard_rank(rank)
         self.world = int(world) if world is not None else _world_size()
-        self._views = [(int(v.data_ptr()), v) for v in views]
+        # an engine's scal and r (r as its exchange sums it: int64 words under
+        # a fixed-point r, whose scale the prologue sets), else the tensors given
+        if engine is not None:
+            views = [lambda: engine.scal, lambda: engine.r_exchange]
+        self._views = [v if callable(v) else (lambda v=v: v) for v in views]
         self._fn = all_reduce
         self.error = None
 
@@ -251,7 +334,9 @@ class CallbackComm:
             try:
                 import torch
                 t = None
-                for base, v in self._views:
+                for view in self._views:
+                    v = view()
+                    base = int(v.data_ptr())
                     off = (int(buf) - base) // 8
                     if 0 <= off and off + count <= v.numel() and int(buf) == base + 8 * off:
                         t = v[off:off + count]
@@ -269,6 +354,29 @@ class CallbackComm:
         check(_native.lib().bsls_comm_create_callback(self.world, self.rank, self._cb, None,
                                                       ctypes.byref(h)),
               'bsls_comm_create_callback')
+        self.handle = h
+
+    def close(self):
+        import _native
+        if self.handle is not None:
+            _native.lib().bsls_comm_destroy(self.handle)
+            self.handle = None
+
+
+class ModelComm:
+    """A modelled exchange (bsls_comm_create_model) for one-GPU rehearsals of
+    rank `rank` of `world`: every all-reduce moves nothing and holds its stream
+    for fixed_us + us_per_mb per MB (timing only)."""
+
+    def __init__(self, world, rank, fixed_us=0.0, us_per_mb=0.0):
+        import ctypes
+        import _native
+        from _native import check
+        self.world, self.rank = int(world), int(rank)
+        h = ctypes.c_void_p()
+        check(_native.lib().bsls_comm_create_model(self.world, self.rank, float(fixed_us),
+                                                   float(us_per_mb), ctypes.byref(h)),
+              'bsls_comm_create_model')
         self.handle = h
 
     def close(self):

@@ -379,6 +379,15 @@ typedef struct bsls_bb_problem {
      * passes from 64k packs on), 1 = one pack per wave, 2 = always two
      * (BSLS_K3_MERGE=0 / 1 of the Python engine). */
     int64_t k3_merge;
+    /* > 0: a column shard's r in 64-bit fixed point -- r holds the int64
+     * llrint(r_true * r_fx) (r_fx a power of two), so the atomic K1's group
+     * sums add as integers (order-free: the same bits whatever order the
+     * groups land in) and the all-reduce of r sums int64 (exact: the same bits
+     * on every rank count).  Needs the atomic K1 with its initialisation
+     * folded into K3 (a dealt K1 image of several groups on shard_role 1 / 2)
+     * and a dealt K2 image; every |partial sum| must stay below 2^62 / r_fx
+     * (distributed.ShardedBB sizes it from the rows' abs-sums).  0: doubles. */
+    double r_fx;
 } bsls_bb_problem;
 
 size_t bsls_bb_workspace_size(int64_t m, int64_t n, int64_t nz);
@@ -524,6 +533,34 @@ int bsls_comm_all_reduce(bsls_comm *comm, double *d_buf, int64_t count, void *st
  * `stream`; nothing waits on the host. */
 int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *comm, int64_t first_iter,
                           int64_t count, int fuse, void *stream);
+
+/* ---- the exchange pipelined behind the walks (link parts) -------------------
+ * The K2 image holds `nparts` column groups whose link ranges
+ * [group_col[q], group_col[q+1]) are K1's row-block ranges [rb[q] R,
+ * rb[q+1] R) (R = the rows per K1 row block, bsls_bb_row_blocks; the last
+ * clipped to m).  Then per iteration: K2 part 0 .. nparts-1 (bsls_bb_k2_part:
+ * stage 10 on column group q only -- parts < nparts - 1 leave their partial
+ * route sums in wpart, the last adds them, runs N' and the sums; part q reads
+ * only its rows of r), the five-sum all-reduce, stage 15, and K1 by the same
+ * row-block parts (bsls_bb_k1_rows: stage 14 on row blocks [rb0, rb1)), each
+ * part's rows of r all-reduced as soon as the part is done -- so part q's
+ * exchange runs under K1's later parts and the next K2's earlier parts.
+ * bsls_bb_shard_iterate_parts enqueues that (the exchanges on comm_stream,
+ * ordered by events; rb_bounds: nparts + 1 host values from 0 to the K1 row
+ * block count).  Parts must be launched in order on one stream. */
+int bsls_bb_k2_part(const bsls_bb_problem *p, int64_t iter, int part, void *stream);
+int bsls_bb_k1_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
+                    void *stream);
+int bsls_bb_shard_iterate_parts(const bsls_bb_problem *p, bsls_comm *comm, int64_t first_iter,
+                                int64_t count, int nparts, const int64_t *rb_bounds,
+                                void *comm_stream, void *stream);
+/* A modelled exchange for one-GPU rehearsals of a rank's share: every
+ * "all-reduce" moves nothing and holds its stream for fixed_us + us_per_mb
+ * per MB of the buffer (one wave sleeping), so the timing shows how much of
+ * an exchange of that cost the schedule hides.  Results are one rank's
+ * partial sums: timing only. */
+int bsls_comm_create_model(int world, int rank, double fixed_us, double us_per_mb,
+                           bsls_comm **out);
 
 /* ---- DORE on the fused images (python/DORE.py:6-90, gradient_descent.py:55-67)
  * The reference loop with linop = scale * A N, linop_T = scale * N'A',

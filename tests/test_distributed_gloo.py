@@ -97,6 +97,53 @@ class FakeStages:
             return
         self.r += torch.from_numpy(self.A.dot(self.x))
 
+    # link parts (bsls_bb_k2_part / bsls_bb_k1_rows): K2 by column groups over
+    # K1's row-block parts; set by _run(link=True)
+    k1_part_bounds = None
+
+    def _rows_of(self, q):
+        lb = self.k1_part_bounds
+        return lb[q] * self.ROWS, min(lb[q + 1] * self.ROWS, self.A.shape[0])
+
+    def k2_part(self, it, q):
+        """stage 10 on link part q: its partial route sums A_q' r_q and its
+        slice of ||r||^2 (only ITS rows of r are read); the last part adds the
+        earlier ones and runs N' and the sums."""
+        s = self.scal
+        last = q == len(self.k1_part_bounds) - 2
+        if it > 0 and float(s[0]) != 0:
+            if last:
+                self._stopped_sums(10)
+            return
+        r0, r1 = self._rows_of(q)
+        rq = self.r.numpy()[r0:r1]
+        wq = self.AT[:, r0:r1].dot(rq)
+        lo, hi = (self.rr_lo, self.rr_hi) if self.rr_hi > self.rr_lo else (0, self.A.shape[0])
+        a, b = max(lo, r0), min(hi, r1)
+        rrq = float(np.dot(self.r.numpy()[a:b], self.r.numpy()[a:b])) if b > a else 0.0
+        self._w = wq if q == 0 else self._w + wq
+        self._rr = rrq if q == 0 else self._rr + rrq
+        if not last:
+            return
+        zc, zn = (it - 1) & 1, it & 1
+        g = self.Ntw(self._w)
+        self.g[zn][:] = g
+        dg = g - self.g[zc]
+        dz = self.z[zc] - self.z[zn]
+        s[11:15] = s[5:9].clone()
+        s[9] = self._rr
+        s[5], s[6], s[7], s[8] = dg.sum(), dz.dot(dg), dg.dot(dg), g.dot(g)
+
+    def k1_rows(self, it, rb0, rb1):
+        """stage 14 on row blocks [rb0, rb1)."""
+        r0, r1 = rb0 * self.ROWS, min(rb1 * self.ROWS, self.A.shape[0])
+        if not self.fold:
+            self._partial(it, r0, r1)
+            return
+        if float(self.scal[0]) != 0:
+            return
+        self.r[r0:r1] += torch.from_numpy(self.A[r0:r1].dot(self.x))
+
     def _stopped_sums(self, k):
         """K2 of a stopped run (k2_stopped_sums): role 2 zeroes the sums the
         driver all-reduces next, so the sum keeps role 1's."""
@@ -201,7 +248,7 @@ class _Done:
         pass
 
 
-def _run(rank, world, iters, out_q, parts=1, stop_at=None, fold=True):
+def _run(rank, world, iters, out_q, parts=1, stop_at=None, fold=True, link=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, PKG)
     from oracle import oracle as orc
@@ -226,7 +273,11 @@ def _run(rank, world, iters, out_q, parts=1, stop_at=None, fold=True):
     red(part)
     target = part.numpy() - b
     eng = FakeStages(A_g, A_g.T.tocsr(), sz_g, target, orc, stop_at or iters, fold=fold)
+    if link:
+        from distributed import row_parts
+        eng.k1_part_bounds = np.array(row_parts(eng.row_blocks()[0], parts))
     drv = ShardedBB(eng, red, parts=parts, all_reduce_async=red_async, rank=rank)
+    assert drv.link == link
     drv.prologue()
     traj = {}
     for i in range(1, iters + 1):
@@ -241,13 +292,13 @@ def _run(rank, world, iters, out_q, parts=1, stop_at=None, fold=True):
         dist.destroy_process_group()
 
 
-def _spawn(world, iters, parts=1, stop_at=None, fold=True):
+def _spawn(world, iters, parts=1, stop_at=None, fold=True, link=False):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(29500 + (os.getpid() % 1000) + 7 * parts + (stop_at or 0)
-                                    + 3 * int(fold))
+                                    + 3 * int(fold) + 41 * int(link))
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_run, args=(r, world, iters, q, parts, stop_at, fold))
+    procs = [ctx.Process(target=_run, args=(r, world, iters, q, parts, stop_at, fold, link))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -307,6 +358,29 @@ def test_two_rank_stop_keeps_final_residual(orc, fold):
         assert d < 1e-10, (rank, d)
         s1, s2 = one[0]['scal'][5:9], two[rank]['scal'][5:9]
         assert np.max(np.abs(s2 - s1)) <= 1e-9 * max(1.0, np.max(np.abs(s1))), (rank, s1, s2)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('fold', [True, False])
+def test_two_rank_link_parts_match_single(orc, fold):
+    """The exchange pipelined behind both walks (link parts: K1 by 3 row-block
+    parts, each part's rows of r all-reduced asynchronously, the next K2 by the
+    matching column groups, part q waiting only for its own exchange and
+    reading only its rows of r): the single rank's trajectory, and the stop
+    (max_iter 5 of 9 enqueued) with the stop iteration's r and sums."""
+    iters = 12
+    one = _spawn(1, iters, fold=fold)
+    three = _spawn(2, iters, parts=3, fold=fold, link=True)
+    for i in one:
+        d = np.max(np.abs(one[i] - three[i])) / max(1.0, np.max(np.abs(one[i])))
+        assert d < 1e-10, (i, d)
+    ref = _spawn(1, 9, stop_at=5, fold=fold)
+    two = _spawn(2, 9, parts=3, stop_at=5, fold=fold, link=True)
+    r1, s1 = ref[0]['r'], ref[0]['scal'][5:9]
+    for rank in (0, 1):
+        assert two[rank]['scal'][0] == 2 and two[rank]['scal'][1] == 5
+        assert np.max(np.abs(two[rank]['r'] - r1)) <= 1e-10 * max(1.0, np.max(np.abs(r1)))
+        assert np.max(np.abs(two[rank]['scal'][5:9] - s1)) <= 1e-9 * max(1.0, np.max(np.abs(s1)))
 
 
 @pytest.mark.timeout(600)

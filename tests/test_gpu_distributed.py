@@ -90,7 +90,7 @@ def _run(rank, world, backend, port, out_q, fmt=None, parts=1, max_iter=10 ** 9,
             zb = int(eng.scalars()[2]) if max_iter < 10 ** 9 else (i & 1)
             traj[i] = eng.current_z(zb).cpu().numpy().copy()
     if max_iter < 10 ** 9:
-        traj['r'] = eng.r.cpu().numpy().copy()
+        traj["r"] = eng.residual_value().cpu().numpy().copy()
         traj['scal'] = eng.scalars().copy()
     out_q.put((rank, traj))
     if comm is not None:

@@ -23,8 +23,15 @@ one-process BB trajectory (python/BB.py:7-45 over main.py:53-65).
   iteration within the band the one-GPU test holds around the reference's
   454 / 569 / 745.
 
+The atomic K1 keeps r in 64-bit fixed point on a shard (bsls_bb_problem.r_fx,
+distributed.ShardedBB._fix_r): its groups' sums add as integers and the r
+exchange sums int64 words, so neither the order the groups land in nor the
+rank count changes r's bits -- what lets a converged run reach BB.py:22's
+exact-zero sum(delta_g) where the one-GPU run does (float atomics moved one
+problem's exit from ~770 to 874 iterations, gpurun_out/r5a_shard.log).
 Tolerance: the north star's 1e-6 per element (|d| <= 1e-6 max(1, |ref|)):
-the atomic K1 and the dealt tiles' LDS atomics sum in a run-dependent order.
+the dealt tiles' LDS atomics still sum each tile's rows in a run-dependent
+order.
 """
 import argparse
 import os
@@ -77,7 +84,7 @@ def _engine(A_g, sizes_g, b, x0_g, max_iter, early_exit, **kw):
 
 def _driver(eng, rank):
     from distributed import ShardedBB, CallbackComm, torch_all_reduce
-    comm = CallbackComm(torch_all_reduce(), [eng.scal, eng.r], rank=rank)
+    comm = CallbackComm(torch_all_reduce(), rank=rank, engine=eng)
     drv = ShardedBB(eng, torch_all_reduce(), rank=rank, native=comm)
     assert drv.native is comm and drv.fuse == 2
     return drv, comm
@@ -112,7 +119,7 @@ def _run_c5(rank, world, port, out_q):
         done = i
         traj[i] = eng.current_z(i & 1).cpu().numpy().copy()
     info = dict(role=int(eng.P.shard_role), groups=int(eng.A_til.img['ngroups']),
-                fmt=(eng.fmt_A, eng.fmt_AT))
+                fmt=(eng.fmt_A, eng.fmt_AT), r_fx=float(eng.P.r_fx))
     out_q.put((rank, traj, info))
     _finish(comm)
 
@@ -145,6 +152,7 @@ def test_native_driver_two_ranks_c5_density_vs_oracle(cuda, orc):
         # (so K1 adds by atomics into the r stage 15 initialised)
         assert info['role'] == (1 if r == 0 else 2)
         assert info['fmt'] == ('tiles', 'tiles') and info['groups'] > 1, info
+        assert info['r_fx'] > 0, info          # r in fixed point (bsls_bb_problem.r_fx)
     full = make_partitioned(N5, P5, M5)
     ref = orc.bb_trace(full['A'], full['Ax'], full['block_sizes'], max(CHECK5), record_every=1)
     for i in CHECK5:
@@ -176,7 +184,8 @@ def _run_stop(rank, world, port, out_q, max_iter, enq):
     drv.iterate(1, enq)
     s = eng.scalars()
     zb = int(s[2])
-    out_q.put((rank, dict(z=eng.current_z(zb).cpu().numpy().copy(), r=eng.r.cpu().numpy().copy(),
+    out_q.put((rank, dict(z=eng.current_z(zb).cpu().numpy().copy(),
+                          r=eng.residual_value().cpu().numpy().copy(),
                           scal=s.copy(), groups=int(eng.A_til.img['ngroups']))))
     _finish(comm)
 
@@ -240,7 +249,8 @@ def _run_exit(rank, world, port, out_q, path):
         if s[0] != 0 or i >= 300000:
             break
     out_q.put((rank, dict(z=eng.current_z(int(s[2])).cpu().numpy().copy(), scal=s.copy(),
-                          groups=int(eng.A_til.img['ngroups']), role=int(eng.P.shard_role))))
+                          groups=int(eng.A_til.img['ngroups']), role=int(eng.P.shard_role),
+                          r_fx=float(eng.P.r_fx))))
     _finish(comm)
 
 
@@ -270,6 +280,7 @@ def test_native_driver_two_ranks_runs_to_exit(cuda, golden, tmp_path, vi):
     s0, s1 = res[0][0]['scal'], res[1][0]['scal']
     for r in (0, 1):
         assert res[r][0]['groups'] > 1 and res[r][0]['role'] == (1 if r == 0 else 2)
+        assert res[r][0]['r_fx'] > 0          # order-free fixed-point r
     # both ranks decide alike: same reason, same iteration
     assert s0[0] != 0 and s0[0] == s1[0] and s0[1] == s1[1], (s0[:3], s1[:3])
     it = int(s0[1])
@@ -279,3 +290,59 @@ def test_native_driver_two_ranks_runs_to_exit(cuda, golden, tmp_path, vi):
     assert err < 1e-16, err                                # tests/fast/test_main.py:31-47
     ref_it = int(G['main%d_iters' % vi][-1])               # 454 / 569 / 745
     assert abs(it - ref_it) <= max(10, ref_it // 16), (it, ref_it)
+
+
+# ---- the exchange pipelined behind both walks (link parts) --------------------
+
+def _run_link(rank, world, port, out_q, parts, native):
+    _setup(rank, world, port)
+    import torch
+    from synthetic import make_partitioned
+    from distributed import ShardedBB, CallbackComm, torch_all_reduce, torch_all_reduce_async
+    full, b, kw = _small()
+    sh = make_partitioned(40_000, 2_000, 3_000, rank=rank, world=world, **kw)
+    x0 = np.zeros(sh['n'])
+    x0[np.cumsum(sh['block_sizes']) - 1] = 1.0
+    eng = _engine(sh['A'], sh['block_sizes'], b, x0, 10 ** 9, False, fmt='tiles',
+                  link_parts=parts)
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    comm = CallbackComm(torch_all_reduce(), rank=rank, engine=eng) if native else None
+    drv = ShardedBB(eng, torch_all_reduce(), parts=parts, rank=rank, native=comm,
+                    all_reduce_async=None if native else torch_all_reduce_async())
+    assert drv.link and (drv.native is comm)
+    drv.prologue()
+    traj, done = {}, 0
+    for i in CHECK5:
+        drv.iterate(done + 1, i - done)
+        done = i
+        traj[i] = eng.current_z(i & 1).cpu().numpy().copy()
+    info = dict(k2_groups=int(eng.AT_til.img['ngroups']), bounds=list(eng.k1_part_bounds),
+                r_fx=float(eng.P.r_fx))
+    out_q.put((rank, traj, info))
+    if comm is not None:
+        _finish(comm)
+    else:
+        import torch.distributed as dist
+        torch.cuda.synchronize()
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('native', [True, False])
+def test_link_parts_two_ranks_vs_oracle(cuda, orc, native):
+    """K1 by 3 row-block parts, each part's rows of r all-reduced as it
+    finishes, the next K2 by the 3 matching column groups (bsls_bb_k2_part:
+    part q reads only its rows of r; the last adds the earlier parts' route
+    sums) -- the C++ driver (bsls_bb_shard_iterate_parts, the exchanges on a
+    second stream ordered by events) and the Python loop -- follows the
+    oracle at 1 / 5 / 20."""
+    res = _spawn(_run_link, 2, 3, native)
+    for r in (0, 1):
+        info = res[r][1]
+        assert info['k2_groups'] == 3 and len(info['bounds']) == 4, info
+    full, b, _ = _small()
+    ref = orc.bb_trace(full['A'], b, full['block_sizes'], max(CHECK5), record_every=1)
+    for i in CHECK5:
+        got = np.concatenate([res[0][0][i], res[1][0][i]])
+        assert elem_err(got, ref[i]) < 1e-6, (i, elem_err(got, ref[i]))
