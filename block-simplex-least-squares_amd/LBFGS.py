@@ -152,6 +152,8 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
     rho_new = 1 / dot(y_new, s_new)
     eng = _device_engine(f, nabla_f, proj, x)
     ls = eng.line_search() if eng is not None else None
+    import solvers
+    normed_ok = stopping is solvers.stopping
     fx_dev = None          # f(x) on the device once x is a projected point
     while not stop:
         i += 1
@@ -211,8 +213,14 @@ def solve(x0, f, nabla_f, stopping, m=50, record_every=500, proj=None, log=None,
             x = x_next
             if math.isnan(fx):
                 raise ArithmeticError('objective function evaluates to NaN')
-            stop = stopping(Normed(g_new, math.sqrt(gg)), fx, i, t, d=Normed(d, dnorm),
-                            options=options)
+            if normed_ok:
+                # solvers.stopping only takes norms and t * d: the norms the
+                # search already read, no device round trip
+                stop = stopping(Normed(g_new, math.sqrt(gg)), fx, i, t, d=Normed(d, dnorm),
+                                options=options)
+            else:
+                # any other rule gets the vectors themselves
+                stop = stopping(g_new, fx, i, t, d=d, options=options)
             if i % record_every == 0:
                 start = log(i, copy(x), time.time() - start)
             continue

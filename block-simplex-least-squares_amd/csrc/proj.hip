@@ -789,11 +789,13 @@ __device__ __forceinline__ double dpp_d(double v) {
 }
 // sum / max over the LPB lanes of a group (xor 1, xor 2 in the quad, then the
 // half-row mirror); every lane ends with the same bits (a + b == b + a)
+// (16: then the row mirror, lane i <-> 15 - i, adds the other half-row)
 template <int LPB>
 __device__ __forceinline__ double grp_sum_d(double v) {
     if constexpr (LPB >= 2) v += dpp_d<0xB1>(v);
     if constexpr (LPB >= 4) v += dpp_d<0x4E>(v);
     if constexpr (LPB >= 8) v += dpp_d<0x141>(v);
+    if constexpr (LPB >= 16) v += dpp_d<0x140>(v);
     return v;
 }
 template <int LPB>
@@ -801,6 +803,7 @@ __device__ __forceinline__ int grp_sum_i(int v) {
     if constexpr (LPB >= 2) v += dpp_i<0xB1>(v);
     if constexpr (LPB >= 4) v += dpp_i<0x4E>(v);
     if constexpr (LPB >= 8) v += dpp_i<0x141>(v);
+    if constexpr (LPB >= 16) v += dpp_i<0x140>(v);
     return v;
 }
 template <int LPB>
@@ -809,6 +812,7 @@ __device__ __forceinline__ double grp_max_d(double v) {
     if constexpr (LPB >= 2) { u = dpp_d<0xB1>(v); v = (u > v) ? u : v; }
     if constexpr (LPB >= 4) { u = dpp_d<0x4E>(v); v = (u > v) ? u : v; }
     if constexpr (LPB >= 8) { u = dpp_d<0x141>(v); v = (u > v) ? u : v; }
+    if constexpr (LPB >= 16) { u = dpp_d<0x140>(v); v = (u > v) ? u : v; }
     return v;
 }
 
@@ -989,7 +993,13 @@ __global__ __launch_bounds__(256, BSLS_PROJ_MINW) void proj_thr_kernel(double *_
 // by itself) and the output is relu(lambda + v) from them: lambda = (1 -
 // S) / c, the reference's expression at rho = c - 1 with its members summed
 // in another order (1e-12 contract, as thr_solve).
-constexpr int PIPE_LPB = 8, PIPE_EB = 8, PIPE_BPG = WAVE / PIPE_LPB;
+#ifndef BSLS_PIPE_LPB
+#define BSLS_PIPE_LPB 8   // lanes per block (4, 8 or 16; A/B variant builds)
+#endif
+#ifndef BSLS_PIPE_KO
+#define BSLS_PIPE_KO 0    // 1: no threshold passes (knock-out timing build, results wrong)
+#endif
+constexpr int PIPE_LPB = BSLS_PIPE_LPB, PIPE_EB = 64 / PIPE_LPB, PIPE_BPG = WAVE / PIPE_LPB;
 
 struct PipeGroup {
     __amdgpu_buffer_rsrc_t rs;   // the group's range [s0, e1) of y (scalar registers)
@@ -1063,11 +1073,17 @@ __device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_
     }
     S = grp_sum_d<PIPE_LPB>(S);
     const bool need = !BALL || S > 1.0;
+    // the slots any lane of the wave holds (wave-uniform: past them every
+    // slot is padding, skipped by a scalar branch instead of computed)
+    int nslot = 0;
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e) nslot += __builtin_amdgcn_ballot_w64(ne > e) != 0;
     double lam = 0.0;
     if (__builtin_amdgcn_ballot_w64(need && k > 0)) {
         double M = v[0];
 #pragma unroll
-        for (int e = 1; e < PIPE_EB; ++e) M = (v[e] > M) ? v[e] : M;
+        for (int e = 1; e < PIPE_EB; ++e)
+            if (e < nslot) M = (v[e] > M) ? v[e] : M;
         M = grp_max_d<PIPE_LPB>(M);
         // tau stays below the max (clamped to the next double down: only a
         // |y| ~ 1e12+ rounding could reach it), so the max never leaves the set
@@ -1078,10 +1094,11 @@ __device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_
         double tau = fmin(from_all ? t_all : t_max, Mdn);
         double cprev = from_all ? kd : 1.0;   // the set tau was taken from
         double c = cprev;
-        for (int pass = 0; pass <= PIPE_LPB * PIPE_EB; ++pass) {
+        for (int pass = 0; pass <= (BSLS_PIPE_KO ? -1 : PIPE_LPB * PIPE_EB); ++pass) {
             double sl = 0.0, cl = 0.0;
 #pragma unroll
             for (int e = 0; e < PIPE_EB; ++e) {
+                if (e >= nslot) break;
                 // sum and count by a 0 / 1 factor (fma: one rounding, = the add)
                 const double f = (v[e] > tau) ? 1.0 : 0.0;
                 sl = __builtin_fma(f, v[e], sl);

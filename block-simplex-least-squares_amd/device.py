@@ -1361,7 +1361,10 @@ class XBBEngine:
         self.hist = None
         P = _native.XBBProblem()
         P.m, P.n, P.nblocks, P.max_block = m, n, proj.p, proj.max_block
-        P.ball = 1 if proj.kind == 'ball' else 0
+        # bit 0: the l1 ball; bit 1: the sort-free projection (BSLS_PROJ=fast,
+        # as c_extensions' proj_multi_*_c take it: 1e-12, not bit-identical)
+        P.ball = ((1 if proj.kind == 'ball' else 0)
+                  | (2 if os.environ.get('BSLS_PROJ', 'exact') == 'fast' else 0))
         for dst, M in ((P.A, obj.A), (P.AT, obj.AT)):
             dst.rows = M.m
             dst.indptr, dst.indices, dst.data = (M.indptr.data_ptr(), M.indices.data_ptr(),

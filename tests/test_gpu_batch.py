@@ -65,6 +65,26 @@ def test_solve_bb_vs_reference(cuda, golden, monkeypatch, tag, lasso, fused, pan
     assert rel(sol['x'], d['%s_bb2000_x' % tag]) < 1e-5
 
 
+@pytest.mark.parametrize('tag,lasso', [('s', False), ('l', True)])
+def test_solve_bb_fast_projection(cuda, golden, monkeypatch, tag, lasso):
+    """BSLS_PROJ=fast: the fused x-space rounds take the sort-free projection
+    (bsls_xbb_problem.ball bit 1; the closures the _fast c_extensions entries):
+    the reference's runs within the same 1e-6, fused and closure loops alike."""
+    import BATCH
+    from algorithm_utils import SparseLSQ, get_solver_parts
+    monkeypatch.setenv('BSLS_PROJ', 'fast')
+    monkeypatch.setattr(SparseLSQ, 'PANEL_MIN_NNZ', 1 << 62)
+    d, A, b, starts, x0 = _problem(golden, tag)
+    step, proj, ls, obj = get_solver_parts((A, b), starts, 1.0, is_sparse=True, lasso=lasso)
+    for k in (2, 6, 15):
+        if str(d['%s_bb%d_stop' % (tag, k)]) != 'max_iter':
+            continue
+        for fused in (True, False):
+            sol = BATCH.solve_BB(obj, proj, ls, x0.copy(), max_iter=k, fused=fused)
+            assert sol['iterations'] == int(d['%s_bb%d_it' % (tag, k)]), (k, fused)
+            assert rel(sol['x'], d['%s_bb%d_x' % (tag, k)]) < 1e-6, (k, fused)
+
+
 @pytest.mark.parametrize('tag', ['s', 'c'])
 def test_solve_md_vs_reference(cuda, golden, tag):
     import BATCH
