@@ -996,6 +996,12 @@ __global__ __launch_bounds__(256, BSLS_PROJ_MINW) void proj_thr_kernel(double *_
 #ifndef BSLS_PIPE_LPB
 #define BSLS_PIPE_LPB 8   // lanes per block (4, 8 or 16; A/B variant builds)
 #endif
+#ifndef BSLS_PIPE_STORE_AUX
+#define BSLS_PIPE_STORE_AUX 16   // the stores' cache policy: sc1 (write-through); 0 plain
+#endif
+#ifndef BSLS_PIPE_LDS_TRIM
+#define BSLS_PIPE_LDS_TRIM 0   // 1: the LDS variant skips its loads past the group's range
+#endif
 #ifndef BSLS_PIPE_KO
 #define BSLS_PIPE_KO 0    // 1: no threshold passes (knock-out timing build, results wrong)
 #endif
@@ -1005,6 +1011,7 @@ struct PipeGroup {
     __amdgpu_buffer_rsrc_t rs;   // the group's range [s0, e1) of y (scalar registers)
     int base;                    // this lane's byte offset of its slot 0
     int k;                       // this lane's block length (0: none, or a big block)
+    int len;                     // e1 - s0 (wave-uniform; clamped to 2^30)
 };
 
 // lanes 0 .. PIPE_BPG: the starts of group q's blocks and the end of its last
@@ -1048,6 +1055,7 @@ __device__ __forceinline__ PipeGroup pipe_setup(double *y, long long st, int64_t
     G.rs = __builtin_amdgcn_make_buffer_rsrc(y + s0, 0, (int)((e1 - s0) * 8), 0x00020000);
     G.base = (int)(s - s0 + j) * 8;
     G.k = (b < nb && !big) ? (int)kk : 0;
+    G.len = (int)((e1 - s0) < ((int64_t)1 << 30) ? e1 - s0 : ((int64_t)1 << 30));
     return G;
 }
 
@@ -1058,10 +1066,17 @@ __device__ __forceinline__ void pipe_load(const PipeGroup &G, double (&v)[PIPE_E
     for (int e = 0; e < PIPE_EB; ++e) v[e] = buf_ld(G.rs, G.base + 8 * PIPE_LPB * e);
 }
 
+struct PipeOut {
+    bool need;     // project (the ball variant: the clamped block sums > 1)
+    double lam;    // the reference's lambda: y <- max(lambda + y, 0)
+    int ne;        // this lane's live slots
+};
+
+// Michelot's passes on this lane's slots of its block (v: the entries, slots
+// past the block anything -- they become PAD; the ball variant clamps them)
 template <bool BALL>
-__device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_EB], int j) {
+__device__ __forceinline__ PipeOut pipe_threshold(int k, double (&v)[PIPE_EB], int j) {
     constexpr double PAD = -1.7976931348623157e308;   // below every entry, finite
-    const int k = G.k;
     const int ne = (k > j) ? (k - j + PIPE_LPB - 1) / PIPE_LPB : 0;
     double S = 0.0;
 #pragma unroll
@@ -1084,15 +1099,25 @@ __device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_
 #pragma unroll
         for (int e = 1; e < PIPE_EB; ++e)
             if (e < nslot) M = (v[e] > M) ? v[e] : M;
+        // a third lower bound: the threshold of the set of the lanes' maxima
+        // (min(k, LPB) members -- any subset's threshold is one).  U[0,1)
+        // blocks of ~32: ~0.68 where the whole block's is ~0.47, one pass less
+        const double SL = grp_sum_d<PIPE_LPB>(ne > 0 ? M : 0.0);
+        const double kl = (double)(k < PIPE_LPB ? k : PIPE_LPB);
         M = grp_max_d<PIPE_LPB>(M);
         // tau stays below the max (clamped to the next double down: only a
         // |y| ~ 1e12+ rounding could reach it), so the max never leaves the set
         const double Mdn = next_down(M);
         const double kd = (double)k;
-        const double t_all = (S - 1.0) / kd, t_max = M - 1.0;
+        const double t_all = (S - 1.0) / kd, t_max = M - 1.0, t_lm = (SL - 1.0) / kl;
         const bool from_all = t_all >= t_max;
-        double tau = fmin(from_all ? t_all : t_max, Mdn);
+        double tau = from_all ? t_all : t_max;
         double cprev = from_all ? kd : 1.0;   // the set tau was taken from
+        if (t_lm > tau) {   // (that set need not be {v > t_lm}: no stop after pass 1)
+            tau = t_lm;
+            cprev = -1.0;
+        }
+        tau = fmin(tau, Mdn);
         double c = cprev;
         for (int pass = 0; pass <= (BSLS_PIPE_KO ? -1 : PIPE_LPB * PIPE_EB); ++pass) {
             double sl = 0.0, cl = 0.0;
@@ -1113,14 +1138,26 @@ __device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_
         }
         lam = (1. - S) / c;
     }
-    // out from the registers; padding slots' offsets past the range, so the
-    // hardware drops their stores (no per-slot branch)
+    return PipeOut{need, lam, ne};
+}
+
+template <bool BALL>
+__device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_EB], int j) {
+    const PipeOut o = pipe_threshold<BALL>(G.k, v, j);
+    const bool need = o.need;
+    const double lam = o.lam;
+    const int ne = o.ne;
+    // out from the registers, write-through (sc1: the lines leave L2 while
+    // other waves still compute, instead of as ~26 MB of dirty lines the next
+    // kernel boundary waits for -- as lds_group's store-out); padding slots'
+    // offsets past the range, so the hardware drops their stores (no per-slot
+    // branch)
 #pragma unroll
     for (int e = 0; e < PIPE_EB; ++e) {
         const double r = need ? relu_ref(lam + v[e]) : v[e];
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, r), G.rs,
-            (e < ne) ? G.base + 8 * PIPE_LPB * e : 0x7FFFFFF0, 0, 0);
+            (e < ne) ? G.base + 8 * PIPE_LPB * e : 0x7FFFFFF0, 0, BSLS_PIPE_STORE_AUX);
     }
 }
 
@@ -1166,6 +1203,64 @@ __global__ __launch_bounds__(256, 2) void proj_pipe_kernel(double *__restrict__ 
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int h = 0; h < PIPE_G; ++h) pipe_solve<BALL>(P[h], v[h], j);
+}
+
+// The same group through LDS (round 5 A/B, BSLS_PROJ_PIPE_LDS): the group's
+// range [s0, e1) comes in by 8-B coalesced loads (lane l, load e: entry 64 e +
+// l -- 512 contiguous bytes per wave instruction, where the block-aligned
+// loads read 8 runs of 64 B), goes to the lanes' block slots through the
+// wave's own 4-KB LDS buffer, and back out the same way (write-through).  A
+// group longer than PIPE_STAGE entries (big blocks inside) takes the direct
+// path.  Entries of big blocks inside the range go back unchanged (the big-
+// block kernel that follows in the stream projects them).
+constexpr int PIPE_STAGE = PIPE_BPG * 64;
+template <bool BALL, bool BIG>
+__global__ __launch_bounds__(256, 2) void proj_pipe_lds_kernel(double *__restrict__ y,
+                                                              const int64_t *__restrict__ starts,
+                                                              int64_t nb, int64_t n,
+                                                              int64_t *__restrict__ big_list,
+                                                              unsigned *__restrict__ big_count,
+                                                              const double *__restrict__ gate) {
+    __shared__ double stage[4][PIPE_STAGE];
+    if (gate && *gate != 1.0) return;
+    const int lane = lane_id(), j = lane % PIPE_LPB, wv = (int)(threadIdx.x / WAVE);
+    const int64_t ngrp = (nb + PIPE_BPG - 1) / PIPE_BPG;
+    const int64_t q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x / WAVE) + wv));
+    if (q >= ngrp) return;
+    PipeGroup G = pipe_setup<BIG>(y, pipe_meta(starts, nb, n, q, lane), q, nb, big_list, big_count,
+                                  true, lane);
+    double v[PIPE_EB];
+    if (G.len > PIPE_STAGE) {
+        pipe_load(G, v);
+        pipe_solve<BALL>(G, v, j);
+        return;
+    }
+    double *buf = stage[wv];
+    constexpr int NL = PIPE_STAGE / WAVE;
+    double t[NL];
+#pragma unroll
+    for (int e = 0; e < NL; ++e)   // past the range: 0
+        t[e] = (BSLS_PIPE_LDS_TRIM && WAVE * e >= G.len) ? 0.0 : buf_ld(G.rs, (WAVE * e + lane) * 8);
+#pragma unroll
+    for (int e = 0; e < NL; ++e) buf[WAVE * e + lane] = t[e];
+    // (a wave's own LDS accesses execute in order: no barrier)
+    const int b0 = G.base / 8;
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e) {
+        const int i = b0 + PIPE_LPB * e;
+        v[e] = buf[i < PIPE_STAGE ? i : PIPE_STAGE - 1];
+    }
+    const PipeOut o = pipe_threshold<BALL>(G.k, v, j);
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e)
+        if (e < o.ne) buf[b0 + PIPE_LPB * e] = o.need ? relu_ref(o.lam + v[e]) : v[e];
+#pragma unroll
+    for (int e = 0; e < NL; ++e) {
+        const int i = WAVE * e + lane;
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, buf[i]), G.rs,
+            i < G.len ? i * 8 : 0x7FFFFFF0, 0, BSLS_PIPE_STORE_AUX);
+    }
 }
 
 struct ProjWork {
@@ -1257,7 +1352,19 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
             proj_pipe_kernel<BALL, false, G><<<grid, 256, 0, st>>>(y, starts, nb, n, w.list,    \
                                                                    w.count, gate);              \
     } while (0)
-        if (pipe == 1) BSLS_PIPE_LAUNCH(1);
+        static const bool via_lds = [] {
+            const char *e = getenv("BSLS_PROJ_PIPE_LDS");
+            return e && atoi(e) != 0;
+        }();
+        if (via_lds) {
+            const unsigned g1 = (unsigned)((groups + 3) / 4);
+            if (big)
+                proj_pipe_lds_kernel<BALL, true><<<g1, 256, 0, st>>>(y, starts, nb, n, w.list,
+                                                                     w.count, gate);
+            else
+                proj_pipe_lds_kernel<BALL, false><<<g1, 256, 0, st>>>(y, starts, nb, n, w.list,
+                                                                      w.count, gate);
+        } else if (pipe == 1) BSLS_PIPE_LAUNCH(1);
         else if (pipe == 2) BSLS_PIPE_LAUNCH(2);
         else if (pipe == 8) BSLS_PIPE_LAUNCH(8);
         else BSLS_PIPE_LAUNCH(4);
