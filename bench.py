@@ -597,6 +597,7 @@ def bench_iso(reps=3, batch=16):
             torch.cuda.synchronize()
             out.append(e0.elapsed_time(e1) / batch * 1e3)
         return sorted(out)[len(out) // 2]
+    floor_us = timed(lambda t: t.mul_(1.0000001))   # the size's practical floor (as bench_proj)
     us_un = timed(iso_unplanned)
     us = timed(plan.apply)
     from oracle import oracle as orc
@@ -609,6 +610,7 @@ def bench_iso(reps=3, batch=16):
     return {'n': nz, 'blocks': int(zs.size), 'packs': plan.npacks, 'avg_us': us,
             'alg_bytes': byt, 'GB_s': byt / (us * 1e-6) / 1e9,
             'frac_hbm_peak': byt / (us * 1e-6) / HBM_PEAK, 'unplanned_avg_us': us_un,
+            'same_size_scale_floor_us': floor_us, 'frac_of_floor': floor_us / us,
             'rocprof_kernels': ['iso_packs_kernel'],
             'cpu_oracle_ms_1thread': cpu_s * 1e3, 'bit_exact_vs_oracle': ok}
 

@@ -18,7 +18,7 @@
 #include "bsls_common.hpp"
 
 // BSLS_K3_KO (timing knock-outs, never in the product build): 1 = no PAVA in
-// K3, 2 = one pass, 3 = two passes.
+// K3 (and no passes in pava_v1_wave_c), 2 = one pass, 3 = two passes.
 #ifndef BSLS_K3_KO
 #define BSLS_K3_KO 0
 #endif
@@ -241,7 +241,7 @@ __device__ __forceinline__ void pava_v1_wave_c(double &y, int L, uint64_t B, dou
                                                int *ps, int *cst, uint64_t *heads = nullptr) {
     WaveRuns s = wave_runs(y, L, B, 0);
     const int maxpass = BSLS_K3_KO >= 2 ? BSLS_K3_KO - 2 : L;
-    for (int pass = 0; pass <= maxpass; ++pass)
+    for (int pass = 0; pass <= maxpass && BSLS_K3_KO != 1; ++pass)
         if (!wave_pass(s, ys, ps, cst)) break;
     y = wave_expand(s, y, L, 0, ps, heads);
 }

@@ -1109,14 +1109,15 @@ __device__ __forceinline__ PipeOut pipe_threshold(int k, double (&v)[PIPE_EB], i
         // |y| ~ 1e12+ rounding could reach it), so the max never leaves the set
         const double Mdn = next_down(M);
         const double kd = (double)k;
-        const double t_all = (S - 1.0) / kd, t_max = M - 1.0, t_lm = (SL - 1.0) / kl;
-        const bool from_all = t_all >= t_max;
-        double tau = from_all ? t_all : t_max;
-        double cprev = from_all ? kd : 1.0;   // the set tau was taken from
-        if (t_lm > tau) {   // (that set need not be {v > t_lm}: no stop after pass 1)
-            tau = t_lm;
-            cprev = -1.0;
-        }
+        // (one division: the larger of the two set thresholds by a cross
+        // product, kd and kl > 0 -- a rounding tie picks either, both bounds)
+        const bool lm = (SL - 1.0) * kd > (S - 1.0) * kl;
+        const double t_set = (lm ? SL - 1.0 : S - 1.0) / (lm ? kl : kd), t_max = M - 1.0;
+        const bool from_set = t_set >= t_max;
+        double tau = from_set ? t_set : t_max;
+        // the set tau was taken from: the lanes' maxima need not be {v > t_lm},
+        // so no stop after pass 1 from there
+        double cprev = from_set ? (lm ? -1.0 : kd) : 1.0;
         tau = fmin(tau, Mdn);
         double c = cprev;
         for (int pass = 0; pass <= (BSLS_PIPE_KO ? -1 : PIPE_LPB * PIPE_EB); ++pass) {
@@ -1221,7 +1222,9 @@ __global__ __launch_bounds__(256, 2) void proj_pipe_lds_kernel(double *__restric
                                                               int64_t *__restrict__ big_list,
                                                               unsigned *__restrict__ big_count,
                                                               const double *__restrict__ gate) {
-    __shared__ double stage[4][PIPE_STAGE];
+    // (PIPE_STAGE + 64 entries: a lane's slot reads b0 + 8 e, b0 <= PIPE_STAGE,
+    // stay inside its wave's buffer with no per-slot clamp)
+    __shared__ double stage[4][PIPE_STAGE + WAVE];
     if (gate && *gate != 1.0) return;
     const int lane = lane_id(), j = lane % PIPE_LPB, wv = (int)(threadIdx.x / WAVE);
     const int64_t ngrp = (nb + PIPE_BPG - 1) / PIPE_BPG;
@@ -1244,12 +1247,9 @@ __global__ __launch_bounds__(256, 2) void proj_pipe_lds_kernel(double *__restric
 #pragma unroll
     for (int e = 0; e < NL; ++e) buf[WAVE * e + lane] = t[e];
     // (a wave's own LDS accesses execute in order: no barrier)
-    const int b0 = G.base / 8;
+    const int b0 = min(G.base / 8, PIPE_STAGE);
 #pragma unroll
-    for (int e = 0; e < PIPE_EB; ++e) {
-        const int i = b0 + PIPE_LPB * e;
-        v[e] = buf[i < PIPE_STAGE ? i : PIPE_STAGE - 1];
-    }
+    for (int e = 0; e < PIPE_EB; ++e) v[e] = buf[b0 + PIPE_LPB * e];
     const PipeOut o = pipe_threshold<BALL>(G.k, v, j);
 #pragma unroll
     for (int e = 0; e < PIPE_EB; ++e)
@@ -1352,9 +1352,12 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
             proj_pipe_kernel<BALL, false, G><<<grid, 256, 0, st>>>(y, starts, nb, n, w.list,    \
                                                                    w.count, gate);              \
     } while (0)
+        // through LDS (coalesced in and out) by default: C2 17.1 against 20.5
+        // us for the direct form (round 5, HBM-fed batch); BSLS_PROJ_PIPE_LDS=0
+        // selects the direct form (A/B)
         static const bool via_lds = [] {
             const char *e = getenv("BSLS_PROJ_PIPE_LDS");
-            return e && atoi(e) != 0;
+            return !e || atoi(e) != 0;
         }();
         if (via_lds) {
             const unsigned g1 = (unsigned)((groups + 3) / 4);
