@@ -57,6 +57,10 @@ def main():
             y.copy_(y0)
             check(L.bsls_proj_multi_simplex(ptr(y), ptr(st), p, n, mb, ptr(ws), ws.numel(),
                                             stream_handle()), 'proj')
+        for _ in range(args.proj):   # the sort-free form (proj_simplex_fast)
+            y.copy_(y0)
+            check(L.bsls_proj_multi_simplex_fast(ptr(y), ptr(st), p, n, mb, ptr(ws), ws.numel(),
+                                                 stream_handle()), 'proj fast')
         torch.cuda.synchronize()
     if args.iso:
         from device import iso_plan

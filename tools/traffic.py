@@ -19,10 +19,15 @@ KERNELS = {
            'K3_pava_clip_z2x': ['bsls::bb_k3<1, false, 2>'],
            'K1_spmv_A': ['bsls::bb_k1t<0, true, true, true,', 'bsls::bb_k1_sum<true, true, true>'],
            'proj_simplex_C2': ['bsls::proj_lds_kernel<false, 2, false>'],   # the exact path
+           'proj_simplex_fast_C2': ['bsls::proj_pipe_lds_kernel<false, false>'],
            'isotonic_C4': ['bsls::iso_packs_kernel<1, false>']},
     'C5': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<3, true, 0, 2>'],
            'K3_pava_clip_z2x': ['bsls::bb_k3<2, true, 2>'],
            'K1_spmv_A': ['bsls::bb_k1t<0, true, true, true,', 'bsls::bb_k1_sum<true, true, true>']},
+    # rank 0 of the 8-way split (stages 10 / 15 / 14: atomic K1, r initialised in K3)
+    'C5_x8': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<3, true, 2, 2>'],
+              'K3_pava_clip_z2x': ['bsls::bb_k3<1, false, 2>'],
+              'K1_spmv_A': ['bsls::bb_k1t<0, true, true, false,']},
 }
 
 
