@@ -22,6 +22,7 @@ BSLS_E_COMM = -100
 
 # scal[] slots and stop reasons (include/bsls_hip.h)
 S_STOP, S_ITER, S_ZBUF, S_T, S_FX, S_SUMDG, S_DZDG, S_DGDG, S_GG, S_RR, S_WARN = range(11)
+S_DD = 15
 S_PSUMDG = 11    # .. 14: stage 10's copy of iteration i - 1's four sums
 S_COUNT = 16
 STOP_NOCHANGE, STOP_MAXITER, STOP_GRAD, STOP_DG = 1, 2, 3, 4
@@ -83,7 +84,8 @@ class BBProblem(ctypes.Structure):
                 ('At', Tiles), ('ATt', Tiles), ('wpart', _vp), ('work_bytes', _sz),
                 ('long_packs', _vp), ('nlong', _i64), ('long_off', _vp), ('long_scratch', _vp),
                 ('colv_n', _vp), ('colv_codec', _i64), ('rr_lo', _i64), ('rr_hi', _i64),
-                ('pava_warm', _i64), ('k1_atomic', _i64), ('k3_merge', _i64), ('r_fx', _dbl)]
+                ('pava_warm', _i64), ('k1_atomic', _i64), ('k3_merge', _i64), ('r_fx', _dbl),
+                ('sy_dr', _i64)]
 
 
 class DoreState(ctypes.Structure):
