@@ -1214,7 +1214,71 @@ __global__ __launch_bounds__(256, 2) void proj_pipe_kernel(double *__restrict__ 
 // group longer than PIPE_STAGE entries (big blocks inside) takes the direct
 // path.  Entries of big blocks inside the range go back unchanged (the big-
 // block kernel that follows in the stream projects them).
-constexpr int PIPE_STAGE = PIPE_BPG * 64;
+// PIPE_STAGE: the LDS buffer's entries per wave (a group's range up to it
+// goes through LDS); BSLS_PIPE_STAGE overrides it for the A/B builds
+#ifndef BSLS_PIPE_STAGE
+#define BSLS_PIPE_STAGE (PIPE_BPG * 64)
+#endif
+constexpr int PIPE_STAGE = BSLS_PIPE_STAGE, PIPE_NL = PIPE_STAGE / WAVE;
+static_assert(PIPE_STAGE % WAVE == 0, "the LDS stage is whole wave rows");
+
+// the group's range by coalesced 8-B loads (lane l, load e: entry 64 e + l;
+// past the range the hardware returns 0)
+__device__ __forceinline__ void lds_range_load(const PipeGroup &G, double (&t)[PIPE_NL], int lane) {
+#pragma unroll
+    for (int e = 0; e < PIPE_NL; ++e)
+        t[e] = (BSLS_PIPE_LDS_TRIM && WAVE * e >= G.len) ? 0.0 : buf_ld(G.rs, (WAVE * e + lane) * 8);
+}
+
+// t to the wave's LDS buffer, the lanes' block slots out of it, Michelot,
+// the results back into the slots and the range out by coalesced
+// write-through stores (a wave's own LDS accesses execute in order: no
+// barrier, and the next group may reuse the buffer right after)
+template <bool BALL>
+__device__ __forceinline__ void lds_group(const PipeGroup &G, const double (&t)[PIPE_NL],
+                                          double *buf, int lane, int j) {
+#pragma unroll
+    for (int e = 0; e < PIPE_NL; ++e) buf[WAVE * e + lane] = t[e];
+    double v[PIPE_EB];
+    const int b0 = min(G.base / 8, PIPE_STAGE);
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e) v[e] = buf[b0 + PIPE_LPB * e];
+    const PipeOut o = pipe_threshold<BALL>(G.k, v, j);
+#pragma unroll
+    for (int e = 0; e < PIPE_EB; ++e)
+        if (e < o.ne) buf[b0 + PIPE_LPB * e] = o.need ? relu_ref(o.lam + v[e]) : v[e];
+#pragma unroll
+    for (int e = 0; e < PIPE_NL; ++e) {
+        const int i = WAVE * e + lane;
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, buf[i]), G.rs,
+            i < G.len ? i * 8 : 0x7FFFFFF0, 0, BSLS_PIPE_STORE_AUX);
+    }
+}
+
+// one group either way: through LDS when its range fits the buffer, else
+// straight into the lanes' registers (pipe_load / pipe_solve)
+template <bool BALL>
+__device__ __forceinline__ void pipe_group_one(const PipeGroup &G, double *buf, int lane, int j) {
+    if (G.len > PIPE_STAGE) {
+        double v[PIPE_EB];
+        pipe_load(G, v);
+        pipe_solve<BALL>(G, v, j);
+        return;
+    }
+    double t[PIPE_NL];
+    lds_range_load(G, t, lane);
+    lds_group<BALL>(G, t, buf, lane, j);
+}
+
+// The same group through LDS (round 5, the default fast form; BSLS_PROJ_PIPE_LDS):
+// the group's range [s0, e1) comes in by 8-B coalesced loads (512 contiguous
+// bytes per wave instruction, where the block-aligned loads read 8 runs of
+// 64 B), goes to the lanes' block slots through the wave's own LDS buffer,
+// and back out the same way (write-through).  A group longer than
+// PIPE_STAGE entries (big blocks inside) takes the direct path.  Entries of
+// big blocks inside the range go back unchanged (the big-block kernel that
+// follows in the stream projects them).
 template <bool BALL, bool BIG>
 __global__ __launch_bounds__(256, 2) void proj_pipe_lds_kernel(double *__restrict__ y,
                                                               const int64_t *__restrict__ starts,
@@ -1230,37 +1294,9 @@ __global__ __launch_bounds__(256, 2) void proj_pipe_lds_kernel(double *__restric
     const int64_t ngrp = (nb + PIPE_BPG - 1) / PIPE_BPG;
     const int64_t q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x / WAVE) + wv));
     if (q >= ngrp) return;
-    PipeGroup G = pipe_setup<BIG>(y, pipe_meta(starts, nb, n, q, lane), q, nb, big_list, big_count,
-                                  true, lane);
-    double v[PIPE_EB];
-    if (G.len > PIPE_STAGE) {
-        pipe_load(G, v);
-        pipe_solve<BALL>(G, v, j);
-        return;
-    }
-    double *buf = stage[wv];
-    constexpr int NL = PIPE_STAGE / WAVE;
-    double t[NL];
-#pragma unroll
-    for (int e = 0; e < NL; ++e)   // past the range: 0
-        t[e] = (BSLS_PIPE_LDS_TRIM && WAVE * e >= G.len) ? 0.0 : buf_ld(G.rs, (WAVE * e + lane) * 8);
-#pragma unroll
-    for (int e = 0; e < NL; ++e) buf[WAVE * e + lane] = t[e];
-    // (a wave's own LDS accesses execute in order: no barrier)
-    const int b0 = min(G.base / 8, PIPE_STAGE);
-#pragma unroll
-    for (int e = 0; e < PIPE_EB; ++e) v[e] = buf[b0 + PIPE_LPB * e];
-    const PipeOut o = pipe_threshold<BALL>(G.k, v, j);
-#pragma unroll
-    for (int e = 0; e < PIPE_EB; ++e)
-        if (e < o.ne) buf[b0 + PIPE_LPB * e] = o.need ? relu_ref(o.lam + v[e]) : v[e];
-#pragma unroll
-    for (int e = 0; e < NL; ++e) {
-        const int i = WAVE * e + lane;
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, buf[i]), G.rs,
-            i < G.len ? i * 8 : 0x7FFFFFF0, 0, BSLS_PIPE_STORE_AUX);
-    }
+    const PipeGroup G = pipe_setup<BIG>(y, pipe_meta(starts, nb, n, q, lane), q, nb, big_list,
+                                        big_count, true, lane);
+    pipe_group_one<BALL>(G, stage[wv], lane, j);
 }
 
 struct ProjWork {
@@ -1355,9 +1391,9 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
         // through LDS (coalesced in and out) by default: C2 17.1 against 20.5
         // us for the direct form (round 5, HBM-fed batch); BSLS_PROJ_PIPE_LDS=0
         // selects the direct form (A/B)
-        static const bool via_lds = [] {
+        static const int via_lds = [] {
             const char *e = getenv("BSLS_PROJ_PIPE_LDS");
-            return !e || atoi(e) != 0;
+            return e ? atoi(e) : 1;
         }();
         if (via_lds) {
             const unsigned g1 = (unsigned)((groups + 3) / 4);
