@@ -526,7 +526,10 @@ int bsls_comm_destroy(bsls_comm *comm);
  * `stream` and before the work enqueued after the call returns (e.g.
  * synchronise the stream, reduce, copy back); it returns 0 or nonzero on
  * failure (-> BSLS_E_COMM).  Called on the enqueueing thread, in order.
- * bsls_comm_destroy frees it (no RCCL involved). */
+ * Under a fixed-point r (bsls_bb_problem.r_fx > 0) the r exchange passes
+ * r's words, which are int64: the callback must sum them as int64 (the 5-slot
+ * scal exchange stays double) -- distributed.CallbackComm does, through the
+ * engine's r_exchange view.  bsls_comm_destroy frees it (no RCCL involved). */
 typedef int (*bsls_all_reduce_fn)(double *d_buf, int64_t count, void *stream, void *user);
 int bsls_comm_create_callback(int world, int rank, bsls_all_reduce_fn fn, void *user,
                               bsls_comm **out);
