@@ -686,6 +686,11 @@ def build_engine(sh, b, world, dist, parts, sharded=False, slices=None, model=No
     elif os.environ.get('BSLS_SHARD_NATIVE', '1') != '0' and dist.get_backend() == 'nccl':
         from distributed import RcclComm
         comm = RcclComm()
+    elif os.environ.get('BSLS_SHARD_NATIVE', '1') != '0' and world > 1:
+        # another backend (the gloo rehearsal of N ranks on one GPU): the same
+        # native loop, its all-reduces through torch.distributed callbacks
+        from distributed import CallbackComm
+        comm = CallbackComm(torch_all_reduce(), rank=dist.get_rank(), world=world, engine=eng)
     drv = ShardedBB(eng, torch_all_reduce(), parts=parts,
                     all_reduce_async=torch_all_reduce_async(),
                     rank=dist.get_rank(), native=comm, slices=slices)
@@ -841,9 +846,13 @@ LEGS = ('main', 'c5', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'g
 
 
 def traffic_file():
-    """The newest PMC traffic summary under profiles/ (tools/traffic.py)."""
+    """The newest PMC traffic summary of the default build under profiles/
+    (tools/traffic.py: traffic_rNN.json; suffixed files such as
+    traffic_r05_sydr.json profile an opt-in variant and are not the line's)."""
     import glob
-    fs = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'traffic_r*.json')))
+    import re
+    fs = sorted(f for f in glob.glob(os.path.join(ROOT, 'profiles', 'traffic_r*.json'))
+                if re.fullmatch(r'traffic_r\d+\.json', os.path.basename(f)))
     return fs[-1] if fs else None
 
 
