@@ -71,10 +71,13 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     off += al16((size_t)(m / 16 + 2) * 4);
     w.tk2rb = (unsigned *)(p + off);             // K2 tiles: one ticket per row block (H >= 64)
     off += al16((size_t)(n / 64 + 2) * 4);
+    // K1's per-row-block partials of ||r||^2 (and sy_dr's ||dr||^2): two per
+    // row block, and a row block holds >= 16 rows (16 panels of >= 1 row;
+    // tiles of >= 64 rows)
     w.p1 = (double *)(p + off);
-    off += al16((size_t)((m + 255) / 256 + 1) * 2 * 8);   // (2: ||r||^2 and sy_dr's ||dr||^2)
+    off += al16((size_t)(m / 16 + 2) * 2 * 8);
     w.p2 = (double *)(p + off);
-    off += al16((size_t)((n + PANEL_WAVES - 1) / PANEL_WAVES + 1) * 4 * 8);
+    off += al16((size_t)((n + PANEL_WAVES - 1) / PANEL_WAVES + 1) * 5 * 8);   // (5 sums fused)
     w.pf = (double *)(p + off);
     off += al16((size_t)((m + 255) / 256 + 1) * 2 * 8);
     w.wsc = (int32_t *)(p + off);
