@@ -886,7 +886,7 @@ class BBEngine:
     def __init__(self, A, b, block_sizes, options=None, early_exit=True, A_dev=None,
                  AT_dev=None, AT=None, target=None, x0=None, general=False, fmt=None,
                  tile_plans=(None, None), colv=None, deterministic=False, tile_layouts=None,
-                 link_parts=None):
+                 link_parts=None, sy_dr=None):
         torch = _torch()
         L = _native.lib()
         self.layout = lay = BlockLayout(block_sizes)
@@ -1072,7 +1072,7 @@ class BBEngine:
         # floor it never produces the exact-zero sum(dg) that ends the
         # reference's runs (BB.py:22) -- C3 noise-free ran to max_iter 50000 at
         # f 4.6e-21 where dz . dg exits at 13830.  set_shard_role clears it.
-        sy = os.environ.get('BSLS_SY_DR')
+        sy = os.environ.get('BSLS_SY_DR') if sy_dr is None else int(bool(sy_dr))
         P.sy_dr = 1 if (sy is not None and int(sy)) and P.k1_atomic != 2 else 0
         self.P = P
         self.z0 = None
