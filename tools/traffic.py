@@ -24,11 +24,17 @@ KERNELS = {
     'C5': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<3, true, 0, 2>'],
            'K3_pava_clip_z2x': ['bsls::bb_k3<2, true, 2>'],
            'K1_spmv_A': ['bsls::bb_k1t<0, true, true, true,', 'bsls::bb_k1_sum<true, true, true>']},
-    # rank 0 of the 8-way split (stages 10 / 15 / 14: atomic K1, r initialised in K3)
-    'C5_x8': {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<3, true, 2, 2>'],
-              'K3_pava_clip_z2x': ['bsls::bb_k3<1, false, 2>'],
-              'K1_spmv_A': ['bsls::bb_k1t<0, true, true, false,']},
 }
+# rank 0 of an N-way split (stages 10 / 15 / 14: atomic K1, r initialised in
+# K3; bench.py --rehearse-shard N [--rehearse-workload C3]), keyed as bench.py
+# looks them up at N GPUs: '<workload>_x<N>'.  A '|' separates alternatives
+# (K3's pack form depends on the shard's pack count).
+SHARD = {'K2_spmvT_Nt_dots': ['bsls::bb_k2t<3, true, 2, 2>'],
+         'K3_pava_clip_z2x': ['bsls::bb_k3<1, false, 2>|bsls::bb_k3<2, true, 2>'],
+         'K1_spmv_A': ['bsls::bb_k1t<0, true, true, false,']}
+for _wl in ('C3', 'C5'):
+    for _n in (2, 4, 8):
+        KERNELS['%s_x%d' % (_wl, _n)] = SHARD
 
 
 def load(dirs):
@@ -50,8 +56,8 @@ def main():
     for name, parts in KERNELS[cfg].items():
         fetch = write = 0.0
         ok = True
-        for pfx in parts:
-            hits = [k for k in vals if pfx in k]
+        for alts in parts:
+            hits = [k for pfx in alts.split('|') for k in vals if pfx in k]
             if not hits:
                 ok = False
                 break
