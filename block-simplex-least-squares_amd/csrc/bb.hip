@@ -594,7 +594,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
     double sums[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) sums[q] = 0.0;
-    if (fin) {
+    if (fin && BSLS_TILE_KO != 4) {   // (KO 4: no epilogue -- timing builds only)
         // K2E rows per thread per batch: every z index, then every operand of
         // the batch in flight at once (two round trips per batch instead of
         // two per row: C5's 19 rows per thread made the epilogue ~90 us)

@@ -58,6 +58,7 @@ __device__ __forceinline__ void tile_map(const bsls_tiles &T, int64_t b, int64_t
 typedef uint32_t tile_quad __attribute__((ext_vector_type(4)));
 
 // BSLS_TILE_KO (timing knock-outs of the dealt walk, never in the product
+// build; 4 = K2's epilogue skipped instead -- bb.hip)
 // build): 1 = plain LDS add instead of ds_add_f64, 2 = no LDS accumulation,
 // 3 = no walk at all (what is left: the LDS clear, the finish, the tail)
 #ifndef BSLS_TILE_KO
