@@ -240,6 +240,32 @@ def test_fast_proj_size_classes_ties_borderline(cx, orc, fast_proj):
             assert close12(a, r), (gi, name)
 
 
+def test_fast_proj_group_ranges(cx, orc, fast_proj):
+    """The group kernel's edges (8 consecutive blocks per wave; through LDS
+    when the group's range fits the 512-entry stage, else straight to the
+    lanes): eight blocks of 64
+    (a full stage), a 65 among sevens (a big block inside an LDS range, left
+    to the big-block kernel), ranges just past the stage (direct), a partial
+    last group, an odd n, and entries before the first block that no block
+    owns -- simplex and ball vs the oracle at 1e-12."""
+    rs = np.random.RandomState(21)
+    layouts = [[64] * 8, [7] * 7 + [65], [65] + [7] * 7, [64] * 7 + [65], [1] * 8,
+               [64, 1, 64, 1, 64, 1, 64, 63], [100, 100, 100, 100, 50, 30, 20, 13],
+               [33] * 8, [3, 5, 64]]
+    sizes = np.array([v for lay in layouts for v in lay])
+    for lead in (0, 3):
+        starts = (lead + np.concatenate(([0], np.cumsum(sizes)[:-1]))).astype(np.int64)
+        n = lead + int(sizes.sum())
+        assert n % 2 == 1 or lead == 0
+        for scale in (1.0, 5.0, 0.01):
+            y = rs.randn(n) * scale
+            for name in ('proj_multi_simplex_c', 'proj_multi_ball_c'):
+                a = y.copy(); getattr(cx, name)(a, starts)
+                r = y.copy(); getattr(orc, name)(r, starts)
+                assert close12(a, r), (lead, scale, name)
+                assert np.array_equal(a[:lead], y[:lead])
+
+
 def test_fast_proj_c_abi_entry(cuda, orc):
     """bsls_proj_multi_simplex_fast through the C ABI directly (what bench.py
     times), on a wave-boundary layout: 16-block waves with the last wave
