@@ -49,6 +49,46 @@ __global__ __launch_bounds__(256) void scaleU(double *y, long n, double a) {
     }
 }
 
+// the window structure a segmented projection would have: each wave a fixed
+// 512-entry window (+64 overhang read, not written), loaded coalesced, turned
+// into 8 consecutive entries per lane through LDS and back, one segmented
+// scan step per lane's run (a stand-in for one pass), stored coalesced
+__global__ __launch_bounds__(256) void window_skel(double *y, long n, double a) {
+    __shared__ double buf[4][576 + 8];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long w = (long)blockIdx.x * 4 + wv;
+    const long b0 = w * 512;
+    if (b0 >= n) return;
+    double t[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        const long i = b0 + 64 * e + lane;
+        t[e] = i < n ? y[i] : 0.0;
+    }
+    double *B = buf[wv];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) B[64 * e + lane] = t[e];
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = B[8 * lane + k];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+    // one wave-wide inclusive scan of the lane sums (6 steps), as a pass costs
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(s, o, 64);
+        if (lane >= o) s += u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) B[8 * lane + k] = v[k] * a + s * 1e-300;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const long i = b0 + 64 * e + lane;
+        if (i < n) __builtin_nontemporal_store(B[64 * e + lane], y + i);
+    }
+}
+
 int main() {
     const long n = 3200000;
     const int B = 16;
@@ -92,6 +132,9 @@ int main() {
     });
     run("8 x 16 B / thread", [&](double *y) {
         scaleU<8, 0><<<(n / 2 + 2047) / 2048, 256>>>(y, n, 1.0000001);
+    });
+    run("window 512 + LDS both ways", [&](double *y) {
+        window_skel<<<(n / 512 + 4) / 4, 256>>>(y, n, 1.0000001);
     });
     return 0;
 }
