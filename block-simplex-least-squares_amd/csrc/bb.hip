@@ -1019,14 +1019,25 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
     if (BSLS_K3_KO != 1) {
         // warm start: the last run partition of each pack, tested first
         // (pava_warm); a pack that passes needs no reference pass
-        bool need[K3_PPW];
+        // (BSLS_K3_REPAIR, the default: a partition that fails is repaired
+        // -- its unsplittable runs kept pooled -- and the reference passes
+        // continue from it, pava_warm_repair)
+        bool need[K3_PPW], store[K3_PPW];
+        uint64_t Hn[K3_PPW];
 #pragma unroll
         for (int q = 0; q < K3_PPW; ++q) {
             need[q] = L[q] > 0 && L[q] <= WAVE;
-            if (hd && need[q] && (H[q] & B[q]) == B[q] && (H[q] & ~mask_lt(L[q])) == 0ull)
-                need[q] = !pava_warm(yv[q], L[q], B[q], H[q]);
+            store[q] = need[q];
+            if (hd && need[q] && (H[q] & B[q]) == B[q] && (H[q] & ~mask_lt(L[q])) == 0ull) {
+#if BSLS_K3_REPAIR
+                store[q] = pava_warm_repair(yv[q], L[q], B[q], H[q], pv_y[wv], pv_p[wv],
+                                            pv_c[wv], &Hn[q]);
+                need[q] = false;
+#else
+                need[q] = store[q] = !pava_warm(yv[q], L[q], B[q], H[q]);
+#endif
+            }
         }
-        uint64_t Hn[K3_PPW];
         if (MERGE && K3_PPW == 2 && need[0] && need[K3_PPW - 1]) {
             pava_v1_wave_pair(yv[0], L[0], B[0], yv[K3_PPW - 1], L[K3_PPW - 1], B[K3_PPW - 1],
                               pv_y[wv], pv_p[wv], pv_c[wv], &Hn[0], &Hn[K3_PPW - 1]);
@@ -1039,7 +1050,7 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
         if (hd) {
 #pragma unroll
             for (int q = 0; q < K3_PPW; ++q)   // the new partition for the next call
-                if (need[q] && l == 0) hd[w0 + q * nw] = Hn[q];
+                if (store[q] && l == 0) hd[w0 + q * nw] = Hn[q];
         }
     }
 #pragma unroll

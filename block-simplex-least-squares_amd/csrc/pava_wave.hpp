@@ -22,6 +22,11 @@
 #ifndef BSLS_K3_KO
 #define BSLS_K3_KO 0
 #endif
+// BSLS_K3_REPAIR: K3's warm start repairs a failed partition
+// (pava_warm_repair) instead of running the reference passes from scratch
+#ifndef BSLS_K3_REPAIR
+#define BSLS_K3_REPAIR 1
+#endif
 
 namespace bsls {
 
@@ -353,6 +358,74 @@ __device__ __forceinline__ bool pava_warm(double &y, int L, uint64_t B, uint64_t
     const bool ok = !act | (split_ok & order_ok);
     if (ballot_b(!ok) != 0ull) return false;
     if (act) y = m;
+    return true;
+}
+
+// The warm start with repair (round 5): as pava_warm, but a pack whose kept
+// partition fails does not start over from single elements.  A kept run that
+// still cannot be split (its every proper prefix mean >= its mean: alone it
+// is one level of its own isotonic fit) is a state the reference's pooling
+// can reach from single elements, and pooling adjacent violators from any
+// such state ends at the one fit; so such runs stay pooled, the runs that can
+// be split go back to their elements, and the reference passes run from
+// there -- usually one or two instead of ~4 from scratch.  The fit is the
+// unique PAVA fit up to the roundings of the kept runs' tree-order sums (the
+// north star's 1e-12, as pava_warm).  Returns false when the kept partition
+// held (y = its run means, nothing to store), true when the passes ran
+// (y = the expanded fit, *heads = its run-head mask).  ys / ps / cst: as
+// pava_v1_wave_c.  H as pava_warm.
+__device__ __forceinline__ bool pava_warm_repair(double &y, int L, uint64_t B, uint64_t H,
+                                                 double *ys, int *ps, int *cst, uint64_t *heads) {
+    const int l = lane_id();
+    const bool act = l < L;
+    const int h = hi_bit(H & mask_le(l));
+    const uint64_t Hg = H & ~mask_le(l);
+    const int e = (Hg != 0ull && lo_bit(Hg) < L) ? lo_bit(Hg) - 1 : L - 1;
+    double s = act ? y : 0.0;
+    double u;
+    u = dpp_mov_d<0x111, 0xF>(s);
+    s += (l - 1 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x112, 0xF>(s);
+    s += (l - 2 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x114, 0xF>(s);
+    s += (l - 4 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x118, 0xF>(s);
+    s += (l - 8 >= h) ? u : 0.0;
+    u = dpp_mov_d<0x142, 0xA>(s);
+    s += ((l & 16) != 0 && h <= (l & ~15) - 1) ? u : 0.0;
+    u = dpp_mov_d<0x143, 0xC>(s);
+    s += (l >= 32 && h <= 31) ? u : 0.0;
+    const double S = shfl_d(s, e);
+    const double m = S / (double)(e - h + 1);
+    const double mp = dpp_shr1_d(m);
+    const bool split_ok = (l == e) | (s >= (double)(l - h + 1) * m);
+    const bool order_ok = (l != h) | (((B >> l) & 1ull) != 0ull) | (mp <= m);
+    const bool ok = !act | (split_ok & order_ok);
+    if (ballot_b(!ok) == 0ull) {
+        if (act) y = m;
+        return false;
+    }
+    // runs holding a lane that fails the split test go back to their
+    // elements; the others stay pooled (value m, weight e - h + 1)
+    const uint64_t bad = ballot_b(act & !split_ok);
+    const bool keep = (bad & mask_le(e) & ~mask_lt(h)) == 0ull;
+    const uint64_t H2 = ballot_b(act & (!keep | (l == h)));
+    if ((H2 >> l) & 1ull) {
+        const int idx = mbcnt64(H2);
+        ys[idx] = keep ? m : y;
+        ps[idx] = (keep ? e - h + 1 : 1) | ((int)((B >> l) & 1ull) << 8) | (l << 9);
+    }
+    WaveRuns r{y, 1, 0, l, (int)__popcll(H2)};
+    if (l < r.nh) {
+        r.Y = ys[l];
+        const int pk = ps[l];
+        r.W = pk & 255;
+        r.BS = (pk >> 8) & 1;
+        r.O = pk >> 9;
+    }
+    for (int pass = 0; pass <= L; ++pass)
+        if (!wave_pass(r, ys, ps, cst)) break;
+    y = wave_expand(r, y, L, 0, ps, heads);
     return true;
 }
 

@@ -236,7 +236,8 @@ def test_k3_wave_pava_bit_exact(cuda, orc, monkeypatch, merge):
 def test_k3_warm_start_within_ulps(cuda, orc, monkeypatch, merge):
     """K3 with the warm start (pava_warm): blocks of 2..150 routes, both pack
     forms; repeated and slightly moved inputs (the kept partitions hold),
-    then an unrelated input (they fail and the reference passes run) -- every
+    then a moved and an unrelated input (they fail: repaired, the reference
+    passes run from the runs that still hold, pava_warm_repair) -- every
     result within 1e-12 of the oracle's PAVA, x = N z exact on the kernel's z."""
     import torch
     monkeypatch.setenv('BSLS_K3_MERGE', merge)
@@ -253,7 +254,8 @@ def test_k3_warm_start_within_ulps(cuda, orc, monkeypatch, merge):
     nz = eng.nz
     base, g = rs.randn(nz), rs.randn(nz) * 0.5
     res = []
-    for k, zc in enumerate((base, base, base + 1e-7 * rs.randn(nz), rs.randn(nz))):
+    for k, zc in enumerate((base, base, base + 1e-7 * rs.randn(nz), base + 0.05 * rs.randn(nz),
+                            rs.randn(nz), base)):
         eng.z[0][:nz].copy_(torch.from_numpy(zc))
         eng.g[1][:nz].copy_(torch.from_numpy(g))
         sc = np.zeros(_native.S_COUNT)
