@@ -8,7 +8,10 @@ against HIP events recorded on the engine's stream at the window's two ends
 
 --prime: before each window's barrier/synchronize, a short untimed spin on the
 stream (the GPU busy right up to the window) -- whether an idle gap before
-the window costs device time."""
+the window costs device time.
+--hold: a ~0.5-ms spin enqueued before the window's first event, so the host
+has enqueued the whole window before the device reaches it (diagnostic: the
+device time without any wait on the host's launches)."""
 import argparse
 import os
 import sys
@@ -27,6 +30,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=400)
     ap.add_argument('--windows', type=int, default=10)
     ap.add_argument('--prime', action='store_true')
+    ap.add_argument('--hold', action='store_true')
     a = ap.parse_args()
     import torch
     import bench
@@ -37,24 +41,28 @@ def main():
     torch.cuda.synchronize()
     first = 1 + a.warmup
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    wall, dev = [], []
+    wall, dev, enq = [], [], []
     for _ in range(a.windows):
         if a.prime:
             torch.cuda._sleep(20000)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        if a.hold:
+            torch.cuda._sleep(500000)
         e0.record()
         run(first, a.steps)
+        enq.append((time.perf_counter() - t0) * 1e6)
         e1.record()
         torch.cuda.synchronize()
         wall.append((time.perf_counter() - t0) * 1e6)
         dev.append(e0.elapsed_time(e1) * 1e3)
         first += a.steps
     wall, dev = np.array(wall), np.array(dev)
-    print('steps %d warmup %d prime %s: wall median %.1f us (%.2f per it), device median %.1f us '
-          '(%.2f per it), wall - device median %.1f us'
-          % (a.steps, a.warmup, a.prime, np.median(wall), np.median(wall) / a.steps,
-             np.median(dev), np.median(dev) / a.steps, np.median(wall - dev)), flush=True)
+    print('steps %d warmup %d prime %s hold %s: wall median %.1f us (%.2f per it), device median '
+          '%.1f us (%.2f per it), wall - device median %.1f us, enqueue median %.1f us'
+          % (a.steps, a.warmup, a.prime, a.hold, np.median(wall), np.median(wall) / a.steps,
+             np.median(dev), np.median(dev) / a.steps, np.median(wall - dev), np.median(enq)),
+          flush=True)
 
 
 if __name__ == '__main__':
