@@ -366,9 +366,10 @@ typedef struct bsls_bb_problem {
     int64_t rr_lo, rr_hi;
     /* 1: K3 first tests each pack's run partition from its previous call (the
      * fit's partition rarely changes between iterations) and skips the PAVA
-     * passes where it still holds -- results within ulps of the reference
-     * PAVA (the north star's 1e-12), not bit-identical; 0: the reference
-     * passes always (bit-identical). */
+     * passes where it still holds (where it fails, its runs that cannot be
+     * split stay pooled and the passes continue from them) -- results within
+     * ulps of the reference PAVA (the north star's 1e-12), not bit-identical;
+     * 0: the reference passes always (bit-identical). */
     int64_t pava_warm;
     /* K1's column-group sums (tile images with several groups): 0 = auto --
      * global f64 atomics into r on a column shard (shard_role 1 / 2), the
