@@ -329,7 +329,17 @@ __device__ __forceinline__ double dpp_mov_d(double v) {
     return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ bool pava_warm(double &y, int L, uint64_t B, uint64_t H) {
+// The test of a kept partition H, shared by both warm forms: this lane's run
+// [h, e], the run's mean m, and the two conditions (split: the prefix of the
+// run up to this lane has a mean >= m; order: a run head's mean is >= the
+// previous run's within its block).
+struct WarmTest {
+    int h, e;
+    double m;
+    bool split_ok, ok;
+};
+
+__device__ __forceinline__ WarmTest warm_test(double y, int L, uint64_t B, uint64_t H) {
     const int l = lane_id();
     const bool act = l < L;
     const int h = hi_bit(H & mask_le(l));                    // this lane's run head
@@ -356,8 +366,13 @@ __device__ __forceinline__ bool pava_warm(double &y, int L, uint64_t B, uint64_t
     const bool split_ok = (l == e) | (s >= (double)(l - h + 1) * m);
     const bool order_ok = (l != h) | (((B >> l) & 1ull) != 0ull) | (mp <= m);
     const bool ok = !act | (split_ok & order_ok);
-    if (ballot_b(!ok) != 0ull) return false;
-    if (act) y = m;
+    return WarmTest{h, e, m, split_ok, ok};
+}
+
+__device__ __forceinline__ bool pava_warm(double &y, int L, uint64_t B, uint64_t H) {
+    const WarmTest w = warm_test(y, L, B, H);
+    if (ballot_b(!w.ok) != 0ull) return false;
+    if (lane_id() < L) y = w.m;
     return true;
 }
 
@@ -373,47 +388,26 @@ __device__ __forceinline__ bool pava_warm(double &y, int L, uint64_t B, uint64_t
 // north star's 1e-12, as pava_warm).  Returns false when the kept partition
 // held (y = its run means, nothing to store), true when the passes ran
 // (y = the expanded fit, *heads = its run-head mask).  ys / ps / cst: as
-// pava_v1_wave_c.  H as pava_warm.
+// pava_v1_wave_c.  H as pava_warm.  CPU model over the oracle's weighted
+// PAVA: tests/test_pava_repair_model.py.
 __device__ __forceinline__ bool pava_warm_repair(double &y, int L, uint64_t B, uint64_t H,
                                                  double *ys, int *ps, int *cst, uint64_t *heads) {
     const int l = lane_id();
     const bool act = l < L;
-    const int h = hi_bit(H & mask_le(l));
-    const uint64_t Hg = H & ~mask_le(l);
-    const int e = (Hg != 0ull && lo_bit(Hg) < L) ? lo_bit(Hg) - 1 : L - 1;
-    double s = act ? y : 0.0;
-    double u;
-    u = dpp_mov_d<0x111, 0xF>(s);
-    s += (l - 1 >= h) ? u : 0.0;
-    u = dpp_mov_d<0x112, 0xF>(s);
-    s += (l - 2 >= h) ? u : 0.0;
-    u = dpp_mov_d<0x114, 0xF>(s);
-    s += (l - 4 >= h) ? u : 0.0;
-    u = dpp_mov_d<0x118, 0xF>(s);
-    s += (l - 8 >= h) ? u : 0.0;
-    u = dpp_mov_d<0x142, 0xA>(s);
-    s += ((l & 16) != 0 && h <= (l & ~15) - 1) ? u : 0.0;
-    u = dpp_mov_d<0x143, 0xC>(s);
-    s += (l >= 32 && h <= 31) ? u : 0.0;
-    const double S = shfl_d(s, e);
-    const double m = S / (double)(e - h + 1);
-    const double mp = dpp_shr1_d(m);
-    const bool split_ok = (l == e) | (s >= (double)(l - h + 1) * m);
-    const bool order_ok = (l != h) | (((B >> l) & 1ull) != 0ull) | (mp <= m);
-    const bool ok = !act | (split_ok & order_ok);
-    if (ballot_b(!ok) == 0ull) {
-        if (act) y = m;
+    const WarmTest w = warm_test(y, L, B, H);
+    if (ballot_b(!w.ok) == 0ull) {
+        if (act) y = w.m;
         return false;
     }
     // runs holding a lane that fails the split test go back to their
     // elements; the others stay pooled (value m, weight e - h + 1)
-    const uint64_t bad = ballot_b(act & !split_ok);
-    const bool keep = (bad & mask_le(e) & ~mask_lt(h)) == 0ull;
-    const uint64_t H2 = ballot_b(act & (!keep | (l == h)));
+    const uint64_t bad = ballot_b(act & !w.split_ok);
+    const bool keep = (bad & mask_le(w.e) & ~mask_lt(w.h)) == 0ull;
+    const uint64_t H2 = ballot_b(act & (!keep | (l == w.h)));
     if ((H2 >> l) & 1ull) {
         const int idx = mbcnt64(H2);
-        ys[idx] = keep ? m : y;
-        ps[idx] = (keep ? e - h + 1 : 1) | ((int)((B >> l) & 1ull) << 8) | (l << 9);
+        ys[idx] = keep ? w.m : y;
+        ps[idx] = (keep ? w.e - w.h + 1 : 1) | ((int)((B >> l) & 1ull) << 8) | (l << 9);
     }
     WaveRuns r{y, 1, 0, l, (int)__popcll(H2)};
     if (l < r.nh) {
