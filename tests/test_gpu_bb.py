@@ -254,8 +254,13 @@ def test_k3_warm_start_within_ulps(cuda, orc, monkeypatch, merge):
     nz = eng.nz
     base, g = rs.randn(nz), rs.randn(nz) * 0.5
     res = []
-    for k, zc in enumerate((base, base, base + 1e-7 * rs.randn(nz), base + 0.05 * rs.randn(nz),
-                            rs.randn(nz), base)):
+    # (the last two with g = 0: coarse inputs with many exact ties, then a
+    # few of them moved -- tied runs through the repair)
+    coarse = np.round(base * 4) / 4
+    g0 = np.zeros(nz)
+    cases = [(base, g), (base, g), (base + 1e-7 * rs.randn(nz), g), (base + 0.05 * rs.randn(nz), g),
+             (rs.randn(nz), g), (base, g), (coarse, g0), (coarse + 0.25 * (rs.rand(nz) < 0.1), g0)]
+    for k, (zc, g) in enumerate(cases):
         eng.z[0][:nz].copy_(torch.from_numpy(zc))
         eng.g[1][:nz].copy_(torch.from_numpy(g))
         sc = np.zeros(_native.S_COUNT)

@@ -96,3 +96,15 @@ def test_split_is_needed(orc):
         yy[a], w[a] = y[a:b].mean(), b - a
     orc.isotonic_regression_multi_c(yy, starts, weight=w, update=1)
     assert np.max(np.abs(yy - _exact(orc, y, starts))) > 1e-3
+
+
+def test_repair_with_ties(orc):
+    """Inputs on a coarse grid (many exact ties: equal runs pool or not as the
+    passes meet them), kept partitions from a nearby tied input."""
+    rs = np.random.RandomState(9)
+    starts, n = _problem(rs)
+    base = np.round(rs.randn(n) * 4) / 4
+    heads = fit_heads(_exact(orc, base, starts), starts)
+    for y in (base, base + 0.25 * (rs.rand(n) < 0.1), np.round(rs.randn(n) * 2) / 2):
+        got = _from_state(orc, y, heads, starts)
+        assert np.max(np.abs(got - _exact(orc, y, starts))) <= 1e-12
