@@ -356,8 +356,13 @@ __global__ __launch_bounds__(256) void bb_k1_init(bsls_bb_problem P, int64_t r0,
 // g's columns of x in LDS; with one group it finishes the block itself,
 // otherwise it publishes its partials (rpart, sc1) and the last of the block's
 // G workgroups finishes (group order) -- as bb_k1.
+// BSLS_K1T_WGS (variant builds): the workgroups of 1024 threads a CU must
+// hold at once (2: registers capped so two tiles share a CU)
+#ifndef BSLS_K1T_WGS
+#define BSLS_K1T_WGS 1
+#endif
 template <int MODE, bool ITER, bool ADD, bool REDUCE, bool ATOM = false>
-__global__ __launch_bounds__(1024) void bb_k1t(bsls_bb_problem P, int64_t iter, unsigned *tkrb,
+__global__ __launch_bounds__(1024, BSLS_K1T_WGS) void bb_k1t(bsls_bb_problem P, int64_t iter, unsigned *tkrb,
                                                double *part, unsigned *ticket, int64_t rb_base) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ double red[32];   // (k1_finish: 2 doubles per wave)
