@@ -9,6 +9,8 @@ against HIP events recorded on the engine's stream at the window's two ends
 --prime: before each window's barrier/synchronize, a short untimed spin on the
 stream (the GPU busy right up to the window) -- whether an idle gap before
 the window costs device time.
+--preheat: ~100 ms of full-chip elementwise work before the warmup (diagnostic:
+whether the walks' slow first iterations are the chip's clocks settling).
 --hold: a ~0.5-ms spin enqueued before the window's first event, so the host
 has enqueued the whole window before the device reaches it (diagnostic: the
 device time without any wait on the host's launches)."""
@@ -31,12 +33,19 @@ def main():
     ap.add_argument('--windows', type=int, default=10)
     ap.add_argument('--prime', action='store_true')
     ap.add_argument('--hold', action='store_true')
+    ap.add_argument('--preheat', action='store_true')
     a = ap.parse_args()
     import torch
     import bench
     torch.cuda.set_device(0)
     sh, b = bench.build_problem('C3', 1, 0, None)
     eng, run = bench.build_engine(sh, b, 1, None, 1)
+    if a.preheat:
+        t = torch.empty(1 << 27, dtype=torch.float64, device='cuda')
+        for _ in range(250):
+            t.mul_(1.0000001)
+        torch.cuda.synchronize()
+        del t
     run(1, a.warmup)
     torch.cuda.synchronize()
     first = 1 + a.warmup
