@@ -11,6 +11,9 @@ stream (the GPU busy right up to the window) -- whether an idle gap before
 the window costs device time.
 --preheat: ~100 ms of full-chip elementwise work before the warmup (diagnostic:
 whether the walks' slow first iterations are the chip's clocks settling).
+--stage K: instead of the windows, stage K (3 = K2, 7 = K1) relaunched 300
+times on one state right after the engine's prologue (diagnostic, under a
+kernel trace: whether the walks' early-iteration trend needs the iterate).
 --hold: a ~0.5-ms spin enqueued before the window's first event, so the host
 has enqueued the whole window before the device reaches it (diagnostic: the
 device time without any wait on the host's launches)."""
@@ -34,6 +37,7 @@ def main():
     ap.add_argument('--prime', action='store_true')
     ap.add_argument('--hold', action='store_true')
     ap.add_argument('--preheat', action='store_true')
+    ap.add_argument('--stage', type=int, default=0)
     a = ap.parse_args()
     import torch
     import bench
@@ -46,6 +50,12 @@ def main():
             t.mul_(1.0000001)
         torch.cuda.synchronize()
         del t
+    if a.stage:
+        for _ in range(300):
+            eng.stage(a.stage, 1)
+        torch.cuda.synchronize()
+        print('stage %d relaunched 300 times' % a.stage)
+        return
     run(1, a.warmup)
     torch.cuda.synchronize()
     first = 1 + a.warmup
