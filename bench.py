@@ -856,6 +856,102 @@ def traffic_file():
     return fs[-1] if fs else None
 
 
+# The N > 1 self-check's problem: one column-sharded BB
+# problem, the same for every world size (synthetic.make_partitioned), large
+# enough that every rank's shard takes the C5 shards' kernels (dealt tiles, an
+# atomic K1 of several column groups, the int64 fixed-point r) and small
+# enough for the oracle to replay 20 iterations on rank 0 in a few seconds.
+SELFCHECK = dict(n=1_600_000, p=80_000, m=160_000, per_col=16, iters=20, tol=1e-6)
+
+
+def gather_z(z, dist, world):
+    """Every rank's z slice, concatenated in rank order on every rank (a
+    padded all_gather: the slices differ in length).  Tensors travel on the
+    GPU under nccl, on the host under gloo."""
+    import torch
+    dev = z.device if dist.get_backend() == 'nccl' else torch.device('cpu')
+    z = z.to(dev)
+    n = torch.tensor([z.numel()], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(v.item()) for v in ns]
+    pad = torch.zeros(max(ns), dtype=torch.float64, device=dev)
+    pad[:z.numel()] = z
+    parts = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return np.concatenate([p[:k].cpu().numpy() for p, k in zip(parts, ns)])
+
+
+def selfcheck_verdict(got, ref, tol):
+    """max over elements of |got - ref| / max(1, |ref|) (the iterate contract of
+    the north star, 1e-6) and whether it holds; a length mismatch fails."""
+    got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
+    if got.shape != ref.shape:
+        return float('inf'), False
+    err = float(np.max(np.abs(got - ref) / np.maximum(1.0, np.abs(ref)))) if ref.size else 0.0
+    return err, bool(np.isfinite(err) and err <= tol)
+
+
+def selfcheck_sharded(world, rank, dist, parts=1, problem=None):
+    """Before any timing at N > 1: a column-sharded BB problem through the
+    shipped transport -- RcclComm + bsls_bb_shard_iterate under nccl (the
+    five-sum and the int64 fixed-point r all-reduces of every iteration), the
+    callback transport under gloo -- for SELFCHECK['iters'] iterations; the
+    ranks' z slices gathered and compared on rank 0 with the oracle's
+    trajectory of the whole problem (python/BB.py:7-45 over main.py:53-65).
+    The oracle is the check leg only, outside every timed region.  Returns the
+    line's fields on every rank (the verdict broadcast from rank 0)."""
+    import torch
+    from synthetic import make_partitioned, add_noise, SEED
+    c = dict(SELFCHECK, **(problem or {}))
+    t0 = time.perf_counter()
+    with _StdoutToStderr():
+        sh = make_partitioned(c['n'], c['p'], c['m'], c['per_col'], rank=rank, world=world)
+        Ax = torch.from_numpy(sh['Ax']).cuda()
+        dist.all_reduce(Ax)
+        b = add_noise(Ax.cpu().numpy(), 0.02, seed=SEED)
+        eng, run = build_engine(sh, b, world, dist, parts)
+    comm = getattr(eng, '_comm', None)
+    run(1, c['iters'])
+    torch.cuda.synchronize()
+    z = gather_z(eng.current_z(c['iters'] & 1), dist, world)
+    sc = eng.scalars()
+    info = {'transport': type(comm).__name__ if comm is not None else 'torch.distributed',
+            'rccl_ranks': comm.count() if hasattr(comm, 'count') else None,
+            'r_fixed_point': bool(float(eng.P.r_fx) > 0),
+            'k1_groups': int(eng.A_til.img['ngroups']) if eng.A_til is not None else None,
+            'formats': [eng.fmt_A, eng.fmt_AT]}
+    if comm is not None:
+        comm.close()
+    del eng, run
+    torch.cuda.empty_cache()
+    v = torch.zeros(2, dtype=torch.float64)
+    if rank == 0:
+        from oracle import oracle as orc
+        full = make_partitioned(c['n'], c['p'], c['m'], c['per_col'])
+        ref = orc.bb_trace(full['A'], b, full['block_sizes'], c['iters'],
+                           record_every=c['iters'])[c['iters']]
+        err, ok = selfcheck_verdict(z, ref, c['tol'])
+        v[0], v[1] = err, 1.0 if ok else 0.0
+    v = v.cuda() if dist.get_backend() == 'nccl' else v
+    dist.broadcast(v, src=0)
+    # one verdict on every rank: rank 0's comparison, and a rank whose RCCL
+    # communicator counts other than the job's ranks fails it for all
+    mine = 1.0 if (info['rccl_ranks'] is None or info['rccl_ranks'] == world) else 0.0
+    flag = torch.tensor([mine * float(v[1].item())], dtype=torch.float64, device=v.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    err, ok = float(v[0].item()), bool(flag.item() == 1.0)
+    res = dict(info, err=err, ok=ok, tol=c['tol'], iters=c['iters'], finite=bool(np.isfinite(sc[4])),
+               problem='%d routes / %d blocks / %d links / %d nnz, column-sharded over %d ranks '
+                       '(synthetic.make_partitioned), 2 %% noise' % (c['n'], c['p'], c['m'],
+                                                                     c['per_col'] * c['n'], world),
+               seconds=time.perf_counter() - t0)
+    log('self-check: %s, %s ranks, fixed-point r %s, max elem err %.3e vs the oracle at '
+        'iteration %d -> %s' % (res['transport'], res['rccl_ranks'], res['r_fixed_point'], err,
+                                c['iters'], 'ok' if ok else 'MISMATCH'))
+    return res
+
+
 class _StdoutToStderr:
     """fd 1 -> fd 2 for a block: RCCL prints its version banner on stdout
     when it initialises, and bench.py's stdout must be the one JSON line."""
@@ -921,7 +1017,10 @@ def main():
         legs &= {'main', 'c5'}
     # (modulo: the gloo rehearsal puts several ranks on one GPU)
     local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
+    if torch.cuda.device_count():
+        torch.cuda.set_device(local)
+    # (no device: only the CPU tests of the line's contract get here, with
+    # the legs replaced; every leg itself needs the HIP library and a GPU)
     dist = None
     if world > 1 or args.rehearse_shard:
         import torch.distributed as dist
@@ -939,6 +1038,22 @@ def main():
     tfile = traffic_file()
     out = {} if rank == 0 else None
     wl = args.workload
+    if world > 1 and not args.rehearse_shard:
+        # parity before rate: the shipped transport against the oracle, before
+        # anything is timed; a mismatch ends the job non-zero on every rank
+        sc = selfcheck_sharded(world, rank, dist, parts=args.parts)
+        if rank == 0:
+            out.update({'selfcheck': sc, 'selfcheck_err': sc['err'],
+                        'rccl_ranks': sc['rccl_ranks']})
+        if not sc['ok']:
+            if rank == 0:
+                out.update({'metric': METRIC, 'value': None, 'n_gpus': world,
+                            'error': 'N > 1 self-check failed: the sharded iterate differs from '
+                                     'the oracle (max elem err %.3e > %.0e) or the communicator '
+                                     'spans another rank count' % (sc['err'], sc['tol'])})
+                print(json.dumps(out), flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
     if 'main' in legs:
         res = bench_workload(wl, args, world, rank, dist, tfile, args.steps,
                              shard_of=args.rehearse_shard or None)

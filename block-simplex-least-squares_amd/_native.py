@@ -202,7 +202,8 @@ _SIGS = {
     'bsls_comm_create_callback': (_int, [_int, _int, _vp, _vp, ctypes.POINTER(_vp)]),
     'bsls_comm_destroy': (_int, [_vp]),
     'bsls_comm_all_reduce': (_int, [_vp, _vp, _i64, _vp]),
-    'bsls_bb_shard_iterate': (_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp]),
+    'bsls_comm_count': (_int, [_vp, ctypes.POINTER(_int)]),
+    'bsls_bb_shard_iterate':(_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp]),
     'bsls_bb_k2_part': (_int, [ctypes.POINTER(BBProblem), _i64, _int, _vp]),
     'bsls_bb_k1_rows': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _i64, _vp]),
     'bsls_bb_shard_iterate_parts': (_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp,

@@ -43,6 +43,7 @@ struct RcclApi {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclGetErrorString) err = nullptr;
+    decltype(&ncclCommCount) count = nullptr;
 };
 
 static const RcclApi &rccl() {
@@ -57,6 +58,7 @@ static const RcclApi &rccl() {
         a.destroy = (decltype(a.destroy))dlsym(h, "ncclCommDestroy");
         a.all_reduce = (decltype(a.all_reduce))dlsym(h, "ncclAllReduce");
         a.err = (decltype(a.err))dlsym(h, "ncclGetErrorString");
+        a.count = (decltype(a.count))dlsym(h, "ncclCommCount");
         a.ok = a.get_id && a.init && a.destroy && a.all_reduce;
         return a;
     }();
@@ -81,6 +83,10 @@ struct bsls_comm {
     // the part pipeline's events (created on first use)
     bool events;
     hipEvent_t ev_k1[MAX_PARTS], ev_ar[MAX_PARTS];
+    // the last K2 image whose column groups were checked against the K1
+    // row-block parts (bsls_bb_shard_iterate_parts: one device read per image)
+    const int64_t *parts_gc;
+    int64_t parts_rb[MAX_PARTS + 1];
 };
 
 namespace bsls {
@@ -184,6 +190,19 @@ static int comm_sum(bsls_comm *c, double *buf, size_t count, hipStream_t st, boo
                                      c->comm, st));
 }
 
+// the ranks the communicator spans: RCCL's own count (ncclCommCount) for an
+// RCCL communicator -- what the library, not the caller, believes the job is
+extern "C" int bsls_comm_count(const bsls_comm *c, int *count_out) {
+    if (!c || !count_out) return BSLS_E_ARG;
+    if (c->fn || c->model) {
+        *count_out = c->world;
+        return BSLS_OK;
+    }
+    const RcclApi &R = rccl();
+    if (!R.count) return BSLS_E_COMM;
+    return comm_rc(R.count(c->comm, count_out));
+}
+
 extern "C" int bsls_comm_all_reduce(bsls_comm *c, double *buf, int64_t count, void *stream) {
     if (!c || !buf || count < 0) return BSLS_E_ARG;
     return comm_sum(c, buf, (size_t)count, (hipStream_t)stream);
@@ -249,6 +268,23 @@ extern "C" int bsls_bb_shard_iterate_parts(const bsls_bb_problem *p, bsls_comm *
     if (rb_bounds[0] != 0 || rb_bounds[nparts] != nrb) return BSLS_E_ARG;
     for (int q = 0; q < nparts; ++q)
         if (rb_bounds[q + 1] <= rb_bounds[q]) return BSLS_E_ARG;
+    // K2 part q waits only for exchange q, so its column group must be exactly
+    // the rows that exchange delivers: group_col[q] = min(rb_bounds[q] R, m).
+    // Checked once per (image, bounds): a mismatch would read rows of r whose
+    // all-reduce is still running on comm_stream.
+    bool same = c->parts_gc == p->ATt.group_col;
+    for (int q = 0; same && q <= nparts; ++q) same = c->parts_rb[q] == rb_bounds[q];
+    if (!same) {
+        int64_t gc[MAX_PARTS + 1];
+        BSLS_CHECK(hipMemcpy(gc, p->ATt.group_col, sizeof(int64_t) * (nparts + 1),
+                             hipMemcpyDeviceToHost));
+        for (int q = 0; q <= nparts; ++q) {
+            const int64_t want = rb_bounds[q] * R < p->m ? rb_bounds[q] * R : p->m;
+            if (gc[q] != want) return BSLS_E_ARG;
+        }
+        c->parts_gc = p->ATt.group_col;
+        for (int q = 0; q <= nparts; ++q) c->parts_rb[q] = rb_bounds[q];
+    }
     if (!c->events) {
         for (int q = 0; q < MAX_PARTS; ++q) {
             BSLS_CHECK(hipEventCreateWithFlags(&c->ev_k1[q], hipEventDisableTiming));

@@ -152,6 +152,10 @@ class ShardedBB:
         self.all_reduce = all_reduce
         self.all_reduce_async = all_reduce_async
         self.parts = int(parts) if (all_reduce_async is not None or self.native) else 1
+        if self.link and self.parts < 2:
+            # (the link pipeline needs its exchanges asynchronous: from Python
+            # through all_reduce_async, or the native driver's comm stream)
+            raise ValueError('link parts need all_reduce_async or a native communicator')
         if self.link and self.fuse != 2:
             raise ValueError('link parts run the sliced schedule (fuse 2)')
         self._slices = None
@@ -187,15 +191,30 @@ class ShardedBB:
         every |partial sum| of a row is at most |target_i| + |N z|max * sum_j
         |A_ij| over all ranks' columns (|N z| <= 2 (max|z0| + 1) in the
         prologue, <= 1 once K3 has clipped z), so the scale 2^k puts that bound
-        B below 2^61.  Collective: every rank computes the same B.
-        BSLS_SHARD_RFX=0 keeps r in doubles."""
+        B below 2^61.  Collective: every rank computes the same B, and the
+        choice itself is all-reduced first -- fixed point only if every rank's
+        engine can take it (fixed_r_ok depends on the rank's own shard: its K1
+        plan, its formats), else every rank keeps doubles; ranks that decided
+        alone would skip the others' all-reduces, or sum int64 words into
+        doubles.  BSLS_SHARD_RFX=0 keeps r in doubles.
+
+        Precision: one scale for all rows resolves every row to 2^-61 B
+        absolute; a row far below the largest bound carries more rounding than
+        a double sum would (|row| 2^-53) -- below 2^-61 B it is still within
+        the 1e-12 relative contract of any row above ~2^-21 B (see
+        test_gpu_shard_native's uneven-rows case)."""
+        import torch
         e = self.e
-        if os.environ.get('BSLS_SHARD_RFX', '1') == '0' or not hasattr(e, 'fixed_r_ok'):
-            return
-        if not e.fixed_r_ok():
+        ok = (os.environ.get('BSLS_SHARD_RFX', '1') != '0' and hasattr(e, 'fixed_r_ok')
+              and bool(e.fixed_r_ok()))
+        dev = getattr(e.r, 'device', 'cpu')
+        world = max(1, _world_size())
+        flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev)
+        if world > 1:
+            self.all_reduce(flag)
+        if float(flag.item()) != float(world):
             return
         import math
-        import torch
         A = e._A_host
         S = np.asarray(abs(A).sum(axis=1)).ravel()
         t = torch.from_numpy(S).to(e.r.device)
@@ -289,6 +308,16 @@ class ShardedBB:
             e.stage(9, first + count - 1)
 
 
+def comm_count(handle):
+    """bsls_comm_count: the ranks a C-ABI communicator spans."""
+    import ctypes
+    import _native
+    from _native import check
+    n = ctypes.c_int(0)
+    check(_native.lib().bsls_comm_count(handle, ctypes.byref(n)), 'bsls_comm_count')
+    return int(n.value)
+
+
 def torch_all_reduce(group=None):
     import torch.distributed as dist
 
@@ -356,6 +385,9 @@ class CallbackComm:
               'bsls_comm_create_callback')
         self.handle = h
 
+    def count(self):
+        return comm_count(self.handle)
+
     def close(self):
         import _native
         if self.handle is not None:
@@ -413,6 +445,10 @@ class RcclComm:
         h = ctypes.c_void_p()
         check(L.bsls_comm_create(raw, self.world, self.rank, ctypes.byref(h)), 'bsls_comm_create')
         self.handle = h
+
+    def count(self):
+        """The ranks RCCL says this communicator spans (ncclCommCount)."""
+        return comm_count(self.handle)
 
     def all_reduce(self, t):
         """In-place sum of a float64 device tensor over the ranks (current stream)."""

@@ -520,6 +520,10 @@ size_t bsls_comm_id_bytes(void);
 int bsls_comm_unique_id(void *id_out);
 int bsls_comm_create(const void *id, int world, int rank, bsls_comm **out);
 int bsls_comm_destroy(bsls_comm *comm);
+/* The ranks the communicator spans: RCCL's ncclCommCount for an RCCL
+ * communicator, the world it was created with for a callback / model one
+ * (bench.py's N > 1 self-check prints it as rccl_ranks). */
+int bsls_comm_count(const bsls_comm *comm, int *count_out);
 /* A communicator whose all-reduce is a host callback instead of RCCL (a
  * different transport -- MPI, gloo, a test double -- under the same C++
  * driver loop).  fn(d_buf, count, stream, user) must leave the sum over the
@@ -560,7 +564,11 @@ int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *comm, int64_t fir
  * exchange runs under K1's later parts and the next K2's earlier parts.
  * bsls_bb_shard_iterate_parts enqueues that (the exchanges on comm_stream,
  * ordered by events; rb_bounds: nparts + 1 host values from 0 to the K1 row
- * block count).  Parts must be launched in order on one stream. */
+ * block count).  Parts must be launched in order on one stream.
+ * bsls_bb_shard_iterate_parts returns BSLS_E_ARG unless the K2 image's
+ * group_col[q] == min(rb_bounds[q] R, m) for every q (read from the device
+ * once per image and bounds): a part whose columns reached past its exchange
+ * would race the all-reduce on comm_stream. */
 int bsls_bb_k2_part(const bsls_bb_problem *p, int64_t iter, int part, void *stream);
 int bsls_bb_k1_rows(const bsls_bb_problem *p, int64_t iter, int64_t rb0, int64_t rb1,
                     void *stream);

@@ -70,3 +70,115 @@ def test_time_run_windows_exact_steps():
     # warmup first, then four windows of exactly K iterations, consecutive
     assert calls == [(1, 5), (6, 20), (26, 20), (46, 20), (66, 20)]
     assert np.median(els) >= min(els)
+
+
+# ---- the N > 1 self-check ---------------------------------
+
+def test_selfcheck_verdict():
+    ref = np.linspace(-2.0, 3.0, 101)
+    assert bench.selfcheck_verdict(ref.copy(), ref, 1e-6) == (0.0, True)
+    got = ref.copy()
+    got[7] += 2e-6 * max(1.0, abs(ref[7]))
+    err, ok = bench.selfcheck_verdict(got, ref, 1e-6)
+    assert not ok and abs(err - 2e-6) < 1e-12
+    assert bench.selfcheck_verdict(ref[:-1], ref, 1e-6) == (float('inf'), False)
+    got = ref.copy()
+    got[3] = np.nan
+    assert not bench.selfcheck_verdict(got, ref, 1e-6)[1]
+
+
+def _gather_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    z = torch.arange(10 * rank, 10 * rank + 3 + 4 * rank, dtype=torch.float64)
+    q.put((rank, bench.gather_z(z, dist, world)))
+    dist.destroy_process_group()
+
+
+def test_gather_z_ragged_two_ranks():
+    """The ranks' z slices (different lengths) in rank order, on every rank."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 33000 + os.getpid() % 900
+    ps = [ctx.Process(target=_gather_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = np.concatenate([np.arange(0, 3), np.arange(10, 17)]).astype(np.float64)
+    for r in (0, 1):
+        assert np.array_equal(res[r], want)
+
+
+def _main_rank(rank, world, port, q, fail):
+    """bench.main() at N = 2 over gloo with the GPU legs replaced: the order of
+    the legs and the line's self-check fields."""
+    import io
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), BSLS_DIST_BACKEND='gloo')
+    calls = []
+
+    def fake_check(world_, rank_, dist, parts=1, problem=None):
+        calls.append('selfcheck')
+        return {'err': 3e-16 if not fail else 1e-3, 'ok': not fail, 'rccl_ranks': world_,
+                'tol': 1e-6, 'transport': 'fake'}
+
+    def fake_workload(wl, args, world_, rank_, dist, tfile, steps, shard_of=None):
+        calls.append('timed:' + wl)
+        return {'value': 1.0, 'unit': 'it/s'} if rank_ == 0 else None
+
+    bench.selfcheck_sharded = fake_check
+    bench.bench_workload = fake_workload
+    sys.argv = ['bench.py', '--gpus', str(world), '--steps', '2', '--warmup', '1']
+    buf, real = io.StringIO(), sys.stdout
+    sys.stdout = buf
+    code = 0
+    try:
+        bench.main()
+    except SystemExit as e:
+        code = e.code
+    finally:
+        sys.stdout = real
+    q.put((rank, code, calls, buf.getvalue()))
+
+
+def _run_main(fail):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 34000 + os.getpid() % 900 + 3 * int(fail)
+    ps = [ctx.Process(target=_main_rank, args=(r, 2, port, q, fail)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {item[0]: item[1:] for item in (q.get(timeout=180) for _ in ps)}
+    for p in ps:
+        p.join(timeout=60)
+    return res
+
+
+def test_main_n2_selfcheck_before_timing_and_in_the_line():
+    res = _run_main(False)
+    for r in (0, 1):
+        code, calls, _ = res[r]
+        assert code in (0, None)
+        # the check runs first, then the headline and the strong-scaling leg
+        assert calls == ['selfcheck', 'timed:C3', 'timed:C5'], calls
+    line = json.loads(res[0][2].strip().splitlines()[-1])
+    assert line['selfcheck_err'] == 3e-16 and line['rccl_ranks'] == 2
+    assert line['selfcheck']['ok'] and line['value'] == 1.0
+    assert res[1][2] == ''                      # one line, on rank 0 only
+
+
+def test_main_n2_selfcheck_mismatch_exits_nonzero_untimed():
+    res = _run_main(True)
+    for r in (0, 1):
+        code, calls, _ = res[r]
+        assert code == 3 and calls == ['selfcheck'], (code, calls)
+    line = json.loads(res[0][2].strip().splitlines()[-1])
+    assert line['value'] is None and line['selfcheck_err'] == 1e-3 and 'error' in line

@@ -442,3 +442,67 @@ def test_partitioned_problem_is_world_independent():
         for q in sh:
             C = q['A'].tocsc()
             assert np.array_equal(C.data, np.repeat(q['colv'], np.diff(C.indptr)))
+
+
+class _FxEngine:
+    """Just what ShardedBB._fix_r reads: whether this rank's engine can keep r
+    in fixed point, and the bound's inputs."""
+
+    def __init__(self, rank, ok):
+        import scipy.sparse as sps
+        self._ok = ok
+        self._A_host = sps.csr_matrix(np.array([[1.0, 2.0], [0.0, 3.0 + rank]]))
+        self.r = torch.zeros(2, dtype=torch.float64)
+        self.target = torch.tensor([0.5, -4.0], dtype=torch.float64)
+        self.z0 = torch.zeros(3, dtype=torch.float64)
+        self.scale = None
+
+    def fixed_r_ok(self):
+        return self._ok
+
+    def set_r_fixed(self, s):
+        self.scale = s
+
+
+def _fx_run(rank, world, port, q, oks):
+    sys.path.insert(0, PKG)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from distributed import ShardedBB
+    e = _FxEngine(rank, oks[rank])
+    drv = ShardedBB.__new__(ShardedBB)        # only the fixed-point decision
+    drv.e, drv._rank = e, rank
+    drv.all_reduce = lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    drv._fix_r()
+    # the ranks still agree on every later collective
+    t = torch.ones(1, dtype=torch.float64)
+    dist.all_reduce(t)
+    q.put((rank, e.scale, float(t.item())))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('oks', [(True, False), (False, True), (True, True)])
+def test_fixed_point_r_is_a_collective_choice(oks):
+    """fixed_r_ok depends on each rank's own shard, so the choice
+    is all-reduced -- fixed point only when every rank can take it, the same
+    scale on every rank; otherwise every rank keeps doubles (no rank skips
+    the others' all-reduces, no int64 words summed into doubles)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 31000 + (os.getpid() % 900) + 11 * (oks[0] + 2 * oks[1])
+    ps = [ctx.Process(target=_fx_run, args=(r, 2, port, q, oks)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {item[0]: item[1:] for item in (q.get(timeout=120) for _ in ps)}
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1] == 2.0
+    if all(oks):
+        # B = max(|target| + 2 (max|z0| + 1) sum over ranks of |A| row sums)
+        #   = max(0.5 + 2 * 6, 4 + 2 * 7) = 18 -> 2^(61 - 5)
+        assert res[0][0] == res[1][0] == 2.0 ** 56
+    else:
+        assert res[0][0] is None and res[1][0] is None

@@ -346,3 +346,84 @@ def test_link_parts_two_ranks_vs_oracle(cuda, orc, native):
     for i in CHECK5:
         got = np.concatenate([res[0][0][i], res[1][0][i]])
         assert elem_err(got, ref[i]) < 1e-6, (i, elem_err(got, ref[i]))
+
+
+def test_link_parts_reject_bounds_unlike_the_k2_groups(cuda):
+    """K2 part q waits only for exchange q, so the C entry point
+    refuses row-block bounds whose rows are not the K2 image's column groups
+    (BSLS_E_ARG) instead of racing the all-reduce on the comm stream."""
+    import ctypes
+    import torch
+    import _native
+    from device import BBEngine
+    from distributed import ModelComm
+    full, b, _ = _small()
+    eng = BBEngine(full['A'], b, full['block_sizes'], options={'max_iter': 10, 'opt_tol': 1e-30},
+                   early_exit=False, fmt='tiles', link_parts=3)
+    eng.set_shard_role(1)
+    comm = ModelComm(1, 0)
+    cs = torch.cuda.Stream()
+    lb = [int(v) for v in eng.k1_part_bounds]
+    L = _native.lib()
+
+    def call(bounds):
+        arr = (ctypes.c_int64 * 4)(*bounds)
+        return L.bsls_bb_shard_iterate_parts(eng.P, comm.handle, 1, 0, 3, arr,
+                                             ctypes.c_void_p(cs.cuda_stream),
+                                             _native.stream_handle())
+    try:
+        assert call(lb) == 0
+        moved = list(lb)
+        moved[1] += 1 if moved[2] - moved[1] > 1 else -1
+        assert moved[1] > 0 and moved[1] < moved[2]
+        assert call(moved) == _native.BSLS_E_ARG
+        assert call(lb) == 0                   # the right bounds still pass after a refusal
+    finally:
+        torch.cuda.synchronize()
+        comm.close()
+
+
+def _run_uneven(rank, world, port, out_q):
+    _setup(rank, world, port)
+    import torch
+    from synthetic import make_partitioned
+    full, b = _uneven()
+    kw = dict(per_col=8, seed=33, gen_chunks=8)
+    sh = make_partitioned(40_000, 2_000, 3_000, rank=rank, world=world, **kw)
+    x0 = np.zeros(sh['n'])
+    x0[np.cumsum(sh['block_sizes']) - 1] = 1.0
+    eng = _engine(sh['A'], sh['block_sizes'], b, x0, 10 ** 9, False, fmt='tiles')
+    eng.set_z0(torch.zeros(eng.nz, dtype=torch.float64))
+    drv, comm = _driver(eng, rank)
+    drv.prologue()
+    traj, done = {}, 0
+    for i in CHECK5:
+        drv.iterate(done + 1, i - done)
+        done = i
+        traj[i] = eng.current_z(i & 1).cpu().numpy().copy()
+    out_q.put((rank, traj, dict(r_fx=float(eng.P.r_fx))))
+    _finish(comm)
+
+
+def _uneven():
+    """The _small problem with b's first 30 links 10^6 times the rest: the
+    fixed-point r's one scale is set by them, so every other
+    row is resolved ~2^20 more coarsely than it would be alone."""
+    from synthetic import make_partitioned, add_noise
+    full = make_partitioned(40_000, 2_000, 3_000, per_col=8, seed=33, gen_chunks=8)
+    b = add_noise(full['Ax'], 0.02, seed=33)
+    b[:30] *= 1e6
+    return full, b
+
+
+@pytest.mark.timeout(600)
+def test_native_driver_fixed_point_r_uneven_rows_vs_oracle(cuda, orc):
+    res = _spawn(_run_uneven, 2)
+    for r in (0, 1):
+        assert res[r][1]['r_fx'] > 0
+    full, b = _uneven()
+    ref = orc.bb_trace(full['A'], b, full['block_sizes'], max(CHECK5), record_every=1)
+    for i in CHECK5:
+        got = np.concatenate([res[0][0][i], res[1][0][i]])
+        # the uneven scale costs resolution, not the contract
+        assert elem_err(got, ref[i]) < 1e-9, (i, elem_err(got, ref[i]))
