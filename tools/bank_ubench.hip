@@ -17,6 +17,9 @@
 //   perm 2: lanes assigned so each group of G lanes holds distinct row
 //           residues mod K (greedy over the column-sorted entries; entries
 //           stay in their instruction)
+//   perm 4: round robin -- the entries ordered by row residue mod K, item k
+//           to group k % (64 / G), each group's lanes in column order (the
+//           residues spread as evenly as counts allow)
 //   perm 3: synthetic rows: lane l's row = (random high bits) * K + l % K
 //           (the conflict-free bound for that (K, G) guess)
 //
@@ -130,6 +133,20 @@ int main(int argc, char **argv) {
                 int l = 0;
                 for (int g = 0; g < ng; ++g)
                     for (auto &e : grp[g]) o[l++] = e;
+            } else if (perm == 4) {
+                const int ng = 64 / G;
+                int ord[64];
+                for (int l = 0; l < 64; ++l) ord[l] = l;
+                std::stable_sort(ord, ord + 64, [&](int x, int y) {
+                    return in[x].second % K < in[y].second % K;
+                });
+                std::vector<std::vector<int>> grp(ng);
+                for (int k = 0; k < 64; ++k) grp[k % ng].push_back(ord[k]);
+                int l = 0;
+                for (int g = 0; g < ng; ++g) {
+                    std::sort(grp[g].begin(), grp[g].end());
+                    for (int x : grp[g]) o[l++] = in[x];
+                }
             } else {
                 for (int l = 0; l < 64; ++l) o[l] = in[l];
                 if (perm == 3)
