@@ -352,9 +352,13 @@ extern "C" int bsls_isotonic_packs(double *d_y, const int64_t *d_pk_start, const
     if (nlong > 0 && (!d_long_packs || !d_work || work_bytes < bsls_isotonic_workspace_size(n)))
         return BSLS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
-    // two packs per wave from 64k packs (several rounds of resident waves), as K3
-    const char *e = getenv("BSLS_K3_MERGE");
-    const bool merge = e ? atoi(e) != 0 : npacks >= 65536;
+    // two packs per wave from 64k packs (several rounds of resident waves), as
+    // K3; BSLS_K3_MERGE = 0 / 1 forces either form (A/B), read once per process
+    static const int env_merge = [] {
+        const char *e = getenv("BSLS_K3_MERGE");
+        return e ? (atoi(e) != 0 ? 1 : 0) : -1;
+    }();
+    const bool merge = env_merge >= 0 ? env_merge == 1 : npacks >= 65536;
     if (merge)
         iso_packs_kernel<2, true><<<grid_for(npacks, 8), 256, 0, st>>>(d_y, d_pk_start, d_pk_mask,
                                                                        d_pk_len, npacks);

@@ -42,3 +42,19 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip('no HIP device')
     return torch.device('cuda:0')
+
+
+@pytest.fixture(scope='session')
+def parity():
+    """parity(tag, err, tol): assert err <= tol and, with BSLS_PARITY_LOG set,
+    append {tag, err, tol} to that file (the measured errors the bounds were
+    set from: profiles/r06_parity_errors.jsonl)."""
+    import json
+    path = os.environ.get('BSLS_PARITY_LOG')
+
+    def check(tag, err, tol):
+        if path:
+            with open(path, 'a') as fh:
+                fh.write(json.dumps({'tag': tag, 'err': float(err), 'tol': float(tol)}) + '\n')
+        assert err <= tol, (tag, err, tol)
+    return check

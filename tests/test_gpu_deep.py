@@ -3,8 +3,9 @@ iteration counts).  Needs an MI355X.
 
 * C3 (BASELINE configs[2], 1M routes / 50k blocks / 100k links / 16M nnz),
   b = A x* exactly: BB iterates at 1, 10, 50 and 200 against the oracle's
-  restatement of python/BB.py over SciPy, within the north star's 1e-6, on the
-  default engine (dealt tiles) and the fixed-order one (panels);
+  restatement of python/BB.py over SciPy, on the default engine (dealt tiles)
+  and the fixed-order one, both at TOL_DEEP (1e-12 per element) -- the north
+  star allows 1e-6;
 * C5 (configs[4], 10M routes / 500k blocks / 1M links / 160M nnz), noise-free,
   iterates 1 and 10;
 * rank 0's and rank 1's shards of make_partitioned's C5-density 2-way split
@@ -31,6 +32,14 @@ def rel_err(a, b):
     return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
 
 
+# per-element bounds by iteration count, for every engine (the dealt tiles'
+# LDS-atomic sums included): what the runs measure with room for the run-to-run
+# order of those sums (profiles/r06_parity_errors.jsonl), not the north star's
+# 1e-6 -- a regression of a few orders of magnitude must fail
+# (round 6: every checkpoint measured <= 3e-15, C3 at 200 iterations 1.8e-15)
+TOL_DEEP = {1: 1e-12, 5: 1e-12, 10: 1e-12, 20: 1e-12, 50: 1e-12, 200: 1e-12}
+
+
 def _run_engine(eng, iters):
     rec = {}
 
@@ -53,21 +62,21 @@ def c3_clean(cuda, orc):
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize('deterministic', [False, True])
-def test_c3_noise_free_iterates_1_10_50_200(c3_clean, deterministic):
+def test_c3_noise_free_iterates_1_10_50_200(c3_clean, deterministic, parity):
     from device import BBEngine
     sh, b, ref = c3_clean
     eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 200, 'opt_tol': 1e-30},
                    AT=sh['AT'], deterministic=deterministic)
     rec = _run_engine(eng, 200)
-    # per element: the fixed-order engine at 1e-10 (measured ~1e-13), the
-    # default one (run-dependent atomic sums) at the north star's 1e-6
-    tol = 1e-10 if deterministic else 1e-6
+    # per element, both engines held to what they measure (TOL_DEEP), far
+    # inside the north star's 1e-6
     for i in (1, 10, 50, 200):
-        assert rel_err(rec[i], ref[i]) <= tol, (deterministic, i, rel_err(rec[i], ref[i]))
+        parity('c3_deep_%s_%d' % ('fixed' if deterministic else 'default', i),
+               rel_err(rec[i], ref[i]), TOL_DEEP[i])
 
 
 @pytest.mark.timeout(1200)
-def test_c5_noise_free_iterates_1_10(cuda, orc):
+def test_c5_noise_free_iterates_1_10(cuda, orc, parity):
     from synthetic import make_partitioned
     from device import BBEngine
     sh = make_partitioned(10_000_000, 500_000, 1_000_000)
@@ -78,7 +87,7 @@ def test_c5_noise_free_iterates_1_10(cuda, orc):
     del eng
     ref = orc.bb_trace(sh['A'], b, sh['block_sizes'], 10, record_every=1)
     for i in (1, 10):
-        assert rel_err(rec[i], ref[i]) < 1e-6, (i, rel_err(rec[i], ref[i]))
+        parity('c5_deep_%d' % i, rel_err(rec[i], ref[i]), TOL_DEEP[i])
 
 
 # ---- two ranks on the device over C5-density shards (make_partitioned) -------
@@ -125,7 +134,7 @@ def _run5(rank, world, port, out_q):
 
 
 @pytest.mark.timeout(900)
-def test_two_rank_c5_density_shards_vs_oracle(cuda, orc):
+def test_two_rank_c5_density_shards_vs_oracle(cuda, orc, parity):
     import torch.multiprocessing as mp
     from synthetic import make_partitioned
     ctx = mp.get_context('spawn')
@@ -147,4 +156,4 @@ def test_two_rank_c5_density_shards_vs_oracle(cuda, orc):
                        record_every=1)
     for i in CHECK5:
         got = np.concatenate([res[0][i], res[1][i]])
-        assert rel_err(got, ref[i]) < 1e-6, (i, rel_err(got, ref[i]))
+        parity('c5dens_2rank_python_%d' % i, rel_err(got, ref[i]), TOL_DEEP[i])

@@ -236,3 +236,13 @@ def test_lsq_fixed_point_dense_row_lined_up_remainders(cuda):
         outs.append(r.cpu().numpy().copy())
     np.testing.assert_allclose(outs[0], ref, rtol=1e-12, atol=0)
     assert exact(outs[0], outs[1])
+    # and against the reference's own arithmetic (SciPy csr_matvec, main.py:53):
+    # within the worst-case error of its left-to-right sum of a row's nnz
+    # non-negative terms, gamma_nnz = nnz 2^-53 / (1 - nnz 2^-53) relative
+    # (6.7e-11 for the dense row) -- the device's sum is the correctly rounded
+    # one, so the gap is SciPy's rounding, bounded by that
+    sp = A.dot(x)
+    for i in range(m):
+        nnz = A.indptr[i + 1] - A.indptr[i]
+        gam = nnz * 2.0 ** -53 / (1 - nnz * 2.0 ** -53)
+        assert abs(outs[0][i] - sp[i]) <= gam * abs(sp[i]), (i, outs[0][i], sp[i], gam)

@@ -108,3 +108,24 @@ def test_repair_with_ties(orc):
     for y in (base, base + 0.25 * (rs.rand(n) < 0.1), np.round(rs.randn(n) * 2) / 2):
         got = _from_state(orc, y, heads, starts)
         assert np.max(np.abs(got - _exact(orc, y, starts))) <= 1e-12
+
+
+def test_repair_near_ties_over_many_warm_starts(orc):
+    """a kept run that can be split only by a rounding margin
+    stays pooled under the repair's floating-point prefix test.  Inputs on a
+    coarse grid (exact ties) perturbed by ~1e-15 relative, 60 warm starts in a
+    row, each keeping the previous result's partition (as K3 does between
+    iterations): every fit within 1e-12 of the exact one."""
+    rs = np.random.RandomState(13)
+    starts, n = _problem(rs)
+    grid = np.round(rs.randn(n) * 4) / 4
+    heads = fit_heads(_exact(orc, grid, starts), starts)
+    worst = 0.0
+    for it in range(60):
+        y = grid * (1.0 + 1e-15 * rs.randn(n)) + 1e-15 * rs.randn(n) * (it % 3 == 0)
+        got = _from_state(orc, y, heads, starts)
+        err = np.max(np.abs(got - _exact(orc, y, starts)))
+        worst = max(worst, err)
+        assert err <= 1e-12 * max(1.0, np.max(np.abs(y))), (it, err)
+        heads = fit_heads(got, starts)
+    assert worst < 1e-13, worst
