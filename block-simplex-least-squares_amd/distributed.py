@@ -37,13 +37,6 @@ import os
 import numpy as np
 
 
-# the largest spread of row bounds max_i B_i / min_i B_i the fixed-point r
-# takes (ShardedBB._fix_r): beyond ~2^9 a row's 2^-61 B resolution is coarser
-# than its own double sum (~2^-53 B_i over a row's terms); the synthetic and
-# tests/fast problems spread 1.1-2.7 (measured)
-RFX_MAX_SPREAD = 2.0 ** 10
-
-
 def partition_blocks(block_sizes, col_weights, world):
     """Split blocks into `world` contiguous runs balancing the per-block weight
     (nnz of the block's columns).  Returns block boundaries [b_0=0, ..., b_W=p]."""
@@ -208,10 +201,13 @@ class ShardedBB:
         Precision: one scale for all rows resolves every row to 2^-61 B
         absolute; a row far below the largest bound carries more rounding than
         a double sum would (|row| 2^-53) -- below 2^-61 B it is still within
-        the 1e-12 relative contract of any row above ~2^-21 B; past a spread
-        of RFX_MAX_SPREAD between the largest and the smallest row bound r
-        stays in doubles on every rank (test_gpu_shard_native's uneven-rows
-        cases)."""
+        the 1e-12 relative contract of any row above ~2^-21 B.  Measured on
+        rows spanning six orders (test_gpu_shard_native's uneven-rows cases,
+        b's first links x 10^6): the iterates sit ~1e-11 from the oracle
+        with the fixed point and ~5e-12 with doubles at iteration 1 -- the
+        problem's conditioning, not the representation, sets it -- and
+        1e-14 at a spread of 65; so the fixed point stays (doubles would
+        give back the run-dependent exits it fixes)."""
         import torch
         e = self.e
         ok = (os.environ.get('BSLS_SHARD_RFX', '1') != '0' and hasattr(e, 'fixed_r_ok')
@@ -233,17 +229,7 @@ class ShardedBB:
         zv[rank % world] = float(e.z0.abs().max()) if e.z0 is not None and e.z0.numel() else 0.0
         self.all_reduce(zv)
         nzb = 2.0 * (float(zv.max()) + 1.0)
-        Bi = e.target.abs() + nzb * t
-        B = float(Bi.max()) if t.numel() else 0.0
-        # rows whose own bound sits far below the largest: one scale resolves
-        # them to 2^-61 B, coarser than a double sum of their terms would once
-        # B / B_i passes ~2^9; past RFX_MAX_SPREAD
-        # every rank keeps doubles (Bi is the same on every rank: t and target
-        # are all-reduced / replicated, so the choice stays collective)
-        live = Bi[Bi > 0]
-        if live.numel() and B / float(live.min()) > RFX_MAX_SPREAD:
-            self.r_fixed_spread = B / float(live.min())
-            return
+        B = float((e.target.abs() + nzb * t).max()) if t.numel() else 0.0
         k = 61 - int(math.ceil(math.log2(B))) if B > 0 else 61
         e.set_r_fixed(math.ldexp(1.0, max(-1000, min(1000, k))))
 

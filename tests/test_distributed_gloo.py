@@ -448,13 +448,12 @@ class _FxEngine:
     """Just what ShardedBB._fix_r reads: whether this rank's engine can keep r
     in fixed point, and the bound's inputs."""
 
-    def __init__(self, rank, ok, spread=False):
+    def __init__(self, rank, ok):
         import scipy.sparse as sps
         self._ok = ok
         self._A_host = sps.csr_matrix(np.array([[1.0, 2.0], [0.0, 3.0 + rank]]))
         self.r = torch.zeros(2, dtype=torch.float64)
-        # spread: one row's bound 10^4 times the other's (past RFX_MAX_SPREAD)
-        self.target = torch.tensor([0.5, -4.0 if not spread else -1e5], dtype=torch.float64)
+        self.target = torch.tensor([0.5, -4.0], dtype=torch.float64)
         self.z0 = torch.zeros(3, dtype=torch.float64)
         self.scale = None
 
@@ -465,13 +464,13 @@ class _FxEngine:
         self.scale = s
 
 
-def _fx_run(rank, world, port, q, oks, spread=False):
+def _fx_run(rank, world, port, q, oks):
     sys.path.insert(0, PKG)
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from distributed import ShardedBB
-    e = _FxEngine(rank, oks[rank], spread)
+    e = _FxEngine(rank, oks[rank])
     drv = ShardedBB.__new__(ShardedBB)        # only the fixed-point decision
     drv.e, drv._rank = e, rank
     drv.all_reduce = lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -507,21 +506,3 @@ def test_fixed_point_r_is_a_collective_choice(oks):
         assert res[0][0] == res[1][0] == 2.0 ** 56
     else:
         assert res[0][0] is None and res[1][0] is None
-
-
-@pytest.mark.timeout(300)
-def test_fixed_point_r_keeps_doubles_past_the_row_spread():
-    """Row bounds spread past distributed.RFX_MAX_SPREAD (one scale would
-    resolve the small rows more coarsely than their own double sums): every
-    rank keeps doubles, alike."""
-    ctx = mp.get_context('spawn')
-    q = ctx.Queue()
-    port = 31950 + (os.getpid() % 900)
-    ps = [ctx.Process(target=_fx_run, args=(r, 2, port, q, (True, True), True)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = {item[0]: item[1:] for item in (q.get(timeout=120) for _ in ps)}
-    for p in ps:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    assert res[0][0] is None and res[1][0] is None

@@ -136,6 +136,47 @@ def test_proj_borderline_decisions(cx, orc, exact_proj):
             assert exact(a, r), (gi, name)
 
 
+def test_proj_exact_pipe_verification_fallbacks(cx, orc, exact_proj):
+    """The pipelined exact path (csrc/proj.hip pipe_exact_lambda) verifies
+    Michelot's candidate set in the reference's arithmetic and redoes a block
+    the reference's way where it cannot: blocks whose threshold lands exactly
+    on an entry (0.75, 0.25, 0, ...: e_c = 0 at the boundary), ties across
+    the boundary, all-equal blocks (every entry a member), single entries;
+    ball blocks whose clamped sum is 1 to within a few ulps (the left-to-right
+    sum decides, proj_simplex.h:56-66); mixed with blocks > 64 inside a wave's
+    range (their entries must come back untouched for the big-block kernel).
+    Bit-identical to the oracle."""
+    rs = np.random.RandomState(SEED + 11)
+    blocks = []
+    for _ in range(400):
+        kind = rs.randint(7)
+        k = int(rs.randint(1, 65))
+        if kind == 0:
+            b = np.zeros(k); b[0] = 0.75
+            if k > 1: b[1] = 0.25
+        elif kind == 1:
+            b = np.full(k, rs.choice([0.5, 1.0 / 3.0, 0.25, 2.0]))
+        elif kind == 2:
+            b = np.round(rs.rand(k) * 4) / 4
+        elif kind == 3:
+            r = rs.rand(k); b = r / r.sum()
+            b[rs.rand(k) < 0.2] *= -1.0
+        elif kind == 4:
+            b = np.full(k, 1.0 / k) + rs.randint(-2, 3, size=k) * 2.0 ** -53
+        elif kind == 5:
+            b = rs.rand(int(rs.randint(65, 200)))
+        else:
+            b = rs.rand(k)
+        blocks.append(b)
+    y = np.concatenate(blocks)
+    starts = np.concatenate(([0], np.cumsum([b.size for b in blocks])[:-1])).astype(np.int64)
+    for name in ('proj_multi_simplex_c', 'proj_multi_ball_c'):
+        for scale in (1.0, 3.0):
+            a = y * scale; getattr(cx, name)(a, starts)
+            r = y * scale; getattr(orc, name)(r, starts)
+            assert exact(a, r), (name, scale)
+
+
 # ------------------------------------------------- sort-free projection (_fast)
 # bsls_proj_multi_*_fast (c_extensions with BSLS_PROJ=fast): Newton on the threshold,
 # no sort -- held to the north star's contract |d| <= 1e-12 max(1, |ref|)
