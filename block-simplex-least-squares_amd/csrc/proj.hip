@@ -1006,20 +1006,12 @@ __global__ __launch_bounds__(256, BSLS_PROJ_MINW) void proj_thr_kernel(double *_
 #define BSLS_PIPE_KO 0    // 1: no threshold passes (knock-out timing build, results wrong)
 #endif
 constexpr int PIPE_LPB = BSLS_PIPE_LPB, PIPE_EB = 64 / PIPE_LPB, PIPE_BPG = WAVE / PIPE_LPB;
-// PIPE_STAGE: the LDS buffer's entries per wave (a group's range up to it
-// goes through LDS); BSLS_PIPE_STAGE overrides it for the A/B builds
-#ifndef BSLS_PIPE_STAGE
-#define BSLS_PIPE_STAGE (PIPE_BPG * 64)
-#endif
-constexpr int PIPE_STAGE = BSLS_PIPE_STAGE, PIPE_NL = PIPE_STAGE / WAVE;
-static_assert(PIPE_STAGE % WAVE == 0, "the LDS stage is whole wave rows");
 
 struct PipeGroup {
     __amdgpu_buffer_rsrc_t rs;   // the group's range [s0, e1) of y (scalar registers)
     int base;                    // this lane's byte offset of its slot 0
     int k;                       // this lane's block length (0: none, or a big block)
     int len;                     // e1 - s0 (wave-uniform; clamped to 2^30)
-    int big_lo, big_hi;          // a big block's entries [lo, hi) in the range (else 0, 0)
 };
 
 // lanes 0 .. PIPE_BPG: the starts of group q's blocks and the end of its last
@@ -1064,9 +1056,6 @@ __device__ __forceinline__ PipeGroup pipe_setup(double *y, long long st, int64_t
     G.base = (int)(s - s0 + j) * 8;
     G.k = (b < nb && !big) ? (int)kk : 0;
     G.len = (int)((e1 - s0) < ((int64_t)1 << 30) ? e1 - s0 : ((int64_t)1 << 30));
-    const bool bigr = big && b < nb;
-    G.big_lo = bigr ? (int)(s - s0) : 0;
-    G.big_hi = bigr ? (int)(e - s0) : 0;
     return G;
 }
 
@@ -1083,214 +1072,10 @@ struct PipeOut {
     int ne;        // this lane's live slots
 };
 
-// ---- the exact lambda on the pipelined layout (round 6) --------------------
-// The reference's lambda (proj_simplex.h:22-31) depends on two things only:
-// rho, the LAST i >= 1 with u_i + (1 - S_i)/(i + 1) > 0 in its arithmetic,
-// and S_rho = u_0 + ... + u_rho summed left to right in descending order.
-// Michelot's passes hand over a candidate: the set {v > tau} of the last pass,
-// c members, necessarily the block's c largest.  The members alone are then
-// sorted (each one's rank by counting, in the wave's LDS stage, which the
-// slots have already been read out of), summed left to right -- S_{c-1}
-// exactly as the reference forms it -- and the candidate is verified in the
-// reference's own arithmetic: the test at i = c - 1 holds (with its division,
-// as the reference computes it), and at i = c, with u_c the largest
-// non-member, the computed e_c = fl((c + 1) u_c + 1 - S_c) < -margin, which
-// (lane_block_lds's chain argument: e_i is non-increasing, margin bounds
-// every rounding of S_i, 1 - S_i and the test) makes every later test false
-// too.  Then rho = c - 1 and lambda = fl(fl(1 - S_{c-1}) / c), the
-// reference's bits (c = 1: 1 - u_0, the reference's initial value; / 1 is
-// exact).  A group whose candidate does not verify (a test within rounding
-// of its threshold) redoes its block the reference's way: every entry
-// ranked, the full loop with a division per i.  The ball variant's "does the
-// clamped block sum past 1" (proj_simplex.h:56-66, a left-to-right sum) is
-// decided on the tree sum when it clears 1 by more than either sum's rounding
-// (k 2^-52 S), else by the left-to-right sum itself.  Bit-identical to the
-// sorting kernels (tests/test_gpu_kernels.py test_proj_pipe_exact_*).
-//
-// scr: the wave's LDS stage (PIPE_STAGE + WAVE doubles), free once the slots
-// are in registers.  Members of group g sit at [M_g, M_g + c_g), sorted at
-// C + [M_g, M_g + c_g) (C: the wave's members); a wave with 2 C past the
-// stage (blocks of mostly equal values) takes the per-group path for all.
-constexpr int PIPE_SCR = PIPE_STAGE + WAVE;
-
-// inclusive sum over the lanes 0 .. j of this lane's 8-lane group
-__device__ __forceinline__ int grp_scan_incl(int x, int j) {
-    int y = __shfl_up(x, 1, PIPE_LPB);
-    x += (j >= 1) ? y : 0;
-    y = __shfl_up(x, 2, PIPE_LPB);
-    x += (j >= 2) ? y : 0;
-    y = __shfl_up(x, 4, PIPE_LPB);
-    x += (j >= 4) ? y : 0;
-    return x;
-}
-
-// Rank and sort the group's c members (at scr[base ..), any order) into
-// scr[dst ..) descending: member t goes to the count of members above it
-// (ties by index).  Member t is lane t % 8's, assignment t / 8; maxc the
-// wave's largest c (the loops' bound, wave-uniform).
-__device__ __forceinline__ void grp_rank_sort(double *scr, int base, int dst, int c, int maxc,
-                                              int j) {
-    for (int a = 0; a * PIPE_LPB < maxc; ++a) {
-        const int t = a * PIPE_LPB + j;
-        const bool own = t < c;
-        const double w = scr[base + (own ? t : 0)];
-        int r = 0;
-        for (int s = 0; s < maxc; s += 4) {
-            double u[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) u[q] = scr[base + min(s + q, c > 0 ? c - 1 : 0)];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = s + q;
-                r += (i < c) & ((u[q] > w) | ((u[q] == w) & (i < t))) ? 1 : 0;
-            }
-        }
-        if (own) scr[dst + r] = w;
-    }
-}
-
-// the reference's loop (proj_simplex.h:22-31) over c sorted values at scr[d ..)
-// (every lane of the group alike): the fallback of an unverified candidate
-__device__ __forceinline__ double grp_lambda_full(const double *scr, int d, int c, int maxc) {
-    double run = scr[d];
-    double lam = 1. - run;
-    for (int i = 1; i < maxc; ++i) {
-        const double u = scr[d + min(i, c - 1)];
-        if (i < c) {
-            run = run + u;
-            const double cand = (1. - run) / ((double)i + 1.);
-            if (u + cand > 0) lam = cand;
-        }
-    }
-    return lam;
-}
-
-// The per-group path: group g (lanes 8 g .. 8 g + 7) ranks all k of its live
-// entries into scr[0 ..) and scr[64 ..) and runs the reference's loop; the
-// other groups idle (rare: an unverified candidate, an ambiguous ball sum, or
-// a wave whose members overflow the stage).
-template <int EB>
-__device__ __forceinline__ double grp_exact_full(double *scr, const double (&v)[EB], int ne, int k,
-                                                 int j) {
-    const int incl = grp_scan_incl(ne, j);
-    int pos = incl - ne;
-#pragma unroll
-    for (int e = 0; e < EB; ++e)
-        if (e < ne) scr[pos++] = v[e];
-    grp_rank_sort(scr, 0, WAVE, k, k, j);
-    return grp_lambda_full(scr, WAVE, k, k);
-}
-
-// The exact lambda of every group of the wave (see above).  v: the lane's
-// slots (PAD past the block), tau: the threshold of Michelot's last pass, k:
-// the block length (0: none / a big block), need: project (ball: decided here).
-template <bool BALL>
-__device__ __forceinline__ double pipe_exact_lambda(double *scr, const double (&v)[PIPE_EB], int ne,
-                                                    int k, double tau, bool active, int j,
-                                                    int lane) {
-    const int g = lane / PIPE_LPB;
-    // members: the last pass's set, the block's c largest
-    int m = 0;
-    double um = -INFINITY, mx = 0.0;
-#pragma unroll
-    for (int e = 0; e < PIPE_EB; ++e) {
-        const bool live = e < ne;
-        const bool mem = active && live && v[e] > tau;
-        m += mem ? 1 : 0;
-        um = (live && !mem && v[e] > um) ? v[e] : um;      // the largest non-member
-        mx = (live && fabs(v[e]) > mx) ? fabs(v[e]) : mx;
-    }
-    const int incl = grp_scan_incl(m, j);
-    const int cg = __shfl(incl, (lane & ~(PIPE_LPB - 1)) + PIPE_LPB - 1, WAVE);
-    um = grp_max_d<PIPE_LPB>(um);
-    mx = grp_max_d<PIPE_LPB>(mx);
-    // the groups' member offsets and the wave's total (scalar)
-    int Mg = 0, C = 0, maxc = 0;
-#pragma unroll
-    for (int h = 0; h < PIPE_BPG; ++h) {
-        const int sh = __builtin_amdgcn_readlane(incl, h * PIPE_LPB + PIPE_LPB - 1);
-        Mg += (h < g) ? sh : 0;
-        C += sh;
-        maxc = sh > maxc ? sh : maxc;
-    }
-    double lam = 0.0;
-    bool ok = false;
-    if (2 * C <= PIPE_SCR) {
-        int pos = Mg + incl - m;
-#pragma unroll
-        for (int e = 0; e < PIPE_EB; ++e)
-            if (active && e < ne && v[e] > tau) scr[pos++] = v[e];
-        grp_rank_sort(scr, Mg, C + Mg, cg, maxc, j);
-        // S_{c-1} left to right over the sorted members (every lane of the
-        // group alike), and u_{c-1}
-        const int d = C + Mg;
-        double S = scr[d], ulast = S;
-        for (int i = 1; i < maxc; i += 4) {
-            double u[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) u[q] = scr[d + min(i + q, cg > 0 ? cg - 1 : 0)];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (i + q < cg) {
-                    S = S + u[q];
-                    ulast = u[q];
-                }
-            }
-        }
-        const double D = 1. - S;
-        const double cd = (double)cg;
-        // the reference's test at i = c - 1 (none at c = 1: its initial lambda)
-        const bool at_rho = (cg <= 1) || (ulast + D / cd > 0);
-        // every later test false: settled at i = c (none past the block)
-        const double kk = (double)k;
-        const double margin = kk * 0x1p-49 * (1. + 2. * kk * mx);
-        const double Sc = S + um;
-        const double E = __builtin_fma(cd + 1., um, 1. - Sc);
-        const bool settled = (cg >= k) || (E < -margin);
-        ok = at_rho && settled && cg >= 1;
-        lam = (cg <= 1) ? D : D / cd;
-    }
-    // the rest the reference's way, one group at a time
-    const bool redo = active && !ok;
-    if (__builtin_amdgcn_ballot_w64(redo)) {
-#pragma unroll 1
-        for (int h = 0; h < PIPE_BPG; ++h) {
-            if (!__builtin_amdgcn_readlane((int)redo, h * PIPE_LPB)) continue;
-            if (g == h) lam = grp_exact_full<PIPE_EB>(scr, v, ne, k, j);
-        }
-    }
-    return lam;
-}
-
-// The ball's "project at all": the clamped block's left-to-right sum > 1
-// (proj_simplex.h:56-66).  S: the group's tree sum of the clamped entries;
-// decided on it where it clears 1 by more than either sum's rounding, else
-// by the reference's own sum (entry order through scr, every group at once:
-// entry i of group g at scr[64 g + i]).
-__device__ __forceinline__ bool ball_need_exact(double *scr, const double (&v)[PIPE_EB], int ne,
-                                                int k, double S, int j, int lane) {
-    const double tol = (double)k * 0x1p-52 * S + 0x1p-1000;
-    const bool amb = k > 0 && fabs(S - 1.0) <= tol;
-    if (!__builtin_amdgcn_ballot_w64(amb)) return S > 1.0;
-    const int g = lane / PIPE_LPB;
-#pragma unroll
-    for (int e = 0; e < PIPE_EB; ++e)
-        if (e < ne) scr[WAVE * g + j + PIPE_LPB * e] = v[e];
-    double acc = 0.0;
-    for (int i = 0; i < WAVE; ++i) {
-        if (!__builtin_amdgcn_ballot_w64(i < k)) break;
-        const double t = scr[WAVE * g + min(i, k > 0 ? k - 1 : 0)];
-        acc += (i < k) ? t : 0.0;
-    }
-    return amb ? acc > 1.0 : S > 1.0;
-}
-
 // Michelot's passes on this lane's slots of its block (v: the entries, slots
-// past the block anything -- they become PAD; the ball variant clamps them).
-// EXACT: lambda (and the ball's decision) the reference's bits, through scr.
-template <bool BALL, bool EXACT = false>
-__device__ __forceinline__ PipeOut pipe_threshold(int k, double (&v)[PIPE_EB], int j,
-                                                  double *scr = nullptr) {
+// past the block anything -- they become PAD; the ball variant clamps them)
+template <bool BALL>
+__device__ __forceinline__ PipeOut pipe_threshold(int k, double (&v)[PIPE_EB], int j) {
     constexpr double PAD = -1.7976931348623157e308;   // below every entry, finite
     const int ne = (k > j) ? (k - j + PIPE_LPB - 1) / PIPE_LPB : 0;
     double S = 0.0;
@@ -1302,9 +1087,7 @@ __device__ __forceinline__ PipeOut pipe_threshold(int k, double (&v)[PIPE_EB], i
         v[e] = ok ? v[e] : PAD;
     }
     S = grp_sum_d<PIPE_LPB>(S);
-    bool need;
-    if constexpr (BALL && EXACT) need = ball_need_exact(scr, v, ne, k, S, j, lane_id());
-    else need = !BALL || S > 1.0;
+    const bool need = !BALL || S > 1.0;
     // the slots any lane of the wave holds (wave-uniform: past them every
     // slot is padding, skipped by a scalar branch instead of computed)
     int nslot = 0;
@@ -1337,9 +1120,7 @@ __device__ __forceinline__ PipeOut pipe_threshold(int k, double (&v)[PIPE_EB], i
         double cprev = from_set ? (lm ? -1.0 : kd) : 1.0;
         tau = fmin(tau, Mdn);
         double c = cprev;
-        double tu = tau;   // the threshold of the last pass run (EXACT: its set)
         for (int pass = 0; pass <= (BSLS_PIPE_KO ? -1 : PIPE_LPB * PIPE_EB); ++pass) {
-            tu = tau;
             double sl = 0.0, cl = 0.0;
 #pragma unroll
             for (int e = 0; e < PIPE_EB; ++e) {
@@ -1356,18 +1137,14 @@ __device__ __forceinline__ PipeOut pipe_threshold(int k, double (&v)[PIPE_EB], i
             tau = fmin((S - 1.0) / c, Mdn);
             if (!__builtin_amdgcn_ballot_w64(more)) break;
         }
-        if constexpr (EXACT)
-            lam = pipe_exact_lambda<BALL>(scr, v, ne, k, tu, need && k > 0, j, lane_id());
-        else
-            lam = (1. - S) / c;
+        lam = (1. - S) / c;
     }
     return PipeOut{need, lam, ne};
 }
 
-template <bool BALL, bool EXACT = false>
-__device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_EB], int j,
-                                           double *scr = nullptr) {
-    const PipeOut o = pipe_threshold<BALL, EXACT>(G.k, v, j, scr);
+template <bool BALL>
+__device__ __forceinline__ void pipe_solve(const PipeGroup &G, double (&v)[PIPE_EB], int j) {
+    const PipeOut o = pipe_threshold<BALL>(G.k, v, j);
     const bool need = o.need;
     const double lam = o.lam;
     const int ne = o.ne;
@@ -1437,6 +1214,13 @@ __global__ __launch_bounds__(256, 2) void proj_pipe_kernel(double *__restrict__ 
 // group longer than PIPE_STAGE entries (big blocks inside) takes the direct
 // path.  Entries of big blocks inside the range go back unchanged (the big-
 // block kernel that follows in the stream projects them).
+// PIPE_STAGE: the LDS buffer's entries per wave (a group's range up to it
+// goes through LDS); BSLS_PIPE_STAGE overrides it for the A/B builds
+#ifndef BSLS_PIPE_STAGE
+#define BSLS_PIPE_STAGE (PIPE_BPG * 64)
+#endif
+constexpr int PIPE_STAGE = BSLS_PIPE_STAGE, PIPE_NL = PIPE_STAGE / WAVE;
+static_assert(PIPE_STAGE % WAVE == 0, "the LDS stage is whole wave rows");
 
 // the group's range by coalesced 8-B loads (lane l, load e: entry 64 e + l;
 // past the range the hardware returns 0)
@@ -1450,7 +1234,7 @@ __device__ __forceinline__ void lds_range_load(const PipeGroup &G, double (&t)[P
 // the results back into the slots and the range out by coalesced
 // write-through stores (a wave's own LDS accesses execute in order: no
 // barrier, and the next group may reuse the buffer right after)
-template <bool BALL, bool EXACT = false>
+template <bool BALL>
 __device__ __forceinline__ void lds_group(const PipeGroup &G, const double (&t)[PIPE_NL],
                                           double *buf, int lane, int j) {
 #pragma unroll
@@ -1459,51 +1243,32 @@ __device__ __forceinline__ void lds_group(const PipeGroup &G, const double (&t)[
     const int b0 = min(G.base / 8, PIPE_STAGE);
 #pragma unroll
     for (int e = 0; e < PIPE_EB; ++e) v[e] = buf[b0 + PIPE_LPB * e];
-    const PipeOut o = pipe_threshold<BALL, EXACT>(G.k, v, j, buf);
+    const PipeOut o = pipe_threshold<BALL>(G.k, v, j);
 #pragma unroll
     for (int e = 0; e < PIPE_EB; ++e)
         if (e < o.ne) buf[b0 + PIPE_LPB * e] = o.need ? relu_ref(o.lam + v[e]) : v[e];
-    // EXACT used the stage as scratch: the entries of a big block inside the
-    // range (projected later by proj_large_kernel, not in registers here) are
-    // not stored back (rare: a wave-uniform branch)
-    uint64_t keep = ~0ull;
-    if constexpr (EXACT) {
-        if (__builtin_amdgcn_ballot_w64(G.big_hi > G.big_lo)) {
-#pragma unroll
-            for (int h = 0; h < PIPE_BPG; ++h) {
-                const int lo = __builtin_amdgcn_readlane(G.big_lo, h * PIPE_LPB);
-                const int hi = __builtin_amdgcn_readlane(G.big_hi, h * PIPE_LPB);
-#pragma unroll
-                for (int e = 0; e < PIPE_NL; ++e) {
-                    const int i = WAVE * e + lane;
-                    if (i >= lo && i < hi) keep &= ~(1ull << e);
-                }
-            }
-        }
-    }
 #pragma unroll
     for (int e = 0; e < PIPE_NL; ++e) {
         const int i = WAVE * e + lane;
-        const bool st = i < G.len && ((keep >> e) & 1ull);
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(HIP_vector_type<unsigned, 2>::Native_vec_, buf[i]), G.rs,
-            st ? i * 8 : 0x7FFFFFF0, 0, BSLS_PIPE_STORE_AUX);
+            i < G.len ? i * 8 : 0x7FFFFFF0, 0, BSLS_PIPE_STORE_AUX);
     }
 }
 
 // one group either way: through LDS when its range fits the buffer, else
 // straight into the lanes' registers (pipe_load / pipe_solve)
-template <bool BALL, bool EXACT = false>
+template <bool BALL>
 __device__ __forceinline__ void pipe_group_one(const PipeGroup &G, double *buf, int lane, int j) {
     if (G.len > PIPE_STAGE) {
         double v[PIPE_EB];
         pipe_load(G, v);
-        pipe_solve<BALL, EXACT>(G, v, j, buf);
+        pipe_solve<BALL>(G, v, j);
         return;
     }
     double t[PIPE_NL];
     lds_range_load(G, t, lane);
-    lds_group<BALL, EXACT>(G, t, buf, lane, j);
+    lds_group<BALL>(G, t, buf, lane, j);
 }
 
 // The same group through LDS (round 5, the default fast form; BSLS_PROJ_PIPE_LDS):
@@ -1514,7 +1279,7 @@ __device__ __forceinline__ void pipe_group_one(const PipeGroup &G, double *buf, 
 // PIPE_STAGE entries (big blocks inside) takes the direct path.  Entries of
 // big blocks inside the range go back unchanged (the big-block kernel that
 // follows in the stream projects them).
-template <bool BALL, bool BIG, bool EXACT = false>
+template <bool BALL, bool BIG>
 __global__ __launch_bounds__(256, 2) void proj_pipe_lds_kernel(double *__restrict__ y,
                                                               const int64_t *__restrict__ starts,
                                                               int64_t nb, int64_t n,
@@ -1531,7 +1296,7 @@ __global__ __launch_bounds__(256, 2) void proj_pipe_lds_kernel(double *__restric
     if (q >= ngrp) return;
     const PipeGroup G = pipe_setup<BIG>(y, pipe_meta(starts, nb, n, q, lane), q, nb, big_list,
                                         big_count, true, lane);
-    pipe_group_one<BALL, EXACT>(G, stage[wv], lane, j);
+    pipe_group_one<BALL>(G, stage[wv], lane, j);
 }
 
 struct ProjWork {
@@ -1608,23 +1373,6 @@ static int proj_launch(double *y, const int64_t *starts, int64_t nb, int64_t n,
         return (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) ? v : 1;
     }();
     const int64_t ngrp = (nb + WAVE - 1) / WAVE;
-    // the bit-identical path on the pipelined layout (round 6: Michelot's
-    // candidate verified in the reference's arithmetic, pipe_exact_lambda)
-    // unless BSLS_PROJ_EXACT_PIPE=0 (A/B: the lane-per-block sorting kernel)
-    static const int exact_pipe = [] {
-        const char *e = getenv("BSLS_PROJ_EXACT_PIPE");
-        return e ? atoi(e) : 1;
-    }();
-    if (!fast && exact_pipe && max_block <= ((int64_t)1 << 24)) {
-        const int64_t groups = (nb + PIPE_BPG - 1) / PIPE_BPG;
-        const unsigned g1 = (unsigned)((groups + 3) / 4);
-        if (max_block > SMALL_MAX)
-            proj_pipe_lds_kernel<BALL, true, true><<<g1, 256, 0, st>>>(y, starts, nb, n, w.list,
-                                                                      w.count, gate);
-        else
-            proj_pipe_lds_kernel<BALL, false, true><<<g1, 256, 0, st>>>(y, starts, nb, n, w.list,
-                                                                       w.count, gate);
-    } else
     // (its group ranges must stay below 2 GB of y: max_block bounds them)
     if (fast && lpb == 0 && pipe > 0 && max_block <= ((int64_t)1 << 24)) {
         const int64_t groups = (nb + PIPE_BPG - 1) / PIPE_BPG;

@@ -7,6 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 T="python -u -m pytest -x -v --timeout 600 --timeout-method thread"
 timeout -k 10 600 $T tests/test_gpu_kernels.py -k "proj" > gpurun_out/r6f_proj_tests.log 2>&1 || exit 1
+timeout -k 10 600 $T tests/test_gpu_shard_native.py -k uneven > gpurun_out/r6f_uneven.log 2>&1 || exit 1
 for ep in 1 0 1 0; do
   BSLS_PROJ_EXACT_PIPE=$ep timeout -k 10 240 python -u bench.py --legs proj > gpurun_out/r6f_proj_ep$ep.json 2> gpurun_out/r6f_proj_ep$ep.err || exit 1
   python -c "
