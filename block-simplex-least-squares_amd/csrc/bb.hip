@@ -71,8 +71,8 @@ static BBWork bb_layout(void *base, int64_t m, int64_t n, int64_t nz) {
     off += al16((size_t)(m / 16 + 2) * 4);
     w.tk2rb = (unsigned *)(p + off);             // K2 tiles: one ticket per row block (H >= 64)
     off += al16((size_t)(n / 64 + 2) * 4);
-    // K1's per-row-block partials of ||r||^2 (and sy_dr's ||dr||^2): two per
-    // row block, and a row block holds >= 16 rows (16 panels of >= 1 row;
+    // K1's per-row-block partials of ||r||^2: one per row block (two slots
+    // reserved), and a row block holds >= 16 rows (16 panels of >= 1 row;
     // tiles of >= 64 rows)
     w.p1 = (double *)(p + off);
     off += al16((size_t)(m / 16 + 2) * 2 * 8);
@@ -167,23 +167,18 @@ __device__ __forceinline__ void k1_stopped_rows(const bsls_bb_problem &P, int64_
 // the G partials of each row summed in group order (from rpart, or from LDS
 // `local` when the block had one group) + target; its share of ||r||^2 goes
 // to the last row block, which records f and runs the stopping test.
-// (sy_dr, REDUCE: sq[1] = ||r - r_prev||^2 over the rows, r_prev read as r is
-// overwritten -- scal[DD] for the next K2; `red` holds 2 doubles per wave)
 template <bool ADD, bool REDUCE>
 __device__ __forceinline__ void k1_finish(const bsls_bb_problem &P, int64_t iter, bool iterating,
                                           int64_t rb, unsigned nrb, int64_t r0, int64_t r1,
                                           int64_t G, const double *local, double *part,
                                           unsigned *ticket, double *red) {
-    double sq[2] = {0.0, 0.0};
-    const bool dr = REDUCE && P.sy_dr;
+    double sq[1] = {0.0};
     if (local) {
         for (int64_t row = r0 + threadIdx.x; row < r1; row += blockDim.x) {
             double o = local[row - r0];
             if (ADD) o += P.target[row];
-            const double d = dr ? o - P.r[row] : 0.0;
             P.r[row] = o;
             sq[0] += o * o;
-            sq[1] += d * d;
         }
     } else {
         // up to RPT rows per thread, every partial load of them in flight at once
@@ -212,20 +207,16 @@ __device__ __forceinline__ void k1_finish(const bsls_bb_problem &P, int64_t iter
                     o += __hip_atomic_load(&P.rpart[c * P.m + row], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 if (ADD) o += P.target[row];
-                const double d = dr ? o - P.r[row] : 0.0;
                 P.r[row] = o;
                 sq[0] += o * o;
-                sq[1] += d * d;
             }
         }
     }
     if (!REDUCE) return;
-    block_sum<2>(sq, red);
-    double tot[2];
-    if (last_of_sum<2>(sq, part, (unsigned)rb, nrb, ticket, tot, red) && threadIdx.x == 0) {
-        if (dr) P.scal[BSLS_S_DD] = tot[1];
+    block_sum<1>(sq, red);
+    double tot[1];
+    if (last_of_sum<1>(sq, part, (unsigned)rb, nrb, ticket, tot, red) && threadIdx.x == 0)
         bb_record_f(P, iter, tot[0], iterating);
-    }
 }
 
 // K1: workgroup (group g = blockIdx % ngroups, panels 16 rb .. 16 rb + 15)
@@ -304,17 +295,15 @@ __global__ __launch_bounds__(256) void bb_k1_sum(bsls_bb_problem P, int64_t iter
                         (int64_t)gridDim.x * blockDim.x);
         return;
     }
-    const bool dr = REDUCE && P.sy_dr;   // (as k1_finish)
     // grid-stride rows: with REDUCE the launch is capped at K1_SUM_GRID
     // workgroups (one per 256 rows made 3.9k arrivals at the ||r||^2 tickets
     // at m = 1M: 12.5 us against 4.6 without the reduction)
     const int64_t gs = (int64_t)gridDim.x * blockDim.x;
-    double sq[2] = {0.0, 0.0};
+    double sq[1] = {0.0};
     for (int64_t row = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < r1; row += gs) {
         double v[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) v[c] = (c < G) ? P.rpart[c * P.m + row] : 0.0;
-        const double rp = dr ? P.r[row] : 0.0;
         double o = v[0];
 #pragma unroll
         for (int c = 1; c < 8; ++c)
@@ -322,17 +311,13 @@ __global__ __launch_bounds__(256) void bb_k1_sum(bsls_bb_problem P, int64_t iter
         for (int64_t c = 8; c < G; ++c) o += P.rpart[c * P.m + row];
         if (ADD) o += P.target[row];
         P.r[row] = o;
-        const double d = dr ? o - rp : 0.0;
         sq[0] += o * o;
-        sq[1] += d * d;
     }
     if (!REDUCE) return;
-    block_sum<2>(sq, red);
-    double tot[2];
-    if (last_block_sum<2>(sq, part, ticket, tot, red) && threadIdx.x == 0) {
-        if (dr) P.scal[BSLS_S_DD] = tot[1];
+    block_sum<1>(sq, red);
+    double tot[1];
+    if (last_block_sum<1>(sq, part, ticket, tot, red) && threadIdx.x == 0)
         bb_record_f(P, iter, tot[0], ITER);
-    }
 }
 
 // K1 with global atomics (BSLS_K1_ATOMIC): rows [r0, r1) of r start as
@@ -624,7 +609,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
                 gq[q] = dq[q] = 0.0;
                 if (ITER && jq[q] >= 0) {
                     gq[q] = gp[jq[q]];
-                    if (dzv) dq[q] = dzv[jq[q]];   // (none: sy_dr, scal[DD] below)
+                    if (dzv) dq[q] = dzv[jq[q]];
                 }
             }
 #pragma unroll
@@ -687,7 +672,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
             sc[BSLS_S_RR] = tot[4];
         }
         P.scal[BSLS_S_SUMDG] = tot[0];
-        P.scal[BSLS_S_DZDG] = dzv ? tot[1] : P.scal[BSLS_S_DD];
+        P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
         P.scal[BSLS_S_GG] = tot[3];
     }
@@ -808,7 +793,7 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
         for (int q = 0; q < 4; ++q) {
             const int32_t jc = j[q] >= 0 ? j[q] : 0;
             gpj[q] = gp[jc];
-            dzj[q] = dzv ? dzv[jc] : 0.0;   // (none: sy_dr)
+            dzj[q] = dzv ? dzv[jc] : 0.0;
         }
     }
 #pragma unroll
@@ -855,7 +840,7 @@ __global__ __launch_bounds__(1024) void bb_k2(bsls_bb_problem P, const double *_
             sc[BSLS_S_RR] = tot[4];
         }
         P.scal[BSLS_S_SUMDG] = tot[0];
-        P.scal[BSLS_S_DZDG] = dzv ? tot[1] : P.scal[BSLS_S_DD];
+        P.scal[BSLS_S_DZDG] = tot[1];
         P.scal[BSLS_S_DGDG] = tot[2];
         P.scal[BSLS_S_GG] = tot[3];
     }
@@ -1077,13 +1062,11 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
                 P.x + z0[q] + b0[q], 0, (L[q] + nb) * 8, 0x00020000);
             if (act) {
                 wt_store_f64(rz, l * 8, v);
-                if (!P.sy_dr) {   // (sy_dr: the next K2 takes ||dr||^2 instead)
 #if BSLS_DZ_PLAIN
-                    dzo[z0[q] + l] = v - zv[q];
+                dzo[z0[q] + l] = v - zv[q];
 #else
-                    wt_store_f64(rd, l * 8, v - zv[q]);   // next K2's z - z_prev
+                wt_store_f64(rd, l * 8, v - zv[q]);   // next K2's z - z_prev
 #endif
-                }
                 const double d = v - (bstart ? 0.0 : vprev);
                 const int xo = (l + bl) * 8;
                 wt_store_f64(rx, xo, P.colv ? cv[q] * d : d);
@@ -1103,7 +1086,7 @@ void bb_k3(bsls_bb_problem P, int64_t iter,
             for (int64_t j = z0[q]; j < z0[q] + L[q]; ++j) {
                 const double v = clip01(zn[j]);
                 zn[j] = v;
-                if (!P.sy_dr) dzo[j] = v - zc[j];
+                dzo[j] = v - zc[j];
                 x_put(P, xo++, v - prev);
                 prev = v;
             }
@@ -1140,7 +1123,7 @@ __global__ __launch_bounds__(LONG_T) void bb_k3_long(bsls_bb_problem P, int64_t 
     for (int64_t j = threadIdx.x; j < L; j += LONG_T) {
         const double v = clip01(zn[z0 + j]);
         zn[z0 + j] = v;
-        if (!P.sy_dr) dzo[z0 + j] = v - zc[z0 + j];
+        dzo[z0 + j] = v - zc[z0 + j];
     }
     __syncthreads();
     const int64_t xs = P.xstarts[b0];
@@ -1309,8 +1292,7 @@ template <bool ITER, int FUSE = 0>
 static void launch_k2(const bsls_bb_problem &P, const double *gp, double *gout,
                       const BBWork &w, hipStream_t st, int64_t iter = 0,
                       const double *dz = nullptr, int gsel = -1) {
-    // (sy_dr: the iteration's K2 takes dz . dg from scal[DD] and reads no dz)
-    if (!dz) dz = (P.sy_dr && ITER && FUSE == 0) ? nullptr : w.dz;
+    if (!dz) dz = w.dz;
     if (P.ATt.ent) {
         if (!P.colv) launch_k2t_mode<1, ITER, FUSE>(P, gp, gout, w, st, iter, dz, gsel);
         else if (P.ATt.ngroups == 1 && P.ATt.layout == 0)
@@ -1385,12 +1367,9 @@ static int check_problem(const bsls_bb_problem *p) {
         return BSLS_E_ARG;
     if (p->colv_codec < 0 || p->colv_codec > 2 || (p->colv_codec && (!p->colv_n || !p->colv)))
         return BSLS_E_ARG;
-    // ||dr||^2 for dz . dg: every K1 that records f must see r_prev as it
-    // overwrites r -- the ordered finishes of one GCD, not an atomic K1 (r
-    // initialised first) nor a shard's partial residual
-    if (p->sy_dr < 0 || p->sy_dr > 1) return BSLS_E_ARG;
-    if (p->sy_dr && (p->shard_role != 0 || (p->At.ent && p->At.ngroups > 1 && k1_atomic(*p, true))))
-        return BSLS_E_ARG;
+    // (sy_dr, dz . dg as ||r - r_prev||^2, retired in round 6: it moved where
+    // the reference's exact-zero sum(delta_g) exit fires, BB.py:22)
+    if (p->sy_dr != 0) return BSLS_E_ARG;
     const bool general = p->colv == nullptr;
     if (p->At.ent) {
         if (!tiles_valid(p->At, p->m, p->n, 0, general, false, PANEL_LDS_MAX)) return BSLS_E_ARG;
@@ -1703,7 +1682,6 @@ extern "C" int bsls_dore_iterate(const bsls_bb_problem *p, const bsls_dore_state
     hipStream_t st = (hipStream_t)stream;
     const BBWork w = bb_layout(*p);
     bsls_bb_problem PS = *p, P2 = *p, PE = *p;
-    PS.sy_dr = P2.sy_dr = PE.sy_dr = 0;   // (DORE's K3 / K1 keep dz and r as the reference)
     PS.scal = d->S;
     PE.scal = d->S;
     PE.r = d->err;                       // K2 reads err as its r
@@ -1782,7 +1760,6 @@ extern "C" int bsls_lbfgs_ls_trials(const bsls_bb_problem *p, const bsls_ls_stat
     // the trial's problems: S1 gates K3 / K1 (and takes f), S2 gates K2; no
     // stopping rule of their own (max_iter unreachable, no early exits)
     bsls_bb_problem P1 = *p, P2 = *p;
-    P1.sy_dr = P2.sy_dr = 0;   // (the trials' K2 dots g(pt) with d itself)
     P1.scal = s->S1;
     P2.scal = s->S2;
     P1.max_iter = P2.max_iter = INT64_MAX;

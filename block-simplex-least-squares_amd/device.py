@@ -886,7 +886,7 @@ class BBEngine:
     def __init__(self, A, b, block_sizes, options=None, early_exit=True, A_dev=None,
                  AT_dev=None, AT=None, target=None, x0=None, general=False, fmt=None,
                  tile_plans=(None, None), colv=None, deterministic=False, tile_layouts=None,
-                 link_parts=None, sy_dr=None):
+                 link_parts=None):
         torch = _torch()
         L = _native.lib()
         self.layout = lay = BlockLayout(block_sizes)
@@ -1066,14 +1066,6 @@ class BBEngine:
         for field, env in (('k1_atomic', 'BSLS_K1_ATOMIC'), ('k3_merge', 'BSLS_K3_MERGE')):
             v = os.environ.get(env)
             setattr(P, field, 0 if v is None else (2 if int(v) else 1))
-        # dz . dg as ||r - r_prev||^2 (bsls_bb_problem.sy_dr: no dz hand-off
-        # between K3 and K2; whole problem, ordered K1 sums) only when asked,
-        # BSLS_SY_DR=1: the same step in exact arithmetic, but at the noise
-        # floor it never produces the exact-zero sum(dg) that ends the
-        # reference's runs (BB.py:22) -- C3 noise-free ran to max_iter 50000 at
-        # f 4.6e-21 where dz . dg exits at 13830.  set_shard_role clears it.
-        sy = os.environ.get('BSLS_SY_DR') if sy_dr is None else int(bool(sy_dr))
-        P.sy_dr = 1 if (sy is not None and int(sy)) and P.k1_atomic != 2 else 0
         self.P = P
         self.z0 = None
         if xin is not None:
@@ -1163,8 +1155,6 @@ class BBEngine:
         if role not in (0, 1, 2):
             raise ValueError('shard role must be 0, 1 or 2')
         self.P.shard_role = int(role)
-        if role:
-            self.P.sy_dr = 0   # (a shard's K1 forms a partial residual: dz . dg from dz)
 
     def row_blocks(self):
         """(K1 row blocks, rows per block): the granule of residual_rows."""

@@ -163,7 +163,7 @@ enum {
     BSLS_S_WARN = 10,      /* count of |t| outside [1e-10, 1e10] (BB.py:27-28) */
     BSLS_S_PSUMDG = 11,    /* stage 10: iteration i - 1's SUMDG, DZDG, DGDG, GG (11..14) */
     BSLS_S_PDZDG = 12, BSLS_S_PDGDG = 13, BSLS_S_PGG = 14,
-    BSLS_S_DD = 15,        /* sy_dr: ||r - r_prev||^2 from the last K1 (= the next delta_z . delta_g) */
+    BSLS_S_DD = 15,        /* unused (was sy_dr's ||r - r_prev||^2, retired in round 6) */
     BSLS_S_COUNT = 16
 };
 enum {
@@ -390,13 +390,11 @@ typedef struct bsls_bb_problem {
      * and a dealt K2 image; every |partial sum| must stay below 2^62 / r_fx
      * (distributed.ShardedBB sizes it from the rows' abs-sums).  0: doubles. */
     double r_fx;
-    /* 1: delta_z . delta_g from the residuals -- dz'dg = dz'N'A'(r - r_prev) =
-     * ||r - r_prev||^2 since A N dz = r - r_prev (target cancels) -- summed by
-     * K1's finish as it overwrites r (scal[BSLS_S_DD]) and taken by the next
-     * K2, so K3 writes no dz (nz doubles) and K2 gathers none: 16 nz bytes
-     * per iteration for 8 m.  Whole problem on one GCD only (shard_role 0, K1
-     * by ordered group sums; the DORE and line-search launches keep dz).
-     * 0: K2 sums dz . dg from K3's dz (the reference's expression). */
+    /* reserved, must be 0 (BSLS_E_ARG otherwise).  Round 5's opt-in delta_z .
+     * delta_g as ||r - r_prev||^2 (equal in exact arithmetic) moved where the
+     * reference's exact-zero sum(delta_g) exit fires (BB.py:22) and was
+     * retired in round 6; K2 sums dz . dg from K3's dz, the reference's
+     * expression. */
     int64_t sy_dr;
 } bsls_bb_problem;
 

@@ -198,7 +198,6 @@ def test_k3_wave_pava_bit_exact(cuda, orc, monkeypatch, merge):
     m = 200
     A = sps.random(m, n, density=0.02, random_state=rs, format='csr')
     eng = BBEngine(A, rs.randn(m), sizes, options={'max_iter': 10, 'opt_tol': 1e-30})
-    eng.P.sy_dr = 0          # (the dz hand-off: K3 writes it only without sy_dr)
     nz = eng.nz
     for trial in range(5):
         zc = np.cumsum(rs.rand(nz)) * 0.01 if trial == 0 else rs.randn(nz)
@@ -417,54 +416,3 @@ def test_stored_value_codecs_vs_oracle(cuda, orc, codec, parity):
     N = orc.block_sizes_to_N(sh['block_sizes'])
     want = N.T.tocsr().dot(A.T.tocsr().dot(r))
     assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
-
-
-def test_sy_dr_identity(cuda, shard100k):
-    """bsls_bb_problem.sy_dr: dz . dg = ||r - r_prev||^2 (A N dz = r - r_prev).
-    K1's finish records scal[DD] = ||r_new - r_old||^2 as it overwrites r,
-    K3 writes no dz, and the iterates match the dz . dg engine and the oracle
-    (per element 1e-10 on the fixed-order panels, where only the sums' order
-    and this identity differ)."""
-    import torch
-    import _native
-    from device import BBEngine
-    sh, b, ref = shard100k
-    # the K1 finish's sum
-    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 5, 'opt_tol': 1e-30},
-                   fmt='panels')
-    assert eng.P.sy_dr == 0          # (opt-in: BSLS_SY_DR=1)
-    eng.P.sy_dr = 1
-    r_old = np.random.RandomState(8).randn(eng.m)
-    eng.r.copy_(torch.from_numpy(r_old))
-    x = np.random.RandomState(6).rand(eng.n)
-    eng.x.copy_(torch.from_numpy(eng.colv.cpu().numpy() * x))
-    eng.stage(7, 0)
-    r_new = eng.r.cpu().numpy()
-    dd = float(eng.scal[_native.S_DD])
-    want = float(np.sum((r_new - r_old) ** 2))
-    assert abs(dd - want) <= 1e-12 * want, (dd, want)
-    # K3 leaves the dz hand-off alone
-    off = _native.load().bsls_bb_dz_offset(eng.m, eng.n, eng.nz)
-    dzb = eng.work[off:off + 8 * eng.nz].view(torch.float64)
-    dzb.fill_(float('nan'))
-    sc = np.zeros(_native.S_COUNT)
-    sc[_native.S_SUMDG], sc[_native.S_DZDG], sc[_native.S_DGDG] = 1.0, 0.5, 1.0
-    eng.scal.copy_(torch.from_numpy(sc))
-    eng.stage(4, 1)
-    assert bool(torch.isnan(dzb).all())
-    # whole runs, both ways
-    outs = {}
-    for sy in (1, 0):
-        e = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 50, 'opt_tol': 1e-30},
-                     fmt='panels')
-        e.P.sy_dr = sy
-        rec = {}
-
-        def log(i, s, dt):
-            rec[i] = s
-            return 0.0
-        e.solve(log=log, record_every=1, poll=1)
-        outs[sy] = rec
-    for i in (1, 10, 50):
-        assert elem_err(outs[1][i], ref[i]) <= 1e-10, (i, elem_err(outs[1][i], ref[i]))
-        assert elem_err(outs[1][i], outs[0][i]) <= 1e-10, i

@@ -130,7 +130,6 @@ def test_c3_k3_warm_start_within_ulps(c3, orc):
     base = rs.rand(nz)
     g = rs.randn(nz)
     warm, eng.P.pava_warm = eng.P.pava_warm, 1
-    sy, eng.P.sy_dr = eng.P.sy_dr, 0          # (the dz hand-off K3 writes without sy_dr)
     outs = []
     try:
         for k, eps in enumerate((0.0, 0.0, 1e-6, 1e-3)):
@@ -152,7 +151,6 @@ def test_c3_k3_warm_start_within_ulps(c3, orc):
             outs.append((got, want))
     finally:
         eng.P.pava_warm = warm
-        eng.P.sy_dr = sy
     # the repeated input took the warm path: its means round differently
     # somewhere from the reference's pooled sequence
     assert not np.array_equal(outs[1][0], outs[1][1])
