@@ -42,7 +42,7 @@ import numpy as np  # noqa: E402
 
 # BASELINE.json's metric text, verbatim; `value` is its 1M-route (C3) rate
 METRIC = 'BB solver iterations/sec (1M-route block-LSQ) + proj_simplex HBM GB/s'
-ROUND = 'r05'
+ROUND = 'r06'
 HBM_PEAK = 8.0e12   # MI355X_MICROARCH.md chip table (spec)
 
 

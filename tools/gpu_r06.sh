@@ -1,10 +1,10 @@
 #!/bin/bash
-# One GPU-box session (round 5): parity tests, smoke, bench, and one rocprofv3
-# kernel-trace run per workload (profiles/r05_<key>_kernel_stats.csv), so a
+# One GPU-box session (round 6): parity tests, smoke, bench, and one rocprofv3
+# kernel-trace run per workload (profiles/r06_<key>_kernel_stats.csv), so a
 # kernel name's rows never mix workloads.  Every GPU step runs under its own
 # timeout; a crash / timeout / abort ends the script (no further GPU work), an
 # ordinary test failure (pytest rc 1) does not.
-#   STEPS="tests smoke bench prof" tools/gpu_r03.sh
+#   STEPS="tests smoke bench prof pmc pmcx sq" tools/gpu_r06.sh
 #   PROF="C5 C3 C2 C4iso md_xs C5x8" (the prof step's workloads)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -31,7 +31,7 @@ prof() {  # prof <key> <bench args...>
     echo "prof $key rc=$rc" | tee -a $OUT/status.txt; fatal $rc
     local f
     f=$(find $OUT/prof_$key -name '*kernel_stats.csv' | head -n 1)
-    [ -n "$f" ] && cp "$f" $OUT/r05_${key}_kernel_stats.csv
+    [ -n "$f" ] && cp "$f" $OUT/r06_${key}_kernel_stats.csv
     return 0
 }
 
@@ -75,7 +75,7 @@ for s in $STEPS; do
               -- python3 tools/kprof.py --config $cfg --iters 10 $extra > $OUT/pmc_${cfg}_$i.log 2>&1
           rc=$?; echo "pmc $cfg $i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
         done
-        python3 tools/traffic.py $cfg $OUT/traffic_r05.json $OUT/pmc_${cfg}_1 $OUT/pmc_${cfg}_2 \
+        python3 tools/traffic.py $cfg $OUT/traffic_r06.json $OUT/pmc_${cfg}_1 $OUT/pmc_${cfg}_2 \
             > /dev/null 2> $OUT/traffic_$cfg.err
       done
       # rank 0 of the 8-way C5 split (the rehearsal bench.py --rehearse-shard 8
@@ -89,9 +89,30 @@ for s in $STEPS; do
               -- python3 bench.py --rehearse-shard 8 --steps 30 --warmup 5 --windows 1 > $OUT/pmc_C5x8_$i.log 2>&1
           rc=$?; echo "pmc C5x8 $i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
         done
-        python3 tools/traffic.py C5_x8 $OUT/traffic_r05.json $OUT/pmc_C5x8_1 $OUT/pmc_C5x8_2 \
+        python3 tools/traffic.py C5_x8 $OUT/traffic_r06.json $OUT/pmc_C5x8_1 $OUT/pmc_C5x8_2 \
             > /dev/null 2> $OUT/traffic_C5x8.err
       fi ;;
+    pmcx)
+      # rank 0's kernels for every N-GPU line the driver can print (C3 weak
+      # shards, C5 strong shards; N = 2, 4, 8) over the one-GPU rehearsal of
+      # that rank, merged into traffic_r06.json as '<workload>_x<N>'
+      for wl in C3 C5; do
+        for n in 2 4 8; do
+          [ "$wl$n" = C58 ] && continue      # (C5_x8: the pmc step's)
+          i=0
+          for grp in FETCH_SIZE WRITE_SIZE; do
+            i=$((i+1))
+            d=$OUT/pmcx_${wl}_${n}_$i
+            rm -rf $d
+            timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d $d -o pmc \
+                -- python3 bench.py --rehearse-shard $n --rehearse-workload $wl --steps 30 --warmup 5 --windows 1 \
+                > $d.log 2>&1
+            rc=$?; echo "pmcx $wl $n $i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
+          done
+          python3 tools/traffic.py ${wl}_x$n $OUT/traffic_r06.json $OUT/pmcx_${wl}_${n}_1 $OUT/pmcx_${wl}_${n}_2 \
+              > /dev/null 2> $OUT/traffic_${wl}x$n.err
+        done
+      done ;;
     sq)
       # SQ occupancy / issue / wait counters over the C3 kernels, the C2
       # projection and the planned standalone PAVA (two passes, 8 SQ each)
@@ -104,7 +125,7 @@ for s in $STEPS; do
             -- python3 tools/kprof.py --config C3 --iters 5 --proj 5 --iso 10 > $OUT/sq_$i.log 2>&1
         rc=$?; echo "sq $i rc=$rc" | tee -a $OUT/status.txt; fatal $rc
       done
-      python3 tools/pmc_summary.py $OUT/sq_1 $OUT/sq_2 > $OUT/r05_sq_summary_C3.txt 2>&1 ;;
+      python3 tools/pmc_summary.py $OUT/sq_1 $OUT/sq_2 > $OUT/r06_sq_summary_C3.txt 2>&1 ;;
     prof)
       for k in $PROF; do
         case "$k" in
