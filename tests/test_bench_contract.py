@@ -27,7 +27,7 @@ def _kern(us):
 
 def test_traffic_file_is_the_default_builds():
     f = bench.traffic_file()
-    assert f is not None and os.path.basename(f) == 'traffic_r05.json'   # not traffic_r05_sydr.json
+    assert f is not None and os.path.basename(f) == 'traffic_r06.json'   # the newest round's
 
 
 def test_traffic_keys_cover_every_line_the_driver_prints():
