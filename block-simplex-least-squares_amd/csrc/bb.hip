@@ -436,6 +436,16 @@ __global__ __launch_bounds__(1024, BSLS_K1T_WGS) void bb_k1t(bsls_bb_problem P, 
 // rest), stored with the sums as scal[RR] for the all-reduce; the last
 // workgroup keeps iteration iter - 1's sums in scal[PSUMDG..PGG] for the
 // stop test that follows the all-reduce (stage 12), instead of testing.
+// K2's epilogue rows per thread per batch (K2E; round 6: 4 -- C3's 3.8 rows
+// per thread fit one batch, C5's 19 run five at the speed of three of 8, and
+// the kernel drops from 124 to 86 VGPRs: C3 13.2k -> 13.4k it/s, C5 and the
+// 8-way C5 rank the same, tools/gpu_r06k.sh; A/B builds: BSLS_K2E.  Loading
+// the first batch's z indices and scales before the walk instead, to land
+// under it, measured no gain: 13.2k)
+#ifndef BSLS_K2E
+#define BSLS_K2E 4
+#endif
+
 // K2 of a stopped sharded run: the driver still all-reduces scal[SUMDG..RR]
 // after every K2 it enqueues, so the shard_role 2 ranks zero their copy and
 // the sum leaves role 1's -- the stop iteration's sums -- instead of world
@@ -589,7 +599,7 @@ __global__ __launch_bounds__(1024) void bb_k2t(bsls_bb_problem P, const double *
         // the batch in flight at once (two round trips per batch instead of
         // two per row: C5's 19 rows per thread made the epilogue ~90 us)
         const int64_t iend = (nloc < T.H) ? nloc : T.H;
-        constexpr int K2E = 8;
+        constexpr int K2E = BSLS_K2E;
         for (int64_t ib = threadIdx.x; ib < iend; ib += K2E * blockDim.x) {
             int32_t jq[K2E];
             double ca[K2E], cb[K2E], gq[K2E], dq[K2E];
