@@ -415,6 +415,16 @@ __global__ __launch_bounds__(1024, BSLS_K1T_WGS) void bb_k1t(bsls_bb_problem P, 
                            red);
 }
 
+// K2's epilogue rows per thread per batch (K2E; round 6: 4 -- C3's 3.8 rows
+// per thread fit one batch, C5's 19 run five at the speed of three of 8, and
+// the kernel drops from 124 to 86 VGPRs: C3 13.2k -> 13.4k it/s, C5 and the
+// 8-way C5 rank the same, tools/gpu_r06k.sh; A/B builds: BSLS_K2E.  Loading
+// the first batch's z indices and scales before the walk instead, to land
+// under it, measured no gain: 13.2k)
+#ifndef BSLS_K2E
+#define BSLS_K2E 4
+#endif
+
 // K2 on a tile image: w = A'r for row block rb (+ its halo row) in LDS, summed
 // over r's column groups (one group: in CSR order, bit-identical to SciPy;
 // several: partials in wpart, summed in group order by the block's last
@@ -436,16 +446,6 @@ __global__ __launch_bounds__(1024, BSLS_K1T_WGS) void bb_k1t(bsls_bb_problem P, 
 // rest), stored with the sums as scal[RR] for the all-reduce; the last
 // workgroup keeps iteration iter - 1's sums in scal[PSUMDG..PGG] for the
 // stop test that follows the all-reduce (stage 12), instead of testing.
-// K2's epilogue rows per thread per batch (K2E; round 6: 4 -- C3's 3.8 rows
-// per thread fit one batch, C5's 19 run five at the speed of three of 8, and
-// the kernel drops from 124 to 86 VGPRs: C3 13.2k -> 13.4k it/s, C5 and the
-// 8-way C5 rank the same, tools/gpu_r06k.sh; A/B builds: BSLS_K2E.  Loading
-// the first batch's z indices and scales before the walk instead, to land
-// under it, measured no gain: 13.2k)
-#ifndef BSLS_K2E
-#define BSLS_K2E 4
-#endif
-
 // K2 of a stopped sharded run: the driver still all-reduces scal[SUMDG..RR]
 // after every K2 it enqueues, so the shard_role 2 ranks zero their copy and
 // the sum leaves role 1's -- the stop iteration's sums -- instead of world
