@@ -51,6 +51,10 @@ for s in $STEPS; do
       timeout -k 10 900 python -u -m pytest $TESTS -m gpu -q --timeout 300 --timeout-method thread \
           > $OUT/gpu_tests.log 2>&1
       rc=$?; echo "alltests rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
+    driverlike)
+      # the driver's own arguments (BENCH_rNN: --steps 20 --warmup 5)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $OUT/bench_driverlike.log 2>&1
+      rc=$?; echo "driverlike rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
     legs)
       timeout -k 10 600 python bench.py --legs "${LEGS:-lbfgs}" > $OUT/bench_legs.log 2>&1
       rc=$?; echo "legs rc=$rc" | tee -a $OUT/status.txt; fatal $rc ;;
