@@ -416,3 +416,19 @@ def test_stored_value_codecs_vs_oracle(cuda, orc, codec, parity):
     N = orc.block_sizes_to_N(sh['block_sizes'])
     want = N.T.tocsr().dot(A.T.tocsr().dot(r))
     assert np.max(np.abs(got - want)) <= 1e-12 * np.max(np.abs(want))
+
+
+def test_sy_dr_retired(cuda, shard100k):
+    """bsls_bb_problem.sy_dr is reserved since round 6 (dz . dg from the
+    residuals moved the reference's exact-zero exit, BB.py:22): a nonzero
+    value is refused (BSLS_E_ARG) before anything is launched."""
+    from device import BBEngine
+    sh, b, _ = shard100k
+    eng = BBEngine(sh['A'], b, sh['block_sizes'], options={'max_iter': 3, 'opt_tol': 1e-30})
+    eng.set_z0(np.zeros(eng.nz))
+    eng.P.sy_dr = 1
+    with pytest.raises(ValueError):
+        eng.prologue()
+    eng.P.sy_dr = 0
+    eng.prologue()
+    eng.iterate(1, 3)

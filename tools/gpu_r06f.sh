@@ -2,6 +2,7 @@
 # round 6, step f: the exact projection on the pipelined layout -- the exact
 # projection tests (bit-identity vs the oracle), then the C2 leg A/B:
 # BSLS_PROJ_EXACT_PIPE=1 (new default) / 0 (the lane-per-block sorting kernel)
+# (the knob went with the kernel when it was reverted: commit 31d8bb5 holds both)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
