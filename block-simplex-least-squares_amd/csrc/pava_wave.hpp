@@ -177,7 +177,6 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
     const int depth = t - mycs;
     const double pr = s.Y * (double)s.W;
     double num = 0.0 + pr;
-    int den = s.W;
     // k = 1 .. the deepest pooled member (a ballot per step instead of a
     // six-round shuffle max up front: 2-4 steps are typical).  Every member
     // at depth >= k steps at k: after step k such a lane holds the left fold
@@ -193,15 +192,15 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
         const bool step = dk >= k;
         if (!ballot_b(step)) break;
         const double np = dpp_shr1_d(num);
-        const int dp = dpp_shr1_i(den);
-        if (step) {
-            num = np + pr;
-            den = dp + s.W;
-        }
+        if (step) num = np + pr;
     }
+    // the pooled length is the chain's element span (runs cover consecutive
+    // elements): the last run's end minus the head's first element -- no
+    // integer fold beside the value's (round 6: -7 VALU per pass)
     const double tn = shfl_d(num, last);
-    const int td = shfl_i(den, last);
+    const int tend = shfl_i(s.O + s.W, last);
     if (pool) {
+        const int td = tend - s.O;
         s.Y = tn / (double)td;
         s.W = td;
     }
