@@ -150,19 +150,25 @@ __device__ __forceinline__ WaveRuns wave_runs(double y, int L, uint64_t B, int o
 // pools, else the pooled chains merged and the survivors packed into lanes
 // 0 .. nh-1.  ys / ps / cst: this wave's 64 doubles / 64 ints / 65 ints of LDS.
 __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int *cst) {
-    // (predicates with bitwise operators: no branches, ballots straight from
-    // the compares; the scan counter is wave-uniform)
+    // (predicates with bitwise operators: no branches; the wave masks are
+    // combined from ballots of single compares with scalar ops -- a ballot of
+    // a compound predicate costs a v_cndmask and a v_cmp to rematerialise the
+    // mask the compares already left in SGPRs; the scan counter is
+    // wave-uniform)
     const int t = lane_id();
     const bool act = t < s.nh;
     const double yp = dpp_shr1_d(s.Y);
     const bool cs = act & ((s.BS != 0) | !(s.Y <= yp));   // lane 0 is always a block start
+    const uint64_t ACT = ballot_b(act);
+    const uint64_t CS = ACT & (ballot_b(s.BS != 0) | ballot_b(!(s.Y <= yp)));
     // every run starts a chain (the converged pack's check pass, usually):
     // no chain has two runs, so none pools -- leave before any LDS traffic
-    if (!ballot_b(act & !cs)) return false;
-    const uint64_t CS = ballot_b(cs);
+    if (!(ACT & ~CS)) return false;
     // chain c of this lane (lanes >= nh: the last chain, unused); the
-    // table holds every chain's first run, then nh
-    const int c = mbcnt64(CS) - (cs ? 0 : 1);
+    // table holds every chain's first run, then nh.  c = (chain starts at or
+    // below this lane) - 1 = the chain starts in [1, t], as lane 0 always
+    // starts one: the count of CS >> 1 below this lane
+    const int c = mbcnt64(CS >> 1);
     if (cs) cst[c] = t;
     if (t == 0) cst[__popcll(CS)] = s.nh;
     const int mycs = cst[c], nxt = cst[c + 1];
@@ -173,7 +179,7 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
     // y[i] != y[j]); every member sees both
     const bool inpool = act & (yfirst != ylast);
     const bool pool = cs & inpool;
-    if (!ballot_b(pool)) return false;
+    if (!(CS & ballot_b(yfirst != ylast))) return false;
     const int depth = t - mycs;
     const double pr = s.Y * (double)s.W;
     double num = 0.0 + pr;
@@ -192,7 +198,12 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
         const bool step = dk >= k;
         if (!ballot_b(step)) break;
         const double np = dpp_shr1_d(num);
-        if (step) num = np + pr;
+        if (step) {
+            // (the empty asm keeps this a masked add: if-converted, the
+            // update costs two v_cndmask per step)
+            num = np + pr;
+            asm volatile("" : "+v"(num));
+        }
     }
     // the pooled length is the chain's element span (runs cover consecutive
     // elements): the last run's end minus the head's first element -- no
@@ -206,7 +217,7 @@ __device__ __forceinline__ bool wave_pass(WaveRuns &s, double *ys, int *ps, int 
     }
     // pack the surviving runs into lanes 0 .. nh-1
     const bool surv = act & !(dk > 0);
-    const uint64_t S = ballot_b(surv);
+    const uint64_t S = ACT & ~ballot_b(dk > 0);
     if (surv) {
         const int idx = mbcnt64(S);
         ys[idx] = s.Y;
