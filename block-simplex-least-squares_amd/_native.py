@@ -203,6 +203,7 @@ _SIGS = {
     'bsls_comm_destroy': (_int, [_vp]),
     'bsls_comm_all_reduce': (_int, [_vp, _vp, _i64, _vp]),
     'bsls_comm_count': (_int, [_vp, ctypes.POINTER(_int)]),
+    'bsls_comm_force_collectives': (_int, [_vp, _int]),
     'bsls_bb_shard_iterate':(_int, [ctypes.POINTER(BBProblem), _vp, _i64, _i64, _int, _vp]),
     'bsls_bb_k2_part': (_int, [ctypes.POINTER(BBProblem), _i64, _int, _vp]),
     'bsls_bb_k1_rows': (_int, [ctypes.POINTER(BBProblem), _i64, _i64, _i64, _vp]),

@@ -74,6 +74,10 @@ constexpr int MAX_PARTS = 16;
 struct bsls_comm {
     ncclComm_t comm;
     int world, rank;
+    // run the collectives at world 1 too (bsls_comm_force_collectives): a
+    // one-rank RCCL sum is the identity, so the results stay those of the
+    // skipped form while every RCCL call of the loop executes
+    bool force;
     bsls_all_reduce_fn fn;   // set: the host callback replaces RCCL
     void *user;
     // a modelled exchange (bsls_comm_create_model): no data moves, a spin
@@ -203,6 +207,12 @@ extern "C" int bsls_comm_count(const bsls_comm *c, int *count_out) {
     return comm_rc(R.count(c->comm, count_out));
 }
 
+extern "C" int bsls_comm_force_collectives(bsls_comm *c, int on) {
+    if (!c || (on != 0 && on != 1)) return BSLS_E_ARG;
+    c->force = on != 0;
+    return BSLS_OK;
+}
+
 extern "C" int bsls_comm_all_reduce(bsls_comm *c, double *buf, int64_t count, void *stream) {
     if (!c || !buf || count < 0) return BSLS_E_ARG;
     return comm_sum(c, buf, (size_t)count, (hipStream_t)stream);
@@ -215,8 +225,9 @@ extern "C" int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *c, int
     hipStream_t st = (hipStream_t)stream;
     // a sum over one rank is the identity: a one-rank communicator (the
     // rehearsal of one rank's share on one GPU) skips the collectives, whose
-    // one-rank form is RCCL's own copies and flag fills (~17 us an iteration)
-    const bool comm = c->world > 1;
+    // one-rank form is RCCL's own copies and flag fills (~17 us an iteration),
+    // unless forced (bsls_comm_force_collectives)
+    const bool comm = c->world > 1 || c->force;
     auto all_reduce = [&](double *buf, size_t cnt) -> int {
         return comm ? comm_sum(c, buf, cnt, st) : BSLS_OK;
     };
@@ -293,7 +304,7 @@ extern "C" int bsls_bb_shard_iterate_parts(const bsls_bb_problem *p, bsls_comm *
         c->events = true;
     }
     hipStream_t st = (hipStream_t)stream, cs = (hipStream_t)comm_stream;
-    const bool comm = c->world > 1;
+    const bool comm = c->world > 1 || c->force;
     int rc;
     for (int64_t i = first_iter; i < first_iter + count; ++i) {
         // K2 by link parts: part q needs only its rows of r

@@ -428,9 +428,11 @@ class RcclComm:
     initialized torch.distributed group: rank 0 makes the RCCL id, a broadcast
     over the group hands it to the others, every rank joins on its current
     device.  In a torch process csrc/shard.hip resolves the RCCL torch loaded,
-    so both drive the same library."""
+    so both drive the same library.  force: the native driver runs its
+    collectives at world 1 too (bsls_comm_force_collectives; a one-rank sum is
+    the identity) -- every RCCL call of the loop executes on a one-GPU box."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force=False):
         import ctypes
         import torch
         import torch.distributed as dist
@@ -450,6 +452,8 @@ class RcclComm:
         h = ctypes.c_void_p()
         check(L.bsls_comm_create(raw, self.world, self.rank, ctypes.byref(h)), 'bsls_comm_create')
         self.handle = h
+        if force:
+            check(L.bsls_comm_force_collectives(h, 1), 'bsls_comm_force_collectives')
 
     def count(self):
         """The ranks RCCL says this communicator spans (ncclCommCount)."""

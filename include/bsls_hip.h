@@ -536,6 +536,12 @@ int bsls_comm_count(const bsls_comm *comm, int *count_out);
 typedef int (*bsls_all_reduce_fn)(double *d_buf, int64_t count, void *stream, void *user);
 int bsls_comm_create_callback(int world, int rank, bsls_all_reduce_fn fn, void *user,
                               bsls_comm **out);
+/* on = 1: bsls_bb_shard_iterate[_parts] run their collectives at world 1 as
+ * well (a one-rank sum is the identity, so the results do not change; every
+ * RCCL call of the loop -- the five-sum, the r exchange, int64 under a
+ * fixed-point r, the parts' exchanges on comm_stream -- then executes on a
+ * one-GPU box).  0 (the default): a one-rank communicator skips them. */
+int bsls_comm_force_collectives(bsls_comm *comm, int on);
 /* in-place sum of `count` doubles over the ranks, on `stream` */
 int bsls_comm_all_reduce(bsls_comm *comm, double *d_buf, int64_t count, void *stream);
 /* Iterations first_iter .. first_iter+count-1 of the sharded schedule (fuse 2:
@@ -544,7 +550,8 @@ int bsls_comm_all_reduce(bsls_comm *comm, double *d_buf, int64_t count, void *st
  * all-reduce r; fuse 0: stage 3 instead of 8 and a stage 9 after every r
  * exchange; stage 9 after the last iteration in all three).  p->shard_role
  * must be 1 on rank 0 and 2 elsewhere (target added once).  A one-rank
- * communicator skips the collectives (a sum over one rank).  All on
+ * communicator skips the collectives (a sum over one rank) unless
+ * bsls_comm_force_collectives turned them on.  All on
  * `stream`; nothing waits on the host. */
 int bsls_bb_shard_iterate(const bsls_bb_problem *p, bsls_comm *comm, int64_t first_iter,
                           int64_t count, int fuse, void *stream);
