@@ -648,7 +648,8 @@ def build_problem(name, world, rank, dist, shard_of=None):
     return sh, b
 
 
-def build_engine(sh, b, world, dist, parts, sharded=False, slices=None, model=None):
+def build_engine(sh, b, world, dist, parts, sharded=False, slices=None, model=None,
+                 force_comm=False):
     """(engine, run(first, count)) for one rank: the fused single-GPU loop, or
     the column-sharded stages with the RCCL all-reduces (distributed.ShardedBB;
     `sharded` forces them at world 1 -- the per-rank host and launch path of
@@ -656,7 +657,9 @@ def build_engine(sh, b, world, dist, parts, sharded=False, slices=None, model=No
     behind both walks (link parts, bsls_bb_shard_iterate_parts).  model
     (us_per_mb, fixed_us), rehearsal only: every exchange a spin of that cost
     on its stream instead of the skipped one-rank collectives
-    (distributed.ModelComm) -- how much of such an exchange the schedule hides."""
+    (distributed.ModelComm) -- how much of such an exchange the schedule hides.
+    force_comm: an RCCL communicator that runs its collectives at world 1 too
+    (bsls_comm_force_collectives: the one-rank self-check of the transport)."""
     import torch
     from device import BBEngine
     opts = {'max_iter': 10 ** 12, 'opt_tol': 1e-30}
@@ -685,7 +688,7 @@ def build_engine(sh, b, world, dist, parts, sharded=False, slices=None, model=No
         comm = ModelComm(slices or 1, 0, fixed_us=model[1], us_per_mb=model[0])
     elif os.environ.get('BSLS_SHARD_NATIVE', '1') != '0' and dist.get_backend() == 'nccl':
         from distributed import RcclComm
-        comm = RcclComm()
+        comm = RcclComm(force=force_comm)
     elif os.environ.get('BSLS_SHARD_NATIVE', '1') != '0' and world > 1:
         # another backend (the gloo rehearsal of N ranks on one GPU): the same
         # native loop, its all-reduces through torch.distributed callbacks
@@ -842,7 +845,7 @@ def host_info(threads):
 
 
 LEGS = ('main', 'c5', 'c3sv', 'proj', 'iso', 'xspace', 'md', 'dore', 'lbfgs', 'gdlbfgs', 'c1',
-        'cpu')
+        'cpu', 'rccl1')
 
 
 def traffic_file():
@@ -892,7 +895,7 @@ def selfcheck_verdict(got, ref, tol):
     return err, bool(np.isfinite(err) and err <= tol)
 
 
-def selfcheck_sharded(world, rank, dist, parts=1, problem=None):
+def selfcheck_sharded(world, rank, dist, parts=1, problem=None, force=False):
     """Before any timing at N > 1: a column-sharded BB problem through the
     shipped transport -- RcclComm + bsls_bb_shard_iterate under nccl (the
     five-sum and the int64 fixed-point r all-reduces of every iteration), the
@@ -900,7 +903,10 @@ def selfcheck_sharded(world, rank, dist, parts=1, problem=None):
     ranks' z slices gathered and compared on rank 0 with the oracle's
     trajectory of the whole problem (python/BB.py:7-45 over main.py:53-65).
     The oracle is the check leg only, outside every timed region.  Returns the
-    line's fields on every rank (the verdict broadcast from rank 0)."""
+    line's fields on every rank (the verdict broadcast from rank 0).  force
+    (N = 1, leg rccl1): the sharded driver on one nccl rank with its RCCL
+    collectives forced on (a one-rank sum is the identity), so the N = 1 line
+    shows the transport's calls executing against the oracle as well."""
     import torch
     from synthetic import make_partitioned, add_noise, SEED
     c = dict(SELFCHECK, **(problem or {}))
@@ -910,7 +916,7 @@ def selfcheck_sharded(world, rank, dist, parts=1, problem=None):
         Ax = torch.from_numpy(sh['Ax']).cuda()
         dist.all_reduce(Ax)
         b = add_noise(Ax.cpu().numpy(), 0.02, seed=SEED)
-        eng, run = build_engine(sh, b, world, dist, parts)
+        eng, run = build_engine(sh, b, world, dist, parts, sharded=force, force_comm=force)
     comm = getattr(eng, '_comm', None)
     run(1, c['iters'])
     torch.cuda.synchronize()
@@ -920,7 +926,7 @@ def selfcheck_sharded(world, rank, dist, parts=1, problem=None):
             'rccl_ranks': comm.count() if hasattr(comm, 'count') else None,
             'r_fixed_point': bool(float(eng.P.r_fx) > 0),
             'k1_groups': int(eng.A_til.img['ngroups']) if eng.A_til is not None else None,
-            'formats': [eng.fmt_A, eng.fmt_AT]}
+            'formats': [eng.fmt_A, eng.fmt_AT], 'collectives_forced': bool(force)}
     if comm is not None:
         comm.close()
     del eng, run
@@ -1233,6 +1239,29 @@ def extras(args, legs, out, tfile):
                                     'loop in C + OpenMP (oracle/bsls_cpu_bb.c)' % (ait, ael),
                           'host': host_info(HOST_THREADS)}}
         log('CPU baseline done')
+    if 'rccl1' in legs:
+        out['rccl_forced_selfcheck'] = rccl_forced_selfcheck()
+        log('RCCL one-rank self-check done')
+
+
+def rccl_forced_selfcheck():
+    """The N > 1 self-check's problem through RcclComm + bsls_bb_shard_iterate
+    on a one-rank nccl group with the collectives forced on (every
+    ncclAllReduce of the shipped loop runs: the five-sum in doubles, the r
+    exchange in int64 words), z against the oracle -- the RCCL transport
+    exercised on the one-GPU box, outside every timed region."""
+    import torch
+    import torch.distributed as dist
+    for k, v in (('MASTER_ADDR', '127.0.0.1'), ('MASTER_PORT', '29547')):
+        os.environ.setdefault(k, v)
+    with _StdoutToStderr():
+        dist.init_process_group('nccl', rank=0, world_size=1,
+                                device_id=torch.device('cuda', torch.cuda.current_device()))
+    try:
+        res = selfcheck_sharded(1, 0, dist, force=True)
+    finally:
+        dist.destroy_process_group()
+    return res
 
 
 if __name__ == '__main__':
