@@ -1240,7 +1240,12 @@ def extras(args, legs, out, tfile):
                           'host': host_info(HOST_THREADS)}}
         log('CPU baseline done')
     if 'rccl1' in legs:
-        out['rccl_forced_selfcheck'] = rccl_forced_selfcheck()
+        # (an extra of the N = 1 line: a failure here is reported in the line,
+        # it does not take the measured legs with it)
+        try:
+            out['rccl_forced_selfcheck'] = rccl_forced_selfcheck()
+        except Exception as exc:
+            out['rccl_forced_selfcheck'] = {'ok': False, 'error': repr(exc)[:400]}
         log('RCCL one-rank self-check done')
 
 
