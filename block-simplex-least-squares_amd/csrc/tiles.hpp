@@ -163,17 +163,6 @@ __device__ __forceinline__ uint32_t tri_entry(const tile_tri &t, int j) {
 #ifndef BSLS_TILE_D
 #define BSLS_TILE_D 1
 #endif
-// The dealt walk's gathers are buffer loads: 32-bit byte offsets from the
-// group's first column through one scalar resource, instead of 64-bit
-// addresses (round 6, tools/gpu_r06x.sh, profiles/r06_gather_buffer_ab.txt:
-// C3 13.47k -> 13.58k it/s, C5 1284 -> 1294, the 8-way C5 rank 147.8 ->
-// 146.7 us; with the nt policy bit (BSLS_TILE_GAUX=2) the walks run ~1.3-1.9x
-// slower, sc0 (1) as 0).  A gathered range past 2 GB of offsets keeps the
-// global loads (GB = false).  BSLS_TILE_GAUX: the loads' cache-policy word, -1
-// global loads everywhere (A/B builds).
-#ifndef BSLS_TILE_GAUX
-#define BSLS_TILE_GAUX 0
-#endif
 template <bool PK3>
 struct TileEnt {
     typedef tile_quad type;
@@ -265,7 +254,7 @@ __device__ __forceinline__ double fx_value(const double *rows, int lr, int lo_of
 // bsls_bb_problem.r_fx): each gathered word is an int64, its value that times
 // fxin (the inverse scale)
 template <int MODE, bool NT, bool PK3 = false, int VT = 0, int P = BSLS_TILE_P,
-          int D = BSLS_TILE_D, bool FX = false, bool FXIN = false, bool GB = false>
+          int D = BSLS_TILE_D, bool FX = false, bool FXIN = false>
 __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb, int64_t g,
                                                 const double *__restrict__ src, double *rows,
                                                 const double *rcol, double fxs = 1.0,
@@ -307,22 +296,11 @@ __device__ __forceinline__ void tile_walk_dealt(const bsls_tiles &T, int64_t rb,
     // v[d] / a[d]: the gathered values (and stored values) of step s + d
     double v[D + 1][4], a[D + 1][4];
     double ko = 0.0;
-    // (GB: the caller checked that the group's columns span < 2 GB of offsets)
-    const int64_t gbytes = (T.cols - T.group_col[g]) * 8;
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)xb, 0, (int)(gbytes < 0x7FFFFFFF ? gbytes : 0x7FFFFFFF), 0x00020000);
-    auto gx = [&](int32_t i) -> double {
-        if constexpr (GB)
-            return __builtin_bit_cast(
-                double, __builtin_amdgcn_raw_buffer_load_b64(xr, i * 8, 0,
-                                                             BSLS_TILE_GAUX < 0 ? 0 : BSLS_TILE_GAUX));
-        else return xb[i];
-    };
     auto gat = [&](const ent_t &u, const int4 &b, int64_t q, double (&o)[4], double (&w)[4]) {
-        o[0] = gx(b.x + (int32_t)(ent(u, 0) & cmask));
-        o[1] = gx(b.y + (int32_t)(ent(u, 1) & cmask));
-        o[2] = gx(b.z + (int32_t)(ent(u, 2) & cmask));
-        o[3] = gx(b.w + (int32_t)(ent(u, 3) & cmask));
+        o[0] = xb[b.x + (ent(u, 0) & cmask)];
+        o[1] = xb[b.y + (ent(u, 1) & cmask)];
+        o[2] = xb[b.z + (ent(u, 2) & cmask)];
+        o[3] = xb[b.w + (ent(u, 3) & cmask)];
         if (MODE == 1) tile_vals4<VT, NT>(T.val, v0 + q * 4096, w);
     };
     // (FXIN: the int64 words to doubles where used, not where gathered, so
@@ -380,25 +358,6 @@ __device__ __forceinline__ void tile_walk_dealt_vt(const bsls_tiles &T, int64_t 
                                                    const double *rcol, double fxs = 1.0,
                                                    double fxin = 1.0) {
     constexpr int P = BSLS_TILE_P, D = BSLS_TILE_D;
-    // gathers by buffer loads while the offsets fit (every image of the
-    // configs: C5's 10M x columns are 80 MB)
-    if (BSLS_TILE_GAUX >= 0 && (T.cols - T.group_col[g]) * 8 <= (int64_t)0x7FFFFFFF) {
-        if constexpr (MODE == 1) {
-            if (T.layout & BSLS_TILE_VAL16)
-                tile_walk_dealt<MODE, NT, PK3, 2, P, D, FX, FXIN, true>(T, rb, g, src, rows, rcol,
-                                                                        fxs, fxin);
-            else if (T.layout & BSLS_TILE_VAL32)
-                tile_walk_dealt<MODE, NT, PK3, 1, P, D, FX, FXIN, true>(T, rb, g, src, rows, rcol,
-                                                                        fxs, fxin);
-            else
-                tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX, FXIN, true>(T, rb, g, src, rows, rcol,
-                                                                        fxs, fxin);
-        } else {
-            tile_walk_dealt<MODE, NT, PK3, 0, P, D, FX, FXIN, true>(T, rb, g, src, rows, rcol, fxs,
-                                                                    fxin);
-        }
-        return;
-    }
     if constexpr (MODE == 1) {
         if (T.layout & BSLS_TILE_VAL16)
             tile_walk_dealt<MODE, NT, PK3, 2, P, D, FX, FXIN>(T, rb, g, src, rows, rcol, fxs, fxin);
